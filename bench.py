@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Benchmark of the go-dsp hot path on MI355X (BASELINE.json metric:
+"Gsamples/s + % HBM roofline, batched N=4096 complex128 FFT at 1/2/4/8 GPUs").
+
+A step = one batched transform over one HBM-resident batch of synthetic
+input (configs[1]: N = 4096 complex128 x 65536 rows per GPU). Multi-GPU: one
+process per GPU (torch.distributed.run), each rank transforms its own
+65536-row shard (weak scaling, no data-path collective: the rows are
+independent). value = samples of all ranks / max-over-ranks wall time.
+
+Other workloads (--workload): bluestein3000, fft2_8192, pwelch (the other
+BASELINE configs; pwelch uses one RCCL all-reduce of the PSD accumulators).
+
+roofline.achieved = algorithmic bytes of one launch (32 B/sample: 16 B read +
+16 B written) / the launch's average duration, measured with
+HIP events on the stream the kernel runs on. roofline.traffic = HBM bytes per
+launch from the committed rocprofv3 PMC summary (profiles/), or null.
+cpu_baseline = the reference algorithm's CPU restatement (oracle/, test
+infrastructure) with the reference's worker-pool structure, timed on a bounded
+row sample on rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+SEED = 0x5EED
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="radix4096",
+                    choices=["radix4096", "bluestein3000", "fft2_8192", "pwelch"])
+    ap.add_argument("--batch", type=int, default=0, help="rows per GPU (0 = config default)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="target CPU seconds for the cpu_baseline sample (0 disables)")
+    ap.add_argument("--check-rows", type=int, default=8, help="rows checked against the oracle")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    gdsp = importlib.import_module("go-dsp_amd")
+    D = importlib.import_module("go-dsp_amd.device")
+    stream = torch.cuda.Stream(dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    w = args.workload
+    if w in ("radix4096", "bluestein3000"):
+        n = 4096 if w == "radix4096" else 3000
+        batch = args.batch or 65536
+        x = torch.empty((batch, n), dtype=torch.complex128, device=dev)
+        y = torch.empty_like(x)
+        D.fill_uniform(x, SEED, offset=rank * batch * n * 2, stream=stream)
+
+        def step():
+            D.fft_batch(x, y, stream=stream)
+
+        samples_per_step = batch * n
+        alg_bytes = 32 * samples_per_step
+        cfg = {"workload": f"fft.FFT batched complex128 N={n} x {batch} rows per GPU",
+               "n": n, "batch_per_gpu": batch, "parallelism": f"shard{world}"}
+        kernel = "fft_lds_kernel<12>" if n == 4096 else "bluestein_kernel<13>"
+        metric = "Gsamples/s + % HBM roofline, batched N=4096 complex128 FFT at 1/2/4/8 GPUs"
+    elif w == "fft2_8192":
+        rows = cols = 8192
+        x = torch.empty((rows, cols), dtype=torch.complex128, device=dev)
+        y = torch.empty_like(x)
+        work = torch.empty_like(x)
+        D.fill_uniform(x, SEED, offset=rank * rows * cols * 2, stream=stream)
+
+        def step():
+            D.fft2(x, y, work=work, stream=stream)
+
+        samples_per_step = rows * cols
+        alg_bytes = 2 * 2 * 16 * samples_per_step
+        cfg = {"workload": "fft.FFT2 complex128 8192x8192", "rows": rows, "cols": cols,
+               "parallelism": f"replicas{world}"}
+        kernel = "fft2 (all launches)"
+        metric = "Gsamples/s, fft.FFT2 8192x8192 complex128"
+    else:  # pwelch: 2^30 samples total, NFFT 4096, 50 % overlap, Hann
+        nfft, nov = 4096, 2048
+        stride = nfft - nov
+        total = 1 << 30
+        nseg_total = (total - nfft) // stride + 1
+        lo = nseg_total * rank // world
+        hi = nseg_total * (rank + 1) // world
+        s0 = lo * stride
+        nloc = (hi - 1 - lo) * stride + nfft
+        x = torch.empty(nloc, dtype=torch.float64, device=dev)
+        D.fill_uniform(x, SEED, offset=s0, stream=stream)
+        win = torch.tensor(gdsp.window.Hann(nfft), dtype=torch.float64, device=dev)
+        acc = torch.zeros(nfft, dtype=torch.float64, device=dev)
+
+        def step():
+            acc.zero_()
+            D.pwelch_accumulate(x, nfft, nfft, nov, 0, hi - lo, win, acc, stream=stream)
+            if world > 1:
+                with torch.cuda.stream(stream):
+                    dist.all_reduce(acc)
+
+        samples_per_step = (hi - lo) * stride  # new samples per GPU
+        alg_bytes = 8 * nloc
+        cfg = {"workload": "spectral.Pwelch 2^30 samples, Hann NFFT 4096, 50% overlap",
+               "segments_total": nseg_total, "parallelism": f"shard{world}+allreduce"}
+        kernel = "pwelch_kernel<12>"
+        metric = "Gsamples/s, spectral.Pwelch 2^30 samples NFFT 4096"
+
+    torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        step()
+        ends[i].record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ev_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    avg_launch_s = sum(ev_ms) / len(ev_ms) / 1e3
+
+    # parity spot check of this run's output (untimed)
+    check = None
+    if rank == 0 and args.check_rows > 0 and w in ("radix4096", "bluestein3000"):
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import numpy as np
+        import oracle
+        rows = np.linspace(0, y.shape[0] - 1, args.check_rows).astype(int)
+        xs = x[rows].cpu().numpy()
+        ys = y[rows].cpu().numpy()
+        ref = oracle.fft_rows(xs)
+        err = max(float(np.linalg.norm(a - b) / np.linalg.norm(b)) for a, b in zip(ys, ref))
+        check = {"rows": len(rows), "max_nrel_vs_oracle": err}
+
+    total_samples = samples_per_step * args.steps * world
+    value = total_samples / elapsed / 1e9
+    achieved = alg_bytes / avg_launch_s / 1e9
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", f"pmc_{w}.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0 and w in ("radix4096", "bluestein3000"):
+        cpu = cpu_baseline(n, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": metric,
+            "value": round(value, 3),
+            "unit": "Gsamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64 (complex128)",
+            "data": "synthetic (splitmix64 uniform[-1,1), generated in HBM)",
+            "config": cfg,
+            "roofline": {"bound": "hbm", "kernel": kernel,
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                         "alg_bytes_per_launch": alg_bytes, "traffic": traffic},
+            "cpu_baseline": cpu,
+            "parity": check,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(n: int, seconds: float):
+    """Reference algorithm (oracle/ restatement of fft/radix2.go +
+    fft/bluestein.go) with the reference's per-call worker pool of nworkers
+    threads (radix2.go:89-151), one fft.FFT call per row, on a bounded row
+    sample of the same synthetic workload."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+    import oracle
+    cores = min(os.cpu_count() or 1, 16)  # the GPU box's CPU share is 16
+    rows = 64
+    x = oracle.fill_uniform(2 * n * rows, SEED).view(np.complex128).reshape(rows, n)
+    done = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        if n & (n - 1) == 0:
+            oracle.fft_rows_threaded(x, cores)
+        else:
+            oracle.fft_rows(x)
+        done += rows
+    dt = time.perf_counter() - t0
+    threaded = n & (n - 1) == 0
+    return {"value": round(done * n / dt / 1e9, 6), "unit": "Gsamples/s",
+            "cores": cores if threaded else 1, "kind": "port",
+            "sample": f"{done} rows x N={n} ({dt:.1f} s), fft.FFT per row, "
+                      f"{'reference worker pool of ' + str(cores) + ' threads' if threaded else 'single thread (Bluestein path is serial in the reference)'}"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,253 @@
+// fft_device.hpp — gfx950 device building blocks for the go-dsp FFT engine:
+// complex128 arithmetic, in-register radix-2/4/8/16 DFTs, the Stockham pass
+// (register twiddle + DFT) and the LDS exchange between passes.
+//
+// Algorithm (replaces fft/radix2.go:80-154, the iterative radix-2 DIT with a
+// bit-reversal copy): a Stockham autosort FFT, radix 16 per pass, so N = 4096
+// needs 3 passes (vs 12 radix-2 stages) and no bit-reversal: pass p with
+// radix R and Ns = product of earlier radices maps butterfly j to inputs
+// j + r*N/R and outputs (j/Ns)*Ns*R + j%Ns + r*Ns, with twiddle
+// W_{Ns*R}^{(j%Ns)*r}. Each thread owns E (<=16) elements at t + k*T, so the
+// first load and the last store are fully coalesced 16-byte-per-lane streams.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gdsp {
+
+struct __attribute__((aligned(16))) cd {
+  double x, y;
+};
+
+__device__ __forceinline__ cd operator+(cd a, cd b) { return {a.x + b.x, a.y + b.y}; }
+__device__ __forceinline__ cd operator-(cd a, cd b) { return {a.x - b.x, a.y - b.y}; }
+__device__ __forceinline__ cd cmul(cd a, cd b) {
+  return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
+}
+__device__ __forceinline__ cd conjg(cd a) { return {a.x, -a.y}; }
+
+// cos/sin(pi/8) and sqrt(2)/2 to double precision
+#define GDSP_C8 0.92387953251128675613
+#define GDSP_S8 0.38268343236508977173
+#define GDSP_R2 0.70710678118654752440
+
+// x * exp(-2*pi*i*m/16): forward-direction twiddle by a multiple of 2*pi/16.
+// m is a compile-time constant once the callers' loops are unrolled, so the
+// switch folds to the special case (free for multiples of 90 degrees, 2 mul
+// for odd multiples of 45 degrees).
+__device__ __forceinline__ cd rot16(cd x, int m) {
+  switch (m & 15) {
+    case 0: return x;
+    case 4: return {x.y, -x.x};
+    case 8: return {-x.x, -x.y};
+    case 12: return {-x.y, x.x};
+    case 2: return {GDSP_R2 * (x.x + x.y), GDSP_R2 * (x.y - x.x)};
+    case 6: return {GDSP_R2 * (x.y - x.x), -GDSP_R2 * (x.x + x.y)};
+    case 10: return {-GDSP_R2 * (x.x + x.y), GDSP_R2 * (x.x - x.y)};
+    case 14: return {GDSP_R2 * (x.x - x.y), GDSP_R2 * (x.x + x.y)};
+    default: break;
+  }
+  // odd m: w = c - i s with c = cos(2 pi m/16), s = sin(2 pi m/16)
+  double c, s;
+  switch (m & 15) {
+    case 1: c = GDSP_C8; s = GDSP_S8; break;
+    case 3: c = GDSP_S8; s = GDSP_C8; break;
+    case 5: c = -GDSP_S8; s = GDSP_C8; break;
+    case 7: c = -GDSP_C8; s = GDSP_S8; break;
+    case 9: c = -GDSP_C8; s = -GDSP_S8; break;
+    case 11: c = -GDSP_S8; s = -GDSP_C8; break;
+    case 13: c = GDSP_S8; s = -GDSP_C8; break;
+    default: c = GDSP_C8; s = -GDSP_S8; break;  // 15
+  }
+  return {x.x * c + x.y * s, x.y * c - x.x * s};
+}
+
+// In-register forward DFT of size R (natural order in, natural order out).
+template <int R>
+struct Dft;
+
+template <>
+struct Dft<1> {
+  __device__ __forceinline__ static void run(cd (&)[1]) {}
+};
+
+template <>
+struct Dft<2> {
+  __device__ __forceinline__ static void run(cd (&a)[2]) {
+    cd t = a[0];
+    a[0] = t + a[1];
+    a[1] = t - a[1];
+  }
+};
+
+template <>
+struct Dft<4> {
+  __device__ __forceinline__ static void run(cd (&a)[4]) {
+    cd t0 = a[0] + a[2], t1 = a[0] - a[2];
+    cd t2 = a[1] + a[3], d = a[1] - a[3];
+    cd t3 = {d.y, -d.x};  // (a1 - a3) * (-i)
+    a[0] = t0 + t2;
+    a[1] = t1 + t3;
+    a[2] = t0 - t2;
+    a[3] = t1 - t3;
+  }
+};
+
+// R = R1*R2 split: n = R2*n1 + n2, k = k1 + R1*k2.
+template <int R1, int R2>
+__device__ __forceinline__ void dft_split(cd (&a)[R1 * R2]) {
+  constexpr int R = R1 * R2;
+  cd y[R2][R1];
+#pragma unroll
+  for (int n2 = 0; n2 < R2; ++n2) {
+    cd tmp[R1];
+#pragma unroll
+    for (int n1 = 0; n1 < R1; ++n1) tmp[n1] = a[R2 * n1 + n2];
+    Dft<R1>::run(tmp);
+#pragma unroll
+    for (int k1 = 0; k1 < R1; ++k1) y[n2][k1] = rot16(tmp[k1], n2 * k1 * (16 / R));
+  }
+#pragma unroll
+  for (int k1 = 0; k1 < R1; ++k1) {
+    cd tmp[R2];
+#pragma unroll
+    for (int n2 = 0; n2 < R2; ++n2) tmp[n2] = y[n2][k1];
+    Dft<R2>::run(tmp);
+#pragma unroll
+    for (int k2 = 0; k2 < R2; ++k2) a[k1 + R1 * k2] = tmp[k2];
+  }
+}
+
+template <>
+struct Dft<8> {
+  __device__ __forceinline__ static void run(cd (&a)[8]) { dft_split<4, 2>(a); }
+};
+template <>
+struct Dft<16> {
+  __device__ __forceinline__ static void run(cd (&a)[16]) { dft_split<4, 4>(a); }
+};
+
+// ---------------------------------------------------------------------------
+// Geometry of the one-kernel (LDS-resident) transform of N = 2^LOG2N points.
+template <int LOG2N>
+struct Geo {
+  static constexpr int N = 1 << LOG2N;
+  static constexpr int E = N < 16 ? N : 16;       // elements per thread
+  static constexpr int T = N / E;                 // threads per transform
+  static constexpr int WG = T >= 256 ? T : 256;   // threads per workgroup
+  static constexpr int TPW = WG / T;              // transforms per workgroup
+  static constexpr int NP16 = LOG2N >= 4 ? LOG2N / 4 : 0;
+  static constexpr int REM = LOG2N >= 4 ? LOG2N % 4 : LOG2N;
+  static constexpr int NPASS = NP16 + (REM ? 1 : 0);
+  static constexpr int STRIDE = N + N / 16;       // padded doubles per transform
+  static constexpr int LDS_DOUBLES = NPASS > 1 ? TPW * STRIDE : 1;
+  __host__ __device__ static constexpr int radix(int p) { return p < NP16 ? 16 : (1 << REM); }
+  __host__ __device__ static constexpr int ns(int p) { return p == 0 ? 1 : ns(p - 1) * radix(p - 1); }
+};
+
+// one padding slot every 16 doubles keeps the stride-16 writes of pass 0
+// conflict-free for ds_write_b64 (bank = (addr/4) mod 32 per 16-lane group)
+__device__ __forceinline__ int padi(int i) { return i + (i >> 4); }
+
+// Twiddle + DFT of one Stockham pass on the thread's registers. v[b + r*B]
+// holds input r of butterfly j = t + b*T. tw: forward table T_N[k] =
+// exp(-2 pi i k/N).
+template <int N, int E, int T, int R, int NS>
+__device__ __forceinline__ void pass_compute(cd (&v)[E], int t, const cd *__restrict__ tw) {
+  constexpr int B = E / R;
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    const int j = t + b * T;
+    cd u[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) u[r] = v[b + r * B];
+    if constexpr (NS > 1) {
+      // W_{NS*R}^{(j%NS)*r}: one table read, powers by two interleaved
+      // recurrences (odd and even exponents) to keep the product depth ~R/2
+      const cd w = tw[(j & (NS - 1)) * (N / (NS * R))];
+      u[1] = cmul(u[1], w);
+      if constexpr (R > 2) {
+        const cd w2 = cmul(w, w);
+        cd wo = w, we = w2;
+        u[2] = cmul(u[2], w2);
+#pragma unroll
+        for (int r = 3; r < R; ++r) {
+          if (r & 1) {
+            wo = cmul(wo, w2);
+            u[r] = cmul(u[r], wo);
+          } else {
+            we = cmul(we, w2);
+            u[r] = cmul(u[r], we);
+          }
+        }
+      }
+    }
+    Dft<R>::run(u);
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[b + r * B] = u[r];
+  }
+}
+
+// Stockham exchange through LDS after pass (R, NS): output r of butterfly j
+// goes to (j/NS)*NS*R + j%NS + r*NS, then every thread reads back t + k*T.
+// SPLIT: real and imaginary halves go through one N-double buffer in turn
+// (half the LDS, two more barriers); otherwise two buffers.
+template <int N, int E, int T, int R, int NS, bool SPLIT>
+__device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, double *lim,
+                                              bool first) {
+  constexpr int B = E / R;
+  int dst[E];
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    const int j = t + b * T;
+    const int base = (j / NS) * (NS * R) + (j & (NS - 1));
+#pragma unroll
+    for (int r = 0; r < R; ++r) dst[b + r * B] = padi(base + r * NS);
+  }
+  if (!first) __syncthreads();
+  if constexpr (SPLIT) {
+#pragma unroll
+    for (int k = 0; k < E; ++k) lre[dst[k]] = v[k].x;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < E; ++k) v[k].x = lre[padi(t + k * T)];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < E; ++k) lre[dst[k]] = v[k].y;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < E; ++k) v[k].y = lre[padi(t + k * T)];
+  } else {
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+      lre[dst[k]] = v[k].x;
+      lim[dst[k]] = v[k].y;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < E; ++k) v[k] = {lre[padi(t + k * T)], lim[padi(t + k * T)]};
+  }
+}
+
+// Full forward FFT of the thread's registers (natural order t + k*T in and
+// out). The final pass needs no exchange: its outputs already sit at t + k*T.
+template <int LOG2N, bool SPLIT, int P = 0>
+__device__ __forceinline__ void fft_regs(cd (&v)[Geo<LOG2N>::E], int t,
+                                         const cd *__restrict__ tw, double *lre, double *lim,
+                                         bool first_exchange = true) {
+  using G = Geo<LOG2N>;
+  if constexpr (P < G::NPASS) {
+    constexpr int R = G::radix(P);
+    constexpr int NS = G::ns(P);
+    if constexpr (P > 0) {
+      // exchange after the previous pass
+      constexpr int RP = G::radix(P - 1);
+      constexpr int NSP = G::ns(P - 1);
+      pass_exchange<G::N, G::E, G::T, RP, NSP, SPLIT>(v, t, lre, lim, first_exchange && P == 1);
+    }
+    pass_compute<G::N, G::E, G::T, R, NS>(v, t, tw);
+    fft_regs<LOG2N, SPLIT, P + 1>(v, t, tw, lre, lim, first_exchange);
+  }
+}
+
+}  // namespace gdsp

@@ -1,0 +1,582 @@
+// fft_kernels.hip — gfx950 kernels of the go-dsp FFT engine and their host
+// launchers (declared in launch.hpp). See DESIGN.md for the roofline of each.
+//
+//   fft_lds_kernel       one launch, one HBM read + one HBM write per
+//                        transform, power-of-2 N <= 16384 (fft/radix2.go:80-154,
+//                        fft/fft.go:35-52 for the inverse)
+//   stockham_global_pass multi-launch power-of-2 N > 16384 (radix-16 passes
+//                        through HBM)
+//   bluestein_kernel     fused chirp-z: premultiply, FFT_M, x FFT_M(b), IFFT_M,
+//                        postmultiply in one launch (fft/bluestein.go:68-94 with
+//                        Convolve fft/fft.go:55-69), M <= 16384
+//   pwelch_kernel        fused window + two-real-segments-per-complex FFT +
+//                        |X|^2 accumulation (spectral/pwelch.go:104-122)
+//   transpose / elementwise helpers for FFT2 (fft/fft.go:123-154) and for the
+//   composed Bluestein / materialised Pwelch paths.
+#include "fft_device.hpp"
+#include "launch.hpp"
+
+namespace gdsp {
+
+// ----------------------------------------------------------------------------
+// One-kernel transform: each workgroup owns TPW whole transforms in registers
+// (16 complex128 per thread) and LDS (exchange between radix-16 passes).
+template <int LOG2N, bool INV, int LOAD, bool SPLIT>
+__global__ __launch_bounds__(Geo<LOG2N>::WG) void fft_lds_kernel(
+    const void *__restrict__ in, cd *__restrict__ out, int64_t batch,
+    const cd *__restrict__ tw, double scale) {
+  using G = Geo<LOG2N>;
+  __shared__ double lds[(SPLIT ? 1 : 2) * G::LDS_DOUBLES];
+  const int lt = threadIdx.x;
+  const int slot = lt / G::T;
+  const int t = lt & (G::T - 1);
+  const int64_t g = (int64_t)blockIdx.x * G::TPW + slot;
+  const bool valid = g < batch;
+  double *lre = lds + slot * G::STRIDE;
+  double *lim = SPLIT ? lre : lds + G::LDS_DOUBLES + slot * G::STRIDE;
+  cd v[G::E];
+  if (valid) {
+    if constexpr (LOAD == LOAD_COMPLEX) {
+      const cd *src = reinterpret_cast<const cd *>(in) + g * G::N;
+#pragma unroll
+      for (int k = 0; k < G::E; ++k) {
+        v[k] = src[t + k * G::T];
+        if constexpr (INV) v[k].y = -v[k].y;
+      }
+    } else {
+      const double *src = reinterpret_cast<const double *>(in) + g * G::N;
+#pragma unroll
+      for (int k = 0; k < G::E; ++k) v[k] = {src[t + k * G::T], 0.0};
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < G::E; ++k) v[k] = {0.0, 0.0};
+  }
+  fft_regs<LOG2N, SPLIT>(v, t, tw, lre, lim);
+  if (valid) {
+    cd *dst = out + g * G::N;
+#pragma unroll
+    for (int k = 0; k < G::E; ++k) {
+      cd o = v[k];
+      if constexpr (INV) o = {o.x * scale, -o.y * scale};
+      dst[t + k * G::T] = o;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Fused Bluestein (chirp-z) for non-power-of-2 n with M = NextPowerOf2(2n-1):
+//   a = x * conj(w) (zero-padded to M), A = FFT_M(a), C = A * bhat,
+//   r = IFFT_M(C) = conj(FFT_M(conj(C))) (1/M folded into bhat),
+//   X = r * conj(w), first n.  chirp[k] = conj(w_k) = exp(-i pi k^2/n).
+// Inverse (fft.IFFT of non-power-of-2 length): conj in, conj + 1/n out.
+template <int LOG2M, bool INV, bool SPLIT>
+__global__ __launch_bounds__(Geo<LOG2M>::WG) void bluestein_kernel(
+    const cd *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
+    const cd *__restrict__ twm, const cd *__restrict__ chirp, const cd *__restrict__ bhat,
+    double scale) {
+  using G = Geo<LOG2M>;
+  __shared__ double lds[(SPLIT ? 1 : 2) * G::LDS_DOUBLES];
+  const int lt = threadIdx.x;
+  const int slot = lt / G::T;
+  const int t = lt & (G::T - 1);
+  const int64_t g = (int64_t)blockIdx.x * G::TPW + slot;
+  const bool valid = g < batch;
+  double *lre = lds + slot * G::STRIDE;
+  double *lim = SPLIT ? lre : lds + G::LDS_DOUBLES + slot * G::STRIDE;
+  cd v[G::E];
+  const cd *src = in + g * n;
+#pragma unroll
+  for (int k = 0; k < G::E; ++k) {
+    const int idx = t + k * G::T;
+    v[k] = {0.0, 0.0};
+    if (valid && idx < n) {
+      cd x = src[idx];
+      if constexpr (INV) x.y = -x.y;
+      v[k] = cmul(x, chirp[idx]);
+    }
+  }
+  fft_regs<LOG2M, SPLIT>(v, t, twm, lre, lim, true);
+#pragma unroll
+  for (int k = 0; k < G::E; ++k) v[k] = conjg(cmul(v[k], bhat[t + k * G::T]));
+  fft_regs<LOG2M, SPLIT>(v, t, twm, lre, lim, false);
+  if (valid) {
+    cd *dst = out + g * n;
+#pragma unroll
+    for (int k = 0; k < G::E; ++k) {
+      const int idx = t + k * G::T;
+      if (idx < n) {
+        cd y = cmul(conjg(v[k]), chirp[idx]);
+        if constexpr (INV) y = {y.x * scale, -y.y * scale};
+        dst[idx] = y;
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// One radix-R Stockham pass through HBM (large power-of-2 N). One thread per
+// butterfly; loads are coalesced across j.
+template <int R, bool CONJ_IN, int LOAD, bool CONJ_SCALE_OUT>
+__global__ __launch_bounds__(256) void stockham_global_pass(
+    const void *__restrict__ in, cd *__restrict__ out, const cd *__restrict__ tw, int log2n,
+    int log2ns, int64_t batch, double scale) {
+  const int64_t nr = ((int64_t)1 << log2n) / R;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= batch * nr) return;
+  const int64_t g = tid / nr;
+  const int64_t j = tid - g * nr;
+  const int64_t N = (int64_t)1 << log2n;
+  const int64_t NS = (int64_t)1 << log2ns;
+  cd u[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if constexpr (LOAD == LOAD_COMPLEX) {
+      u[r] = reinterpret_cast<const cd *>(in)[g * N + j + r * nr];
+      if constexpr (CONJ_IN) u[r].y = -u[r].y;
+    } else {
+      u[r] = {reinterpret_cast<const double *>(in)[g * N + j + r * nr], 0.0};
+    }
+  }
+  if (NS > 1) {
+    const cd w = tw[(j & (NS - 1)) * (N / (NS * R))];
+    cd wr = w;
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+      u[r] = cmul(u[r], wr);
+      wr = cmul(wr, w);
+    }
+  }
+  Dft<R>::run(u);
+  const int64_t base = g * N + (j >> log2ns) * (NS * R) + (j & (NS - 1));
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    cd o = u[r];
+    if constexpr (CONJ_SCALE_OUT) o = {o.x * scale, -o.y * scale};
+    out[base + r * NS] = o;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Fused Welch periodogram accumulation over packed segment pairs:
+// z = w*x_s0 + i*w*x_s1, Z = FFT(z); |X_s0,k|^2 + |X_s1,k|^2 =
+// (|Z_k|^2 + |Z_{F-k}|^2)/2, so each thread accumulates |Z_k|^2 for its own
+// bins across all pairs of its worker, in registers; the k / F-k fold is done
+// once in gdsp_pwelch_finalize.
+template <int LOG2F, bool SPLIT>
+__global__ __launch_bounds__(Geo<LOG2F>::WG) void pwelch_kernel(
+    const double *__restrict__ x, int64_t nfft, int64_t stride, int64_t seg_begin,
+    int64_t seg_end, int64_t pairs_per_worker, const double *__restrict__ win,
+    const cd *__restrict__ tw, double *__restrict__ partial) {
+  using G = Geo<LOG2F>;
+  __shared__ double lds[(SPLIT ? 1 : 2) * G::LDS_DOUBLES];
+  const int lt = threadIdx.x;
+  const int slot = lt / G::T;
+  const int t = lt & (G::T - 1);
+  const int64_t worker = (int64_t)blockIdx.x * G::TPW + slot;
+  double *lre = lds + slot * G::STRIDE;
+  double *lim = SPLIT ? lre : lds + G::LDS_DOUBLES + slot * G::STRIDE;
+  const int64_t npairs = (seg_end - seg_begin + 1) / 2;
+  double wv[G::E];
+#pragma unroll
+  for (int k = 0; k < G::E; ++k) wv[k] = win[t + k * G::T];
+  double acc[G::E];
+#pragma unroll
+  for (int k = 0; k < G::E; ++k) acc[k] = 0.0;
+  for (int64_t it = 0; it < pairs_per_worker; ++it) {
+    const int64_t p = worker * pairs_per_worker + it;
+    const bool active = p < npairs;
+    const int64_t s0 = seg_begin + 2 * p;
+    const bool has1 = active && (s0 + 1 < seg_end);
+    const double *x0 = x + s0 * stride;
+    const double *x1 = x0 + stride;
+    cd v[G::E];
+#pragma unroll
+    for (int k = 0; k < G::E; ++k) {
+      const int i = t + k * G::T;
+      const bool in_seg = i < nfft;
+      const double a = (active && in_seg) ? x0[i] : 0.0;
+      const double b = (has1 && in_seg) ? x1[i] : 0.0;
+      v[k] = {a * wv[k], b * wv[k]};
+    }
+    fft_regs<LOG2F, SPLIT>(v, t, tw, lre, lim, it == 0);
+    if (active) {
+#pragma unroll
+      for (int k = 0; k < G::E; ++k) acc[k] += v[k].x * v[k].x + v[k].y * v[k].y;
+    }
+  }
+  if (worker * pairs_per_worker < npairs) {
+    double *dst = partial + worker * G::N;
+#pragma unroll
+    for (int k = 0; k < G::E; ++k) dst[t + k * G::T] = acc[k];
+  }
+}
+
+// acc[k] += sum over workers w < nworkers of partial[w*F + k] (fixed order:
+// deterministic).
+__global__ void reduce_partials_kernel(const double *__restrict__ partial, int64_t nworkers,
+                                       int64_t F, double *__restrict__ acc) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= F) return;
+  double s = 0.0;
+  for (int64_t w = 0; w < nworkers; ++w) s += partial[w * F + k];
+  acc[k] += s;
+}
+
+// Materialised Pwelch path (any segment length): windowed, zero-padded real
+// segments as complex rows.
+__global__ void segments_to_complex_kernel(const double *__restrict__ x, int64_t nfft,
+                                           int64_t flen, int64_t stride, int64_t seg0,
+                                           int64_t nseg, const double *__restrict__ win,
+                                           cd *__restrict__ buf) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= nseg * flen) return;
+  const int64_t s = tid / flen;
+  const int64_t i = tid - s * flen;
+  const double a = i < nfft ? x[(seg0 + s) * stride + i] * win[i] : 0.0;
+  buf[tid] = {a, 0.0};
+}
+
+// acc[k] += sum_s |buf[s][k]|^2
+__global__ void power_accumulate_kernel(const cd *__restrict__ buf, int64_t nseg, int64_t flen,
+                                        double *__restrict__ acc) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= flen) return;
+  double s = 0.0;
+  for (int64_t r = 0; r < nseg; ++r) {
+    const cd z = buf[r * flen + k];
+    s += z.x * z.x + z.y * z.y;
+  }
+  acc[k] += s;
+}
+
+// out[c*rows + r] = in[r*cols + c] through a 32x33 LDS tile (complex128).
+__global__ __launch_bounds__(256) void transpose_kernel(const cd *__restrict__ in,
+                                                        cd *__restrict__ out, int64_t rows,
+                                                        int64_t cols) {
+  __shared__ cd tile[32][33];
+  const int64_t tiles_c = (cols + 31) / 32;
+  const int64_t tiles_r = (rows + 31) / 32;
+  for (int64_t tb = blockIdx.x; tb < tiles_c * tiles_r; tb += gridDim.x) {
+    const int64_t tr = tb / tiles_c, tc = tb - tr * tiles_c;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+#pragma unroll
+    for (int i = 0; i < 32; i += 8) {
+      const int64_t r = tr * 32 + ty + i, c = tc * 32 + tx;
+      if (r < rows && c < cols) tile[ty + i][tx] = in[r * cols + c];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 32; i += 8) {
+      const int64_t c = tc * 32 + ty + i, r = tr * 32 + tx;
+      if (r < rows && c < cols) out[c * rows + r] = tile[tx][ty + i];
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void real_to_complex_kernel(const double *__restrict__ in, cd *__restrict__ out,
+                                       int64_t count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) out[i] = {in[i], 0.0};
+}
+
+// Composed Bluestein (n > 8192): premultiply into M-length rows.
+__global__ void chirp_premul_kernel(const cd *__restrict__ in, cd *__restrict__ a, int64_t n,
+                                    int64_t m, int64_t batch, const cd *__restrict__ chirp,
+                                    int conj_in) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= batch * m) return;
+  const int64_t g = tid / m, i = tid - g * m;
+  cd v = {0.0, 0.0};
+  if (i < n) {
+    cd x = in[g * n + i];
+    if (conj_in) x.y = -x.y;
+    v = cmul(x, chirp[i]);
+  }
+  a[tid] = v;
+}
+
+// a = conj(a * bhat) (elementwise over batch rows of m)
+__global__ void bhat_mul_conj_kernel(cd *__restrict__ a, int64_t m, int64_t batch,
+                                     const cd *__restrict__ bhat) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= batch * m) return;
+  a[tid] = conjg(cmul(a[tid], bhat[tid % m]));
+}
+
+__global__ void chirp_postmul_kernel(const cd *__restrict__ a, cd *__restrict__ out, int64_t n,
+                                     int64_t m, int64_t batch, const cd *__restrict__ chirp,
+                                     int inv, double scale) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= batch * n) return;
+  const int64_t g = tid / n, k = tid - g * n;
+  cd y = cmul(conjg(a[g * m + k]), chirp[k]);
+  if (inv) y = {y.x * scale, -y.y * scale};
+  out[tid] = y;
+}
+
+__global__ void pointwise_mul_kernel(const cd *__restrict__ a, const cd *__restrict__ b,
+                                     cd *__restrict__ out, int64_t count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) out[i] = cmul(a[i], b[i]);
+}
+
+__global__ void scale_kernel(cd *__restrict__ a, int64_t count, double s) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) a[i] = {a[i].x * s, a[i].y * s};
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+__global__ void fill_uniform_kernel(double *__restrict__ out, int64_t count, uint64_t seed,
+                                    uint64_t offset) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t z = splitmix64(seed + (offset + (uint64_t)i + 1) * 0x9E3779B97F4A7C15ULL);
+    out[i] = (double)(z >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0;
+  }
+}
+
+// ============================================================================
+// Host launchers
+// ============================================================================
+static inline unsigned blocks_for(int64_t work, int per) {
+  return (unsigned)((work + per - 1) / per);
+}
+
+template <int LOG2N, bool INV, int LOAD, bool SPLIT>
+static hipError_t launch_lds_t(const void *in, cd *out, int64_t batch, const cd *tw,
+                               double scale, hipStream_t s) {
+  using G = Geo<LOG2N>;
+  const int64_t nblk = (batch + G::TPW - 1) / G::TPW;
+  hipLaunchKernelGGL((fft_lds_kernel<LOG2N, INV, LOAD, SPLIT>), dim3((unsigned)nblk),
+                     dim3(G::WG), 0, s, in, out, batch, tw, scale);
+  return hipGetLastError();
+}
+
+template <int LOG2N, bool INV, int LOAD>
+static hipError_t launch_lds_s(const void *in, cd *out, int64_t batch, const cd *tw,
+                               double scale, bool split, hipStream_t s) {
+  // the two-buffer exchange is only instantiated where it still fits LDS
+  if constexpr (LOG2N <= 13) {
+    if (!split) return launch_lds_t<LOG2N, INV, LOAD, false>(in, out, batch, tw, scale, s);
+  }
+  return launch_lds_t<LOG2N, INV, LOAD, true>(in, out, batch, tw, scale, s);
+}
+
+#define GDSP_LDS_CASE(L)                                                                   \
+  case L:                                                                                  \
+    if (load == LOAD_COMPLEX)                                                              \
+      return inv ? launch_lds_s<L, true, LOAD_COMPLEX>(in, out, batch, tw, scale, split, s) \
+                 : launch_lds_s<L, false, LOAD_COMPLEX>(in, out, batch, tw, scale, split, s); \
+    return launch_lds_s<L, false, LOAD_REAL>(in, out, batch, tw, scale, split, s);
+
+hipError_t launch_fft_lds(int log2n, bool inv, int load, bool split, const void *in, cd *out,
+                          int64_t batch, const cd *tw, double scale, hipStream_t s) {
+  if (load == LOAD_REAL && inv) return hipErrorInvalidValue;
+  switch (log2n) {
+    GDSP_LDS_CASE(1)
+    GDSP_LDS_CASE(2)
+    GDSP_LDS_CASE(3)
+    GDSP_LDS_CASE(4)
+    GDSP_LDS_CASE(5)
+    GDSP_LDS_CASE(6)
+    GDSP_LDS_CASE(7)
+    GDSP_LDS_CASE(8)
+    GDSP_LDS_CASE(9)
+    GDSP_LDS_CASE(10)
+    GDSP_LDS_CASE(11)
+    GDSP_LDS_CASE(12)
+    GDSP_LDS_CASE(13)
+    GDSP_LDS_CASE(14)
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int LOG2M, bool INV>
+static hipError_t launch_blu_t(const cd *in, cd *out, int64_t n, int64_t batch, const cd *twm,
+                               const cd *chirp, const cd *bhat, double scale, hipStream_t s) {
+  using G = Geo<LOG2M>;
+  const int64_t nblk = (batch + G::TPW - 1) / G::TPW;
+  hipLaunchKernelGGL((bluestein_kernel<LOG2M, INV, true>), dim3((unsigned)nblk), dim3(G::WG), 0,
+                     s, in, out, n, batch, twm, chirp, bhat, scale);
+  return hipGetLastError();
+}
+
+#define GDSP_BLU_CASE(L)                                                                     \
+  case L:                                                                                    \
+    return inv ? launch_blu_t<L, true>(in, out, n, batch, twm, chirp, bhat, scale, s)        \
+               : launch_blu_t<L, false>(in, out, n, batch, twm, chirp, bhat, scale, s);
+
+hipError_t launch_bluestein(int log2m, bool inv, const cd *in, cd *out, int64_t n,
+                            int64_t batch, const cd *twm, const cd *chirp, const cd *bhat,
+                            double scale, hipStream_t s) {
+  switch (log2m) {
+    GDSP_BLU_CASE(2)
+    GDSP_BLU_CASE(3)
+    GDSP_BLU_CASE(4)
+    GDSP_BLU_CASE(5)
+    GDSP_BLU_CASE(6)
+    GDSP_BLU_CASE(7)
+    GDSP_BLU_CASE(8)
+    GDSP_BLU_CASE(9)
+    GDSP_BLU_CASE(10)
+    GDSP_BLU_CASE(11)
+    GDSP_BLU_CASE(12)
+    GDSP_BLU_CASE(13)
+    GDSP_BLU_CASE(14)
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int R>
+static hipError_t launch_gpass_r(bool conj_in, int load, bool conj_scale_out, const void *in,
+                                 cd *out, const cd *tw, int log2n, int log2ns, int64_t batch,
+                                 double scale, hipStream_t s) {
+  const int64_t work = batch * (((int64_t)1 << log2n) / R);
+  const unsigned nb = blocks_for(work, 256);
+#define GDSP_GP(CI, LD, CO)                                                                  \
+  hipLaunchKernelGGL((stockham_global_pass<R, CI, LD, CO>), dim3(nb), dim3(256), 0, s, in, out, \
+                     tw, log2n, log2ns, batch, scale)
+  if (load == LOAD_REAL) {
+    if (conj_scale_out) GDSP_GP(false, LOAD_REAL, true);
+    else GDSP_GP(false, LOAD_REAL, false);
+  } else if (conj_in) {
+    if (conj_scale_out) GDSP_GP(true, LOAD_COMPLEX, true);
+    else GDSP_GP(true, LOAD_COMPLEX, false);
+  } else {
+    if (conj_scale_out) GDSP_GP(false, LOAD_COMPLEX, true);
+    else GDSP_GP(false, LOAD_COMPLEX, false);
+  }
+#undef GDSP_GP
+  return hipGetLastError();
+}
+
+hipError_t launch_global_pass(int radix, bool conj_in, int load, bool conj_scale_out,
+                              const void *in, cd *out, const cd *tw, int log2n, int log2ns,
+                              int64_t batch, double scale, hipStream_t s) {
+  switch (radix) {
+    case 2: return launch_gpass_r<2>(conj_in, load, conj_scale_out, in, out, tw, log2n, log2ns, batch, scale, s);
+    case 4: return launch_gpass_r<4>(conj_in, load, conj_scale_out, in, out, tw, log2n, log2ns, batch, scale, s);
+    case 8: return launch_gpass_r<8>(conj_in, load, conj_scale_out, in, out, tw, log2n, log2ns, batch, scale, s);
+    case 16: return launch_gpass_r<16>(conj_in, load, conj_scale_out, in, out, tw, log2n, log2ns, batch, scale, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int LOG2F>
+static hipError_t launch_pw_t(const double *x, int64_t nfft, int64_t stride, int64_t seg_begin,
+                              int64_t seg_end, int64_t ppw, int64_t nworkers, const double *win,
+                              const cd *tw, double *partial, hipStream_t s) {
+  using G = Geo<LOG2F>;
+  const int64_t nblk = (nworkers + G::TPW - 1) / G::TPW;
+  hipLaunchKernelGGL((pwelch_kernel<LOG2F, true>), dim3((unsigned)nblk), dim3(G::WG), 0, s, x,
+                     nfft, stride, seg_begin, seg_end, ppw, win, tw, partial);
+  return hipGetLastError();
+}
+
+int pwelch_workers_per_block(int log2f) {
+  switch (log2f) {
+#define GDSP_PWT(L) case L: return Geo<L>::TPW;
+    GDSP_PWT(4) GDSP_PWT(5) GDSP_PWT(6) GDSP_PWT(7) GDSP_PWT(8) GDSP_PWT(9) GDSP_PWT(10)
+    GDSP_PWT(11) GDSP_PWT(12) GDSP_PWT(13) GDSP_PWT(14)
+#undef GDSP_PWT
+    default: return 1;
+  }
+}
+
+hipError_t launch_pwelch(int log2f, const double *x, int64_t nfft, int64_t stride,
+                         int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,
+                         const double *win, const cd *tw, double *partial, hipStream_t s) {
+  switch (log2f) {
+#define GDSP_PWC(L) \
+  case L: return launch_pw_t<L>(x, nfft, stride, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
+    GDSP_PWC(4) GDSP_PWC(5) GDSP_PWC(6) GDSP_PWC(7) GDSP_PWC(8) GDSP_PWC(9) GDSP_PWC(10)
+    GDSP_PWC(11) GDSP_PWC(12) GDSP_PWC(13) GDSP_PWC(14)
+#undef GDSP_PWC
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_reduce_partials(const double *partial, int64_t nworkers, int64_t F, double *acc,
+                                  hipStream_t s) {
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(blocks_for(F, 256)), dim3(256), 0, s, partial,
+                     nworkers, F, acc);
+  return hipGetLastError();
+}
+
+hipError_t launch_segments_to_complex(const double *x, int64_t nfft, int64_t flen, int64_t stride,
+                                      int64_t seg0, int64_t nseg, const double *win, cd *buf,
+                                      hipStream_t s) {
+  hipLaunchKernelGGL(segments_to_complex_kernel, dim3(blocks_for(nseg * flen, 256)), dim3(256), 0,
+                     s, x, nfft, flen, stride, seg0, nseg, win, buf);
+  return hipGetLastError();
+}
+
+hipError_t launch_power_accumulate(const cd *buf, int64_t nseg, int64_t flen, double *acc,
+                                   hipStream_t s) {
+  hipLaunchKernelGGL(power_accumulate_kernel, dim3(blocks_for(flen, 256)), dim3(256), 0, s, buf,
+                     nseg, flen, acc);
+  return hipGetLastError();
+}
+
+hipError_t launch_transpose(const cd *in, cd *out, int64_t rows, int64_t cols, hipStream_t s) {
+  const int64_t tiles = ((rows + 31) / 32) * ((cols + 31) / 32);
+  const unsigned nb = (unsigned)(tiles < 65536 ? tiles : 65536);
+  hipLaunchKernelGGL(transpose_kernel, dim3(nb), dim3(256), 0, s, in, out, rows, cols);
+  return hipGetLastError();
+}
+
+hipError_t launch_real_to_complex(const double *in, cd *out, int64_t count, hipStream_t s) {
+  hipLaunchKernelGGL(real_to_complex_kernel, dim3(blocks_for(count, 256)), dim3(256), 0, s, in,
+                     out, count);
+  return hipGetLastError();
+}
+
+hipError_t launch_chirp_premul(const cd *in, cd *a, int64_t n, int64_t m, int64_t batch,
+                               const cd *chirp, bool conj_in, hipStream_t s) {
+  hipLaunchKernelGGL(chirp_premul_kernel, dim3(blocks_for(batch * m, 256)), dim3(256), 0, s, in,
+                     a, n, m, batch, chirp, (int)conj_in);
+  return hipGetLastError();
+}
+
+hipError_t launch_bhat_mul_conj(cd *a, int64_t m, int64_t batch, const cd *bhat, hipStream_t s) {
+  hipLaunchKernelGGL(bhat_mul_conj_kernel, dim3(blocks_for(batch * m, 256)), dim3(256), 0, s, a, m,
+                     batch, bhat);
+  return hipGetLastError();
+}
+
+hipError_t launch_chirp_postmul(const cd *a, cd *out, int64_t n, int64_t m, int64_t batch,
+                                const cd *chirp, bool inv, double scale, hipStream_t s) {
+  hipLaunchKernelGGL(chirp_postmul_kernel, dim3(blocks_for(batch * n, 256)), dim3(256), 0, s, a,
+                     out, n, m, batch, chirp, (int)inv, scale);
+  return hipGetLastError();
+}
+
+hipError_t launch_pointwise_mul(const cd *a, const cd *b, cd *out, int64_t count, hipStream_t s) {
+  hipLaunchKernelGGL(pointwise_mul_kernel, dim3(blocks_for(count, 256)), dim3(256), 0, s, a, b,
+                     out, count);
+  return hipGetLastError();
+}
+
+hipError_t launch_scale(cd *a, int64_t count, double sc, hipStream_t s) {
+  hipLaunchKernelGGL(scale_kernel, dim3(blocks_for(count, 256)), dim3(256), 0, s, a, count, sc);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_uniform(double *out, int64_t count, uint64_t seed, uint64_t offset,
+                               hipStream_t s) {
+  int64_t nb = (count + 255) / 256;
+  if (nb > 8192) nb = 8192;
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(fill_uniform_kernel, dim3((unsigned)nb), dim3(256), 0, s, out, count, seed,
+                     offset);
+  return hipGetLastError();
+}
+
+}  // namespace gdsp

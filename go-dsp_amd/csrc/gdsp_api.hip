@@ -1,0 +1,694 @@
+// gdsp_api.hip — the C ABI of libgdspfft (include/gdsp_fft.h): plan cache,
+// per-thread streams, host-pointer entry points (what cgo binds) and
+// device-pointer entry points (what the multi-GPU drivers call).
+//
+// Every transform runs on the GPU. There is no CPU compute path: without a
+// HIP device the entry points return GDSP_ERR_NO_DEVICE.
+#include <math.h>
+#include <string.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "fft_device.hpp"
+#include "gdsp_fft.h"
+#include "launch.hpp"
+
+using gdsp::cd;
+
+#define GDSP_VERSION "gdspfft 0.1.0 (gfx950)"
+
+namespace {
+
+thread_local std::string g_last_error;
+int g_worker_pool_size = 0;  // fft.SetWorkerPoolSize mirror (no GPU meaning)
+
+int fail(int st, const std::string &msg) {
+  g_last_error = msg;
+  return st;
+}
+
+#define HIPCHK(expr)                                                                       \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return fail(GDSP_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));      \
+  } while (0)
+
+#define STCHK(expr)               \
+  do {                            \
+    int s_ = (expr);              \
+    if (s_ != GDSP_OK) return s_; \
+  } while (0)
+
+bool is_pow2(int64_t x) { return (x & (x - 1)) == 0; }
+
+int ilog2(int64_t x) {
+  int r = 0;
+  while (x > 1) {
+    x >>= 1;
+    ++r;
+  }
+  return r;
+}
+
+// dsputils.NextPowerOf2 (dsputils/dsputils.go:39-45): float Log2/Ceil/Pow.
+int64_t next_pow2_ref(int64_t x) {
+  if (is_pow2(x)) return x;
+  return (int64_t)pow(2.0, ceil(log2((double)x)));
+}
+
+int current_device(int *dev) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+    return fail(GDSP_ERR_NO_DEVICE, "no HIP device visible");
+  if (hipGetDevice(dev) != hipSuccess) return fail(GDSP_ERR_NO_DEVICE, "hipGetDevice failed");
+  return GDSP_OK;
+}
+
+// One non-blocking stream per (thread, device) for the host-pointer API.
+hipStream_t thread_stream(int dev) {
+  thread_local std::map<int, hipStream_t> streams;
+  auto it = streams.find(dev);
+  if (it != streams.end()) return it->second;
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  streams[dev] = s;
+  return s;
+}
+
+bool lds_split_default() {
+  static int v = [] {
+    const char *e = getenv("GDSP_LDS_SPLIT");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v != 0;
+}
+
+// RAII for stream-ordered device scratch.
+struct DevBuf {
+  void *p = nullptr;
+  hipStream_t s = nullptr;
+  DevBuf() = default;
+  DevBuf(const DevBuf &) = delete;
+  ~DevBuf() {
+    if (p) (void)hipFreeAsync(p, s);
+  }
+  int alloc(size_t bytes, hipStream_t st) {
+    s = st;
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMallocAsync(&p, bytes, st);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return fail(GDSP_ERR_NOMEM, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+    }
+    return GDSP_OK;
+  }
+};
+
+}  // namespace
+
+enum PlanKind { KIND_TRIVIAL = 0, KIND_LDS = 1, KIND_GLOBAL = 2, KIND_BLUESTEIN = 3,
+                KIND_BLUESTEIN_COMPOSED = 4 };
+
+struct gdsp_plan {
+  int device = 0;
+  int64_t n = 0;
+  int kind = KIND_TRIVIAL;
+  int log2n = 0;
+  cd *tw = nullptr;  // power of 2: T_n[k] = exp(-2 pi i k/n), n entries
+  // Bluestein (fft/bluestein.go): M = NextPowerOf2(2n-1), chirp = conj(w),
+  // bhat = FFT_M(b)/M
+  int64_t m = 0;
+  int log2m = 0;
+  gdsp_plan *mplan = nullptr;
+  cd *chirp = nullptr;
+  cd *bhat = nullptr;
+};
+
+namespace {
+
+std::mutex g_plan_mu;
+std::map<std::pair<int, int64_t>, gdsp_plan *> g_plans;
+
+int exec_plan(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
+              hipStream_t s);
+
+// T_n[k] = exp(-2 pi i k/n), evaluated in long double and rounded once.
+int upload_twiddles(int64_t n, cd **dst) {
+  std::vector<cd> h((size_t)n);
+  for (int64_t k = 0; k < n; ++k) {
+    long double a = -2.0L * 3.141592653589793238462643383279502884L * (long double)k /
+                    (long double)n;
+    h[(size_t)k].x = (double)cosl(a);
+    h[(size_t)k].y = (double)sinl(a);
+  }
+  HIPCHK(hipMalloc((void **)dst, (size_t)n * sizeof(cd)));
+  HIPCHK(hipMemcpy(*dst, h.data(), (size_t)n * sizeof(cd), hipMemcpyHostToDevice));
+  return GDSP_OK;
+}
+
+int get_plan_locked(int dev, int64_t n, gdsp_plan **out);
+
+int build_plan(int dev, int64_t n, gdsp_plan *p) {
+  p->device = dev;
+  p->n = n;
+  if (n <= 1) {
+    p->kind = KIND_TRIVIAL;
+    return GDSP_OK;
+  }
+  if (is_pow2(n)) {
+    p->log2n = ilog2(n);
+    p->kind = p->log2n <= gdsp::kMaxLdsLog2 ? KIND_LDS : KIND_GLOBAL;
+    return upload_twiddles(n, &p->tw);
+  }
+  // Bluestein factors, bluestein.go:32-61: w_k = (cos, sin)(Pi/n * k*k),
+  // k = 0 exactly 1 (angle not reduced, as the reference computes it).
+  p->m = next_pow2_ref(2 * n - 1);
+  p->log2m = ilog2(p->m);
+  p->kind = p->log2m <= gdsp::kMaxLdsLog2 ? KIND_BLUESTEIN : KIND_BLUESTEIN_COMPOSED;
+  STCHK(get_plan_locked(dev, p->m, &p->mplan));
+  std::vector<cd> w((size_t)n), chirp((size_t)n), b((size_t)p->m, cd{0.0, 0.0});
+  for (int64_t k = 0; k < n; ++k) {
+    double sn = 0.0, cs = 1.0;
+    if (k != 0) {
+      const double ang = M_PI / (double)n * (double)(k * k);
+      sn = sin(ang);
+      cs = cos(ang);
+    }
+    w[(size_t)k] = {cs, sn};
+    chirp[(size_t)k] = {cs, -sn};
+  }
+  for (int64_t i = 0; i < n; ++i) {  // bluestein.go:78-85
+    b[(size_t)i] = w[(size_t)i];
+    if (i != 0) b[(size_t)(p->m - i)] = w[(size_t)i];
+  }
+  HIPCHK(hipMalloc((void **)&p->chirp, (size_t)n * sizeof(cd)));
+  HIPCHK(hipMemcpy(p->chirp, chirp.data(), (size_t)n * sizeof(cd), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc((void **)&p->bhat, (size_t)p->m * sizeof(cd)));
+  cd *db = nullptr;
+  HIPCHK(hipMalloc((void **)&db, (size_t)p->m * sizeof(cd)));
+  HIPCHK(hipMemcpy(db, b.data(), (size_t)p->m * sizeof(cd), hipMemcpyHostToDevice));
+  // FFT_M(b) on the device with the engine itself, then fold the IFFT's 1/M
+  hipStream_t s = thread_stream(dev);
+  int st = exec_plan(p->mplan, db, p->bhat, 1, false, gdsp::LOAD_COMPLEX, s);
+  if (st == GDSP_OK) {
+    hipError_t e = gdsp::launch_scale(p->bhat, p->m, 1.0 / (double)p->m, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) st = fail(GDSP_ERR_HIP, hipGetErrorString(e));
+  }
+  (void)hipFree(db);
+  return st;
+}
+
+int get_plan_locked(int dev, int64_t n, gdsp_plan **out) {
+  auto key = std::make_pair(dev, n);
+  auto it = g_plans.find(key);
+  if (it != g_plans.end()) {
+    *out = it->second;
+    return GDSP_OK;
+  }
+  gdsp_plan *p = new gdsp_plan();
+  int st = build_plan(dev, n, p);
+  if (st != GDSP_OK) {
+    delete p;  // device tables of a failed plan are leaked deliberately (rare)
+    return st;
+  }
+  g_plans[key] = p;
+  *out = p;
+  return GDSP_OK;
+}
+
+int get_plan(int64_t n, gdsp_plan **out) {
+  int dev = 0;
+  STCHK(current_device(&dev));
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  return get_plan_locked(dev, n, out);
+}
+
+// Large power of 2: radix-16 Stockham passes through HBM, last pass into out.
+int exec_global(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
+                hipStream_t s) {
+  std::vector<int> radix;
+  int rem = p->log2n;
+  while (rem >= 4) {
+    radix.push_back(16);
+    rem -= 4;
+  }
+  if (rem) radix.push_back(1 << rem);
+  const int np = (int)radix.size();
+  const size_t bytes = (size_t)batch * (size_t)p->n * sizeof(cd);
+  DevBuf scratch, inbuf;
+  STCHK(scratch.alloc(bytes, s));
+  const void *src = in;
+  if (in == (const void *)out && ((np - 1) % 2 == 0)) {
+    STCHK(inbuf.alloc(bytes, s));
+    HIPCHK(hipMemcpyAsync(inbuf.p, in, bytes, hipMemcpyDeviceToDevice, s));
+    src = inbuf.p;
+  }
+  int log2ns = 0;
+  for (int q = 0; q < np; ++q) {
+    cd *dst = ((np - 1 - q) % 2 == 0) ? out : (cd *)scratch.p;
+    HIPCHK(gdsp::launch_global_pass(radix[q], inv && q == 0, q == 0 ? load : gdsp::LOAD_COMPLEX,
+                                    inv && q == np - 1, src, dst, p->tw, p->log2n, log2ns, batch,
+                                    1.0 / (double)p->n, s));
+    src = dst;
+    log2ns += ilog2(radix[q]);
+  }
+  return GDSP_OK;
+}
+
+int exec_bluestein_composed(const gdsp_plan *p, const cd *in, cd *out, int64_t batch, bool inv,
+                            hipStream_t s) {
+  DevBuf a;
+  STCHK(a.alloc((size_t)batch * (size_t)p->m * sizeof(cd), s));
+  cd *da = (cd *)a.p;
+  HIPCHK(gdsp::launch_chirp_premul(in, da, p->n, p->m, batch, p->chirp, inv, s));
+  STCHK(exec_plan(p->mplan, da, da, batch, false, gdsp::LOAD_COMPLEX, s));
+  HIPCHK(gdsp::launch_bhat_mul_conj(da, p->m, batch, p->bhat, s));
+  STCHK(exec_plan(p->mplan, da, da, batch, false, gdsp::LOAD_COMPLEX, s));
+  HIPCHK(gdsp::launch_chirp_postmul(da, out, p->n, p->m, batch, p->chirp, inv,
+                                    1.0 / (double)p->n, s));
+  return GDSP_OK;
+}
+
+// Batched transform of `batch` rows of n on device buffers. load = LOAD_REAL
+// reads float64 rows (fft.FFTReal); in == out is allowed.
+int exec_plan(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
+              hipStream_t s) {
+  if (batch <= 0) return GDSP_OK;
+  const double scale = 1.0 / (double)(p->n > 0 ? p->n : 1);
+  switch (p->kind) {
+    case KIND_TRIVIAL: {
+      if (p->n == 0) return GDSP_OK;
+      if (load == gdsp::LOAD_REAL) {
+        HIPCHK(gdsp::launch_real_to_complex((const double *)in, out, batch, s));
+      } else if (in != (const void *)out) {
+        HIPCHK(hipMemcpyAsync(out, in, (size_t)batch * sizeof(cd), hipMemcpyDeviceToDevice, s));
+      }
+      return GDSP_OK;
+    }
+    case KIND_LDS:
+      HIPCHK(gdsp::launch_fft_lds(p->log2n, inv, load, lds_split_default(), in, out, batch, p->tw,
+                                  scale, s));
+      return GDSP_OK;
+    case KIND_GLOBAL:
+      return exec_global(p, in, out, batch, inv, load, s);
+    case KIND_BLUESTEIN:
+    case KIND_BLUESTEIN_COMPOSED: {
+      const cd *src = (const cd *)in;
+      DevBuf tmp;
+      if (load == gdsp::LOAD_REAL) {
+        STCHK(tmp.alloc((size_t)batch * (size_t)p->n * sizeof(cd), s));
+        HIPCHK(gdsp::launch_real_to_complex((const double *)in, (cd *)tmp.p, batch * p->n, s));
+        src = (const cd *)tmp.p;
+      }
+      if (p->kind == KIND_BLUESTEIN) {
+        HIPCHK(gdsp::launch_bluestein(p->log2m, inv, src, out, p->n, batch, p->mplan->tw, p->chirp,
+                                      p->bhat, scale, s));
+        return GDSP_OK;
+      }
+      return exec_bluestein_composed(p, src, out, batch, inv, s);
+    }
+  }
+  return fail(GDSP_ERR_INVALID, "bad plan kind");
+}
+
+// Host-pointer batched transform: H2D, exec, D2H, synchronise.
+int host_batch(const void *x, size_t in_elem_bytes, double *out, int64_t n, int64_t batch,
+               bool inv, int load) {
+  if (n < 0 || batch < 0) return fail(GDSP_ERR_INVALID, "negative size");
+  if (batch == 0) return GDSP_OK;
+  if (n == 0) {
+    if (inv) return fail(GDSP_ERR_EMPTY, "IFFT of an empty slice (index out of range)");
+    return GDSP_OK;
+  }
+  if (!x || !out) return fail(GDSP_ERR_INVALID, "NULL pointer");
+  gdsp_plan *p = nullptr;
+  STCHK(get_plan(n, &p));
+  hipStream_t s = thread_stream(p->device);
+  if (!s) return fail(GDSP_ERR_HIP, "stream creation failed");
+  const size_t in_bytes = (size_t)batch * (size_t)n * in_elem_bytes;
+  const size_t out_bytes = (size_t)batch * (size_t)n * sizeof(cd);
+  DevBuf din, dout;
+  STCHK(din.alloc(in_bytes, s));
+  STCHK(dout.alloc(out_bytes, s));
+  HIPCHK(hipMemcpyAsync(din.p, x, in_bytes, hipMemcpyHostToDevice, s));
+  STCHK(exec_plan(p, din.p, (cd *)dout.p, batch, inv, load, s));
+  HIPCHK(hipMemcpyAsync(out, dout.p, out_bytes, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return GDSP_OK;
+}
+
+void hann_table(int64_t L, double *r) {  // window/window.go:62-76
+  if (L <= 0) return;
+  if (L == 1) {
+    r[0] = 1;
+    return;
+  }
+  const int64_t N = L - 1;
+  const double coef = 2 * M_PI / (double)N;
+  for (int64_t i = 0; i <= N; ++i) r[i] = 0.5 * (1 - cos(coef * (double)i));
+}
+
+int segment_count(int64_t lx, int64_t size, int64_t noverlap, int64_t *count) {
+  const int64_t stride = size - noverlap;  // spectral/spectral.go:22-33
+  if (lx == size) {
+    *count = 1;
+  } else if (lx > size) {
+    if (stride == 0) return fail(GDSP_ERR_DIVIDE_BY_ZERO, "integer divide by zero");
+    *count = (lx - size) / stride + 1;
+    if (*count < 0) return fail(GDSP_ERR_INVALID, "makeslice: len out of range");
+  } else {
+    *count = 0;
+  }
+  return GDSP_OK;
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+const char *gdsp_status_string(int st) {
+  switch (st) {
+    case GDSP_OK: return "ok";
+    case GDSP_ERR_INVALID: return "invalid argument";
+    case GDSP_ERR_UNEQUAL: return "arrays not of equal size";
+    case GDSP_ERR_EMPTY: return "empty input array";
+    case GDSP_ERR_RAGGED: return "ragged input array";
+    case GDSP_ERR_DIVIDE_BY_ZERO: return "integer divide by zero";
+    case GDSP_ERR_NO_DEVICE: return "no HIP device";
+    case GDSP_ERR_HIP: return "HIP runtime error";
+    case GDSP_ERR_NOMEM: return "out of memory";
+    case GDSP_ERR_UNSUPPORTED: return "unsupported size";
+  }
+  return "unknown status";
+}
+
+const char *gdsp_last_error(void) { return g_last_error.c_str(); }
+const char *gdsp_version(void) { return GDSP_VERSION; }
+
+int gdsp_device_count(void) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) return 0;
+  return c;
+}
+
+int gdsp_fft(const double *x, double *out, int64_t n) {
+  return host_batch(x, sizeof(cd), out, n, 1, false, gdsp::LOAD_COMPLEX);
+}
+
+int gdsp_ifft(const double *x, double *out, int64_t n) {
+  return host_batch(x, sizeof(cd), out, n, 1, true, gdsp::LOAD_COMPLEX);
+}
+
+int gdsp_fft_real(const double *x, double *out, int64_t n) {
+  return host_batch(x, sizeof(double), out, n, 1, false, gdsp::LOAD_REAL);
+}
+
+int gdsp_ifft_real(const double *x, double *out, int64_t n) {
+  if (n < 0) return fail(GDSP_ERR_INVALID, "negative size");
+  if (n == 0) return fail(GDSP_ERR_EMPTY, "IFFT of an empty slice (index out of range)");
+  std::vector<double> c((size_t)(2 * n), 0.0);  // dsputils.ToComplex
+  for (int64_t i = 0; i < n; ++i) c[(size_t)(2 * i)] = x[i];
+  return host_batch(c.data(), sizeof(cd), out, n, 1, true, gdsp::LOAD_COMPLEX);
+}
+
+int gdsp_fft_batch(const double *x, double *out, int64_t n, int64_t batch, int inverse) {
+  return host_batch(x, sizeof(cd), out, n, batch, inverse != 0, gdsp::LOAD_COMPLEX);
+}
+
+int gdsp_fft_real_batch(const double *x, double *out, int64_t n, int64_t batch) {
+  return host_batch(x, sizeof(double), out, n, batch, false, gdsp::LOAD_REAL);
+}
+
+int gdsp_convolve(const double *x, const double *y, double *out, int64_t n) {
+  // fft.Convolve, fft/fft.go:55-69: IFFT(FFT(x) * FFT(y))
+  if (n < 0) return fail(GDSP_ERR_INVALID, "negative size");
+  if (n == 0) return fail(GDSP_ERR_EMPTY, "IFFT of an empty slice (index out of range)");
+  if (!x || !y || !out) return fail(GDSP_ERR_INVALID, "NULL pointer");
+  gdsp_plan *p = nullptr;
+  STCHK(get_plan(n, &p));
+  hipStream_t s = thread_stream(p->device);
+  const size_t bytes = (size_t)n * sizeof(cd);
+  DevBuf d;
+  STCHK(d.alloc(3 * bytes, s));
+  cd *dx = (cd *)d.p, *dy = dx + n, *dz = dy + n;
+  HIPCHK(hipMemcpyAsync(dx, x, bytes, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(dy, y, bytes, hipMemcpyHostToDevice, s));
+  STCHK(exec_plan(p, dx, dx, 2, false, gdsp::LOAD_COMPLEX, s));  // both rows at once
+  HIPCHK(gdsp::launch_pointwise_mul(dx, dy, dz, n, s));
+  STCHK(exec_plan(p, dz, dz, 1, true, gdsp::LOAD_COMPLEX, s));
+  HIPCHK(hipMemcpyAsync(out, dz, bytes, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return GDSP_OK;
+}
+
+int gdsp_fft2_device(const void *d_in, void *d_out, int64_t rows, int64_t cols, int inverse,
+                     void *d_work, void *stream) {
+  // fft/fft.go:123-154: column pass (length rows, batch cols), then row pass
+  if (rows <= 0) return fail(GDSP_ERR_EMPTY, "empty input array");
+  if (cols < 0) return fail(GDSP_ERR_INVALID, "negative size");
+  if (cols == 0) return GDSP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  int dev = 0;
+  STCHK(current_device(&dev));
+  if (!s) s = thread_stream(dev);
+  gdsp_plan *pr = nullptr, *pc = nullptr;
+  STCHK(get_plan(rows, &pr));
+  STCHK(get_plan(cols, &pc));
+  DevBuf w;
+  cd *work = (cd *)d_work;
+  if (!work) {
+    STCHK(w.alloc((size_t)rows * (size_t)cols * sizeof(cd), s));
+    work = (cd *)w.p;
+  }
+  const bool inv = inverse != 0;
+  HIPCHK(gdsp::launch_transpose((const cd *)d_in, work, rows, cols, s));
+  STCHK(exec_plan(pr, work, work, cols, inv, gdsp::LOAD_COMPLEX, s));
+  HIPCHK(gdsp::launch_transpose(work, (cd *)d_out, cols, rows, s));
+  STCHK(exec_plan(pc, d_out, (cd *)d_out, rows, inv, gdsp::LOAD_COMPLEX, s));
+  return GDSP_OK;
+}
+
+static int fft2_host(const double *x, bool real_in, double *out, int64_t rows, int64_t cols,
+                     int inverse) {
+  if (rows <= 0) return fail(GDSP_ERR_EMPTY, "empty input array");
+  if (cols < 0) return fail(GDSP_ERR_INVALID, "negative size");
+  if (cols == 0) return GDSP_OK;
+  int dev = 0;
+  STCHK(current_device(&dev));
+  hipStream_t s = thread_stream(dev);
+  const size_t cnt = (size_t)rows * (size_t)cols;
+  DevBuf din, dout;
+  STCHK(din.alloc(cnt * sizeof(cd), s));
+  STCHK(dout.alloc(cnt * sizeof(cd), s));
+  if (real_in) {
+    DevBuf dr;
+    STCHK(dr.alloc(cnt * sizeof(double), s));
+    HIPCHK(hipMemcpyAsync(dr.p, x, cnt * sizeof(double), hipMemcpyHostToDevice, s));
+    HIPCHK(gdsp::launch_real_to_complex((const double *)dr.p, (cd *)din.p, (int64_t)cnt, s));
+  } else {
+    HIPCHK(hipMemcpyAsync(din.p, x, cnt * sizeof(cd), hipMemcpyHostToDevice, s));
+  }
+  STCHK(gdsp_fft2_device(din.p, dout.p, rows, cols, inverse, nullptr, s));
+  HIPCHK(hipMemcpyAsync(out, dout.p, cnt * sizeof(cd), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return GDSP_OK;
+}
+
+int gdsp_fft2(const double *x, double *out, int64_t rows, int64_t cols, int inverse) {
+  return fft2_host(x, false, out, rows, cols, inverse);
+}
+
+int gdsp_fft2_real(const double *x, double *out, int64_t rows, int64_t cols, int inverse) {
+  return fft2_host(x, true, out, rows, cols, inverse);
+}
+
+int gdsp_ensure_plan(int64_t n) {
+  if (n < 0) return fail(GDSP_ERR_INVALID, "negative size");
+  gdsp_plan *p = nullptr;
+  return get_plan(n, &p);
+}
+
+void gdsp_set_worker_pool_size(int n) { g_worker_pool_size = n < 0 ? 0 : n; }
+int gdsp_worker_pool_size(void) { return g_worker_pool_size; }
+
+int gdsp_segment_count(int64_t lx, int64_t size, int64_t noverlap, int64_t *count) {
+  if (!count) return fail(GDSP_ERR_INVALID, "NULL pointer");
+  return segment_count(lx, size, noverlap, count);
+}
+
+int gdsp_window_hann(int64_t L, double *out) {
+  if (L < 0) return fail(GDSP_ERR_INVALID, "negative size");
+  hann_table(L, out);
+  return GDSP_OK;
+}
+
+int gdsp_plan_create(int64_t n, gdsp_plan **plan) {
+  if (n < 0 || !plan) return fail(GDSP_ERR_INVALID, "bad argument");
+  return get_plan(n, plan);
+}
+
+int gdsp_plan_destroy(gdsp_plan *) { return GDSP_OK; }
+
+int gdsp_plan_kind(const gdsp_plan *plan) { return plan ? plan->kind : -1; }
+
+int gdsp_fft_batch_device(const gdsp_plan *plan, const void *d_in, void *d_out, int64_t batch,
+                          int inverse, void *stream) {
+  if (!plan || batch < 0) return fail(GDSP_ERR_INVALID, "bad argument");
+  if (plan->n == 0 && inverse) return fail(GDSP_ERR_EMPTY, "IFFT of an empty slice");
+  hipStream_t s = (hipStream_t)stream;
+  if (!s) s = thread_stream(plan->device);
+  return exec_plan(plan, d_in, (cd *)d_out, batch, inverse != 0, gdsp::LOAD_COMPLEX, s);
+}
+
+int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, int64_t pad,
+                                  int64_t noverlap, int64_t seg_begin, int64_t seg_end,
+                                  const double *d_win_seg, double *d_acc, void *stream) {
+  if (nfft <= 0 || pad <= 0 || seg_begin < 0 || seg_end < seg_begin)
+    return fail(GDSP_ERR_INVALID, "bad Pwelch geometry");
+  if (seg_end == seg_begin) return GDSP_OK;
+  const int64_t stride = nfft - noverlap;
+  if ((seg_end - 1) * stride + nfft > n && seg_end > 1)
+    return fail(GDSP_ERR_INVALID, "segments exceed the signal");
+  const int64_t flen = pad > nfft ? pad : nfft;
+  int dev = 0;
+  STCHK(current_device(&dev));
+  hipStream_t s = (hipStream_t)stream;
+  if (!s) s = thread_stream(dev);
+  gdsp_plan *p = nullptr;
+  STCHK(get_plan(flen, &p));
+  const int64_t nseg = seg_end - seg_begin;
+  if (p->kind == KIND_LDS && p->log2n >= 4) {
+    // fused path: packed segment pairs, persistent workers over contiguous
+    // pair ranges (the 50 % overlap of consecutive pairs is re-read from L2)
+    const int64_t npairs = (nseg + 1) / 2;
+    int64_t target = 2048 * (int64_t)gdsp::pwelch_workers_per_block(p->log2n);
+    if (target > npairs) target = npairs;
+    const int64_t ppw = (npairs + target - 1) / target;
+    const int64_t nworkers = (npairs + ppw - 1) / ppw;
+    DevBuf part;
+    STCHK(part.alloc((size_t)nworkers * (size_t)flen * sizeof(double), s));
+    HIPCHK(gdsp::launch_pwelch(p->log2n, d_x, nfft, stride, seg_begin, seg_end, ppw, nworkers,
+                               d_win_seg, p->tw, (double *)part.p, s));
+    HIPCHK(gdsp::launch_reduce_partials((const double *)part.p, nworkers, flen, d_acc, s));
+    return GDSP_OK;
+  }
+  // materialised path: windowed segments as complex rows, batched FFT, |X|^2
+  int64_t chunk = ((int64_t)1 << 24) / flen;
+  if (chunk < 1) chunk = 1;
+  if (chunk > nseg) chunk = nseg;
+  DevBuf buf;
+  STCHK(buf.alloc((size_t)chunk * (size_t)flen * sizeof(cd), s));
+  for (int64_t s0 = seg_begin; s0 < seg_end; s0 += chunk) {
+    const int64_t ns = (seg_end - s0) < chunk ? (seg_end - s0) : chunk;
+    HIPCHK(gdsp::launch_segments_to_complex(d_x, nfft, flen, stride, s0, ns, d_win_seg,
+                                            (cd *)buf.p, s));
+    STCHK(exec_plan(p, buf.p, (cd *)buf.p, ns, false, gdsp::LOAD_COMPLEX, s));
+    HIPCHK(gdsp::launch_power_accumulate((const cd *)buf.p, ns, flen, d_acc, s));
+  }
+  return GDSP_OK;
+}
+
+int gdsp_pwelch_finalize(const double *acc, int64_t flen, int64_t nsegs, int64_t nfft,
+                         int64_t pad, const double *win_nfft, double fs, int scale_off,
+                         double *pxx, double *freqs) {
+  // spectral/pwelch.go:113-142
+  if (flen <= 0 || nfft <= 0 || pad <= 0 || !pxx || !freqs)
+    return fail(GDSP_ERR_INVALID, "bad argument");
+  const int64_t lp = pad / 2 + 1;
+  std::vector<double> hw;
+  if (!win_nfft) {
+    hw.resize((size_t)nfft);
+    hann_table(nfft, hw.data());
+    win_nfft = hw.data();
+  }
+  double norm = 0;
+  for (int64_t i = 0; i < nfft; ++i) norm += win_nfft[i] * win_nfft[i];
+  if (!scale_off) norm *= fs;
+  for (int64_t j = 0; j < lp; ++j) {
+    double d = 0.0;
+    if (nsegs > 0) {
+      d = 0.5 * (acc[j] + acc[(flen - j) % flen]) / (double)nsegs;
+      if (j > 0 && j < lp - 1) d *= 2;
+    }
+    pxx[j] = d / norm;
+  }
+  const double coef = fs / (double)pad;
+  for (int64_t j = 0; j < lp; ++j) freqs[j] = (double)j * coef;
+  return GDSP_OK;
+}
+
+int gdsp_pwelch(const double *x, int64_t n, double fs, int64_t nfft, int64_t pad,
+                int64_t noverlap, const double *win_seg, const double *win_nfft, int scale_off,
+                double *pxx, double *freqs, int64_t *lp_out) {
+  // spectral/pwelch.go:74-145
+  if (!lp_out) return fail(GDSP_ERR_INVALID, "NULL pointer");
+  *lp_out = 0;
+  if (n < 0) return fail(GDSP_ERR_INVALID, "negative size");
+  if (n == 0) return GDSP_OK;
+  if (nfft == 0) nfft = 256;
+  if (pad == 0) pad = nfft;
+  if (nfft < 0 || pad < 0) return fail(GDSP_ERR_INVALID, "negative NFFT/Pad");
+  const int64_t lx = n < nfft ? nfft : n;  // dsputils.ZeroPadF(x, nfft)
+  int64_t nsegs = 0;
+  STCHK(segment_count(lx, nfft, noverlap, &nsegs));
+  const int64_t flen = pad > nfft ? pad : nfft;
+  const int64_t lp = pad / 2 + 1;
+  std::vector<double> hseg, hnfft;
+  if (!win_seg) {
+    hseg.resize((size_t)flen);
+    hann_table(flen, hseg.data());
+    win_seg = hseg.data();
+  }
+  if (!win_nfft) {
+    hnfft.resize((size_t)nfft);
+    hann_table(nfft, hnfft.data());
+    win_nfft = hnfft.data();
+  }
+  std::vector<double> acc((size_t)flen, 0.0);
+  if (nsegs > 0) {
+    int dev = 0;
+    STCHK(current_device(&dev));
+    hipStream_t s = thread_stream(dev);
+    DevBuf dx, dw, dacc;
+    STCHK(dx.alloc((size_t)lx * sizeof(double), s));
+    STCHK(dw.alloc((size_t)flen * sizeof(double), s));
+    STCHK(dacc.alloc((size_t)flen * sizeof(double), s));
+    if (lx > n) HIPCHK(hipMemsetAsync(dx.p, 0, (size_t)lx * sizeof(double), s));
+    HIPCHK(hipMemcpyAsync(dx.p, x, (size_t)n * sizeof(double), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(dw.p, win_seg, (size_t)flen * sizeof(double), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(dacc.p, 0, (size_t)flen * sizeof(double), s));
+    STCHK(gdsp_pwelch_accumulate_device((const double *)dx.p, lx, nfft, pad, noverlap, 0, nsegs,
+                                        (const double *)dw.p, (double *)dacc.p, s));
+    HIPCHK(hipMemcpyAsync(acc.data(), dacc.p, (size_t)flen * sizeof(double),
+                          hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
+  STCHK(gdsp_pwelch_finalize(acc.data(), flen, nsegs, nfft, pad, win_nfft, fs, scale_off, pxx,
+                             freqs));
+  *lp_out = lp;
+  return GDSP_OK;
+}
+
+int gdsp_fill_uniform_device(double *d_out, int64_t count, uint64_t seed, uint64_t offset,
+                             void *stream) {
+  if (count < 0 || (!d_out && count)) return fail(GDSP_ERR_INVALID, "bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  if (!s) {
+    int dev = 0;
+    STCHK(current_device(&dev));
+    s = thread_stream(dev);
+  }
+  HIPCHK(gdsp::launch_fill_uniform(d_out, count, seed, offset, s));
+  return GDSP_OK;
+}
+
+}  // extern "C"

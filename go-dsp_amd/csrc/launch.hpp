@@ -1,0 +1,48 @@
+// launch.hpp — host launchers of the gfx950 kernels (fft_kernels.hip), used by
+// the C ABI layer (gdsp_api.hip). Internal to libgdspfft.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gdsp {
+
+struct cd;
+
+enum { LOAD_COMPLEX = 0, LOAD_REAL = 1 };
+
+// largest power-of-2 length handled by the one-kernel LDS transform / the
+// fused Bluestein kernel (M) / the fused Pwelch kernel
+constexpr int kMaxLdsLog2 = 14;
+
+hipError_t launch_fft_lds(int log2n, bool inv, int load, bool split, const void *in, cd *out,
+                          int64_t batch, const cd *tw, double scale, hipStream_t s);
+hipError_t launch_bluestein(int log2m, bool inv, const cd *in, cd *out, int64_t n,
+                            int64_t batch, const cd *twm, const cd *chirp, const cd *bhat,
+                            double scale, hipStream_t s);
+hipError_t launch_global_pass(int radix, bool conj_in, int load, bool conj_scale_out,
+                              const void *in, cd *out, const cd *tw, int log2n, int log2ns,
+                              int64_t batch, double scale, hipStream_t s);
+int pwelch_workers_per_block(int log2f);
+hipError_t launch_pwelch(int log2f, const double *x, int64_t nfft, int64_t stride,
+                         int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,
+                         const double *win, const cd *tw, double *partial, hipStream_t s);
+hipError_t launch_reduce_partials(const double *partial, int64_t nworkers, int64_t F, double *acc,
+                                  hipStream_t s);
+hipError_t launch_segments_to_complex(const double *x, int64_t nfft, int64_t flen, int64_t stride,
+                                      int64_t seg0, int64_t nseg, const double *win, cd *buf,
+                                      hipStream_t s);
+hipError_t launch_power_accumulate(const cd *buf, int64_t nseg, int64_t flen, double *acc,
+                                   hipStream_t s);
+hipError_t launch_transpose(const cd *in, cd *out, int64_t rows, int64_t cols, hipStream_t s);
+hipError_t launch_real_to_complex(const double *in, cd *out, int64_t count, hipStream_t s);
+hipError_t launch_chirp_premul(const cd *in, cd *a, int64_t n, int64_t m, int64_t batch,
+                               const cd *chirp, bool conj_in, hipStream_t s);
+hipError_t launch_bhat_mul_conj(cd *a, int64_t m, int64_t batch, const cd *bhat, hipStream_t s);
+hipError_t launch_chirp_postmul(const cd *a, cd *out, int64_t n, int64_t m, int64_t batch,
+                                const cd *chirp, bool inv, double scale, hipStream_t s);
+hipError_t launch_pointwise_mul(const cd *a, const cd *b, cd *out, int64_t count, hipStream_t s);
+hipError_t launch_scale(cd *a, int64_t count, double sc, hipStream_t s);
+hipError_t launch_fill_uniform(double *out, int64_t count, uint64_t seed, uint64_t offset,
+                               hipStream_t s);
+
+}  // namespace gdsp

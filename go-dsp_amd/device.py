@@ -1,0 +1,101 @@
+"""Device-pointer entry points of libgdspfft for callers that hold HBM-resident
+data in torch tensors (bench.py, distributed.py). torch provides device memory,
+streams and torch.distributed only; the transforms are the library's HIP
+kernels. Each call is stream-ordered on torch's current stream of the tensor's
+device (or the given stream)."""
+from __future__ import annotations
+
+import ctypes
+
+from . import _lib
+from ._lib import check, lib
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _stream_ptr(stream, device):
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class Plan:
+    """Cached device plan for transform length n on the current device
+    (gdsp_plan_create). kind: 0 trivial, 1 LDS Stockham, 2 multi-pass
+    Stockham, 3 fused Bluestein, 4 composed Bluestein."""
+
+    def __init__(self, n: int):
+        self.n = int(n)
+        self.handle = ctypes.c_void_p()
+        check(lib().gdsp_plan_create(self.n, ctypes.byref(self.handle)), "plan_create")
+        self.kind = int(lib().gdsp_plan_kind(self.handle))
+
+
+_plans: dict = {}
+
+
+def plan(n: int) -> Plan:
+    torch = _torch()
+    key = (torch.cuda.current_device(), int(n))
+    if key not in _plans:
+        _plans[key] = Plan(n)
+    return _plans[key]
+
+
+def fft_batch(x, out=None, inverse: bool = False, stream=None):
+    """Batched FFT/IFFT of the rows of a (batch, n) complex128 CUDA tensor."""
+    torch = _torch()
+    assert x.is_cuda and x.dtype == torch.complex128 and x.dim() == 2 and x.is_contiguous()
+    if out is None:
+        out = torch.empty_like(x)
+    assert out.shape == x.shape and out.dtype == x.dtype and out.is_contiguous()
+    with torch.cuda.device(x.device):
+        p = plan(x.shape[1])
+        check(lib().gdsp_fft_batch_device(p.handle, _ptr(x), _ptr(out), x.shape[0], int(inverse),
+                                          _stream_ptr(stream, x.device)), "fft_batch_device")
+    return out
+
+
+def fft2(x, out=None, inverse: bool = False, work=None, stream=None):
+    """FFT2/IFFT2 of a (rows, cols) complex128 CUDA tensor."""
+    torch = _torch()
+    assert x.is_cuda and x.dtype == torch.complex128 and x.dim() == 2 and x.is_contiguous()
+    if out is None:
+        out = torch.empty_like(x)
+    with torch.cuda.device(x.device):
+        wp = _ptr(work) if work is not None else ctypes.c_void_p()
+        check(lib().gdsp_fft2_device(_ptr(x), _ptr(out), x.shape[0], x.shape[1], int(inverse), wp,
+                                     _stream_ptr(stream, x.device)), "fft2_device")
+    return out
+
+
+def fill_uniform(t, seed: int, offset: int = 0, stream=None):
+    """Fill a float64 (or complex128, as interleaved pairs) CUDA tensor with the
+    counter-based uniform[-1,1) generator."""
+    torch = _torch()
+    assert t.is_cuda and t.is_contiguous()
+    count = t.numel() * (2 if t.dtype == torch.complex128 else 1)
+    with torch.cuda.device(t.device):
+        check(lib().gdsp_fill_uniform_device(_ptr(t), count, seed, offset,
+                                             _stream_ptr(stream, t.device)), "fill_uniform")
+    return t
+
+
+def pwelch_accumulate(x, nfft: int, pad: int, noverlap: int, seg_begin: int, seg_end: int,
+                      win_seg, acc, stream=None):
+    """Adds the per-bin power sums of segments [seg_begin, seg_end) of the
+    float64 CUDA signal x into acc (float64, max(pad, nfft) entries)."""
+    torch = _torch()
+    assert x.is_cuda and x.dtype == torch.float64 and acc.dtype == torch.float64
+    with torch.cuda.device(x.device):
+        check(lib().gdsp_pwelch_accumulate_device(
+            _ptr(x), x.numel(), nfft, pad, noverlap, seg_begin, seg_end, _ptr(win_seg), _ptr(acc),
+            _stream_ptr(stream, x.device)), "pwelch_accumulate")
+    return acc

@@ -1,0 +1,148 @@
+"""Host mirror of go-dsp's `fft` package (fft/fft.go, fft/radix2.go,
+fft/bluestein.go) over the libgdspfft C ABI. Same names, argument meaning and
+panics as the Go API; slices become numpy arrays. Every transform runs on the
+GPU (gfx950 kernels); nothing here computes a transform on the CPU.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from ._lib import Panic, check, lib
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(_lib._P)
+
+
+def _as_c(x) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(x, dtype=np.complex128).reshape(-1))
+
+
+def _as_f(x) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(x, dtype=np.float64).reshape(-1))
+
+
+def FFT(x) -> np.ndarray:
+    """fft.FFT — fft/fft.go:72-87. Returns a new array; x is not modified."""
+    x = _as_c(x)
+    out = np.empty_like(x)
+    check(lib().gdsp_fft(_p(x), _p(out), x.size), "FFT")
+    return out
+
+
+def IFFT(x) -> np.ndarray:
+    """fft.IFFT — fft/fft.go:35-52. Panics (index out of range) on len 0."""
+    x = _as_c(x)
+    if x.size == 0:
+        raise Panic(_lib.GDSP_ERR_EMPTY, "runtime error: index out of range [0] with length 0")
+    out = np.empty_like(x)
+    check(lib().gdsp_ifft(_p(x), _p(out), x.size), "IFFT")
+    return out
+
+
+def FFTReal(x) -> np.ndarray:
+    """fft.FFTReal — fft/fft.go:25-27 (full N-point complex spectrum)."""
+    x = _as_f(x)
+    out = np.empty(x.size, np.complex128)
+    check(lib().gdsp_fft_real(_p(x), _p(out), x.size), "FFTReal")
+    return out
+
+
+def IFFTReal(x) -> np.ndarray:
+    """fft.IFFTReal — fft/fft.go:30-32."""
+    x = _as_f(x)
+    if x.size == 0:
+        raise Panic(_lib.GDSP_ERR_EMPTY, "runtime error: index out of range [0] with length 0")
+    out = np.empty(x.size, np.complex128)
+    check(lib().gdsp_ifft_real(_p(x), _p(out), x.size), "IFFTReal")
+    return out
+
+
+def Convolve(x, y) -> np.ndarray:
+    """fft.Convolve — fft/fft.go:55-69."""
+    x, y = _as_c(x), _as_c(y)
+    if x.size != y.size:
+        raise Panic(_lib.GDSP_ERR_UNEQUAL, "arrays not of equal size")
+    out = np.empty_like(x)
+    check(lib().gdsp_convolve(_p(x), _p(y), _p(out), x.size), "Convolve")
+    return out
+
+
+def FFTBatch(x, inverse: bool = False) -> np.ndarray:
+    """Additive batched entry point: FFT (or IFFT) of every row
+    of a (batch, n) complex array, in one GPU launch."""
+    x = np.ascontiguousarray(np.asarray(x, dtype=np.complex128))
+    if x.ndim != 2:
+        raise ValueError("FFTBatch expects a 2-D (batch, n) array")
+    out = np.empty_like(x)
+    check(lib().gdsp_fft_batch(_p(x), _p(out), x.shape[1], x.shape[0], int(inverse)), "FFTBatch")
+    return out
+
+
+def FFTRealBatch(x) -> np.ndarray:
+    """FFTReal of every row of a (batch, n) float64 array."""
+    x = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    if x.ndim != 2:
+        raise ValueError("FFTRealBatch expects a 2-D (batch, n) array")
+    out = np.empty(x.shape, np.complex128)
+    check(lib().gdsp_fft_real_batch(_p(x), _p(out), x.shape[1], x.shape[0]), "FFTRealBatch")
+    return out
+
+
+def _matrix(x, dtype) -> np.ndarray:
+    """Flatten [][]T after the reference's checks (fft/fft.go:124-136)."""
+    if isinstance(x, np.ndarray):
+        if x.ndim != 2 or x.shape[0] == 0:
+            if x.ndim == 2 or x.size == 0:
+                raise Panic(_lib.GDSP_ERR_EMPTY, "empty input array")
+            raise ValueError("expected a 2-D matrix")
+        return np.ascontiguousarray(x, dtype=dtype)
+    rows = list(x)
+    if len(rows) == 0:
+        raise Panic(_lib.GDSP_ERR_EMPTY, "empty input array")
+    cols = len(rows[0])
+    for r in rows:
+        if len(r) != cols:
+            raise Panic(_lib.GDSP_ERR_RAGGED, "ragged input array")
+    return np.ascontiguousarray(np.asarray(rows, dtype=dtype).reshape(len(rows), cols))
+
+
+def _fft2(x, real: bool, inverse: bool) -> np.ndarray:
+    m = _matrix(x, np.float64 if real else np.complex128)
+    out = np.empty(m.shape, np.complex128)
+    fn = lib().gdsp_fft2_real if real else lib().gdsp_fft2
+    check(fn(_p(m), _p(out), m.shape[0], m.shape[1], int(inverse)), "FFT2")
+    return out
+
+
+def FFT2(x) -> np.ndarray:
+    """fft.FFT2 — fft/fft.go:109-111 (computeFFT2 :123-154)."""
+    return _fft2(x, False, False)
+
+
+def IFFT2(x) -> np.ndarray:
+    """fft.IFFT2 — fft/fft.go:119-121."""
+    return _fft2(x, False, True)
+
+
+def FFT2Real(x) -> np.ndarray:
+    """fft.FFT2Real — fft/fft.go:104-106."""
+    return _fft2(x, True, False)
+
+
+def IFFT2Real(x) -> np.ndarray:
+    """fft.IFFT2Real — fft/fft.go:114-116."""
+    return _fft2(x, True, True)
+
+
+def SetWorkerPoolSize(n: int) -> None:
+    """fft.SetWorkerPoolSize — fft/fft.go:95-101 (recorded; the GPU path has no
+    goroutine pool)."""
+    lib().gdsp_set_worker_pool_size(int(n))
+
+
+def EnsureRadix2Factors(input_len: int) -> None:
+    """fft.EnsureRadix2Factors — fft/radix2.go:35-37: pre-build the device plan
+    (twiddle table, and for non-powers of 2 the Bluestein tables)."""
+    check(lib().gdsp_ensure_plan(int(input_len)), "EnsureRadix2Factors")

@@ -1,0 +1,180 @@
+/*
+ * gdsp_fft.h — C ABI of libgdspfft, the MI355X (gfx950) batched-FFT engine for
+ * the go-dsp hot path (maddyblue/go-dsp: fft/, spectral/Pwelch, window/Hann).
+ *
+ * This is the drop-in boundary: each entry point names the reference Go
+ * function it replaces (file:line under maddyblue/go-dsp). A Go maintainer
+ * binds these through cgo; tests bind them via ctypes.
+ *
+ * Conventions (mirroring the reference):
+ *  - complex data are interleaved (re, im) IEEE float64 pairs, i.e. the memory
+ *    layout of Go []complex128 and of C99 double _Complex;
+ *  - inputs are never modified; outputs are caller-owned buffers that the
+ *    library fills (Go allocates the result slice, C fills it);
+ *  - the library never retains a caller pointer after returning (cgo rule);
+ *  - every compute runs on the GPU. There is no CPU fallback: without a usable
+ *    HIP device the calls return GDSP_ERR_NO_DEVICE;
+ *  - the reference's panics become status codes; the Go shim re-panics with
+ *    the reference's message (gdsp_status_string);
+ *  - host-pointer entry points are synchronous and thread-safe; device-pointer
+ *    entry points ("_device") are stream-ordered on the given hipStream_t
+ *    (passed as void*, NULL = the library's per-thread stream) and run on the
+ *    calling thread's current HIP device.
+ */
+#ifndef GDSP_FFT_H
+#define GDSP_FFT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status ------------------------------------------------------------- */
+typedef enum {
+  GDSP_OK = 0,
+  GDSP_ERR_INVALID = 1,        /* bad argument (negative size, NULL pointer, ...) */
+  GDSP_ERR_UNEQUAL = 2,        /* "arrays not of equal size"   fft/fft.go:57 */
+  GDSP_ERR_EMPTY = 3,          /* "empty input array"          fft/fft.go:126;
+                                  IFFT of len 0 (index out of range, fft/fft.go:40) */
+  GDSP_ERR_RAGGED = 4,         /* "ragged input array"         fft/fft.go:133 */
+  GDSP_ERR_DIVIDE_BY_ZERO = 5, /* Segment stride 0 (integer divide, spectral.go:31) */
+  GDSP_ERR_NO_DEVICE = 6,      /* no HIP device / runtime error at init */
+  GDSP_ERR_HIP = 7,            /* HIP runtime error during a call */
+  GDSP_ERR_NOMEM = 8,          /* device or host allocation failed */
+  GDSP_ERR_UNSUPPORTED = 9     /* size beyond what this build implements */
+} gdsp_status;
+
+/* Reference panic message (or a description) for a status code. */
+const char *gdsp_status_string(int status);
+/* Detail of the last error raised on the calling thread ("" if none). */
+const char *gdsp_last_error(void);
+/* Library version string. */
+const char *gdsp_version(void);
+/* Number of visible HIP devices (0 without a GPU; never initialises a context
+ * beyond hipGetDeviceCount). */
+int gdsp_device_count(void);
+
+/* ---- fft package: host pointers, synchronous ----------------------------- */
+
+/* fft.FFT — fft/fft.go:72-87. n <= 1 copies; power of 2 → Stockham radix-16
+ * kernels (reference: radix2FFT, fft/radix2.go:80-154); otherwise Bluestein
+ * (fft/bluestein.go:68-94). x, out: n complex128. */
+int gdsp_fft(const double *x, double *out, int64_t n);
+
+/* fft.IFFT — fft/fft.go:35-52. n == 0 → GDSP_ERR_EMPTY (reference panics). */
+int gdsp_ifft(const double *x, double *out, int64_t n);
+
+/* fft.FFTReal — fft/fft.go:25-27. x: n float64; out: n complex128 (full
+ * spectrum, as the reference returns). */
+int gdsp_fft_real(const double *x, double *out, int64_t n);
+
+/* fft.IFFTReal — fft/fft.go:30-32. */
+int gdsp_ifft_real(const double *x, double *out, int64_t n);
+
+/* fft.Convolve — fft/fft.go:55-69 (IFFT(FFT(x)·FFT(y))). The reference's
+ * length check ("arrays not of equal size") is the caller's: both are n. */
+int gdsp_convolve(const double *x, const double *y, double *out, int64_t n);
+
+/* Additive batched entry point (no reference equivalent): the
+ * same transform as fft.FFT / fft.IFFT applied to `batch` contiguous rows of n
+ * complex128. inverse != 0 → IFFT semantics. */
+int gdsp_fft_batch(const double *x, double *out, int64_t n, int64_t batch, int inverse);
+
+/* Real-input batch (FFTReal per row): x is batch*n float64. */
+int gdsp_fft_real_batch(const double *x, double *out, int64_t n, int64_t batch);
+
+/* fft.FFT2 / fft.IFFT2 — fft/fft.go:109-121 → computeFFT2 :123-154. x is a
+ * row-major rows×cols complex128 matrix (the Go shim flattens [][]complex128
+ * after checking raggedness). rows == 0 → GDSP_ERR_EMPTY. */
+int gdsp_fft2(const double *x, double *out, int64_t rows, int64_t cols, int inverse);
+
+/* fft.FFT2Real / fft.IFFT2Real — fft/fft.go:104-107, :114-117. x: rows×cols
+ * float64. */
+int gdsp_fft2_real(const double *x, double *out, int64_t rows, int64_t cols, int inverse);
+
+/* fft.EnsureRadix2Factors — fft/radix2.go:35-37: pre-build (and cache) the
+ * device plan for length n on the current device. Works for any n >= 2. */
+int gdsp_ensure_plan(int64_t n);
+
+/* fft.SetWorkerPoolSize — fft/fft.go:95-101. The GPU path has no worker
+ * pool; the value is recorded (n < 0 → 0) and reported by
+ * gdsp_worker_pool_size for API parity. */
+void gdsp_set_worker_pool_size(int n);
+int gdsp_worker_pool_size(void);
+
+/* ---- spectral package ------------------------------------------------------ */
+
+/* spectral.Segment — spectral/spectral.go:22-33: number of segments of length
+ * `size` with `noverlap` overlap in a signal of length lx. Writes *count. */
+int gdsp_segment_count(int64_t lx, int64_t size, int64_t noverlap, int64_t *count);
+
+/* spectral.Pwelch — spectral/pwelch.go:74-145.
+ * x: n float64 samples. nfft/pad/noverlap as PwelchOptions (0 = defaults:
+ * nfft 256, pad nfft). Go's PwelchOptions.Window is a Go func, so the shim
+ * passes its tables: win_seg = wf(max(pad, nfft)) — the window the reference
+ * applies to each zero-padded segment (pwelch.go:108-109, window.go:25-29) —
+ * and win_nfft = wf(nfft) for the normalisation (pwelch.go:124). NULL for
+ * either selects window.Hann (the default, pwelch.go:89-91).
+ * pxx, freqs: caller buffers of pad/2+1 float64; *lp_out receives the count
+ * (0 for empty x, as the reference returns empty slices). */
+int gdsp_pwelch(const double *x, int64_t n, double fs, int64_t nfft, int64_t pad,
+                int64_t noverlap, const double *win_seg, const double *win_nfft,
+                int scale_off, double *pxx, double *freqs, int64_t *lp_out);
+
+/* window.Hann — window/window.go:62-76, as a host table generator used by the
+ * shim for the default window (L float64 written to out). */
+int gdsp_window_hann(int64_t L, double *out);
+
+/* ---- device-pointer API (stream-ordered; multi-GPU building blocks) ---------- */
+
+typedef struct gdsp_plan gdsp_plan;
+
+/* Create / fetch the cached plan for transform length n on the current
+ * device. Plans are owned by the library cache; destroy is a no-op for cached
+ * plans and exists for API symmetry. */
+int gdsp_plan_create(int64_t n, gdsp_plan **plan);
+int gdsp_plan_destroy(gdsp_plan *plan);
+/* Which algorithm a plan runs: 0 trivial (n<=1), 1 one-kernel LDS Stockham,
+ * 2 multi-pass global Stockham (large power of 2), 3 fused Bluestein. */
+int gdsp_plan_kind(const gdsp_plan *plan);
+
+/* Batched C2C on device buffers: d_in/d_out hold batch*n complex128 (may
+ * alias only if equal). inverse != 0 → IFFT semantics (1/n scaling). */
+int gdsp_fft_batch_device(const gdsp_plan *plan, const void *d_in, void *d_out,
+                          int64_t batch, int inverse, void *stream);
+
+/* FFT2/IFFT2 on a device rows×cols complex128 matrix. d_work: scratch of
+ * rows*cols complex128 (may be NULL: the library allocates stream-ordered). */
+int gdsp_fft2_device(const void *d_in, void *d_out, int64_t rows, int64_t cols,
+                     int inverse, void *d_work, void *stream);
+
+/* Pwelch partial accumulation over segments [seg_begin, seg_end) of a device
+ * signal d_x (n float64, sample 0 = sample 0 of segment 0). Adds into
+ * d_acc[0..flen) (flen = max(pad, nfft)) the per-bin sums S_k of |Z_k|² over
+ * the packed segment pairs; gdsp_pwelch_finalize turns the summed
+ * accumulators (over every shard / rank) into Pxx. d_win_seg: flen float64
+ * window table on the device. d_acc must be zeroed by the caller before the
+ * first call. */
+int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, int64_t pad,
+                                  int64_t noverlap, int64_t seg_begin, int64_t seg_end,
+                                  const double *d_win_seg, double *d_acc, void *stream);
+
+/* Host finalisation (spectral/pwelch.go:113-142): from the summed
+ * accumulators acc[0..flen) over all nsegs segments produce
+ * pxx[j] = c_j * (acc[j] + acc[(flen-j)%flen]) / 2 / nsegs / norm and
+ * freqs[j] = j*fs/pad for j < pad/2+1. */
+int gdsp_pwelch_finalize(const double *acc, int64_t flen, int64_t nsegs, int64_t nfft,
+                         int64_t pad, const double *win_nfft, double fs, int scale_off,
+                         double *pxx, double *freqs);
+
+/* Device synthetic input: d_out[i] = uniform[-1,1) from splitmix64(seed,
+ * offset + i), i < count (float64). Identical to the host generator the tests
+ * use; lets the bench generate inputs in HBM without a PCIe copy. */
+int gdsp_fill_uniform_device(double *d_out, int64_t count, uint64_t seed, uint64_t offset,
+                             void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GDSP_FFT_H */

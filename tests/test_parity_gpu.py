@@ -1,0 +1,247 @@
+"""GPU parity: the HIP path through the C ABI against the oracle (CPU
+restatement of the reference) and the reference's own golden vectors.
+
+Tolerances: the north star's 1e-9 normwise relative for every
+complex128 result; the reference's known-answer tables with its own
+Float64Equal (1e-8, dsputils/compare.go:94-96) because their constants carry
+8-9 digits. Measured errors are ~1e-15 (powers of 2) and ~1e-13 (Bluestein)."""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import cpx, nrel, row_nrel
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-9  # north star: within 1e-9 relative for complex128
+
+
+def f64eq(a, b):
+    if abs(a - b) <= 1e-8:
+        return True
+    return b != 0 and abs(1 - a / b) <= 1e-8
+
+
+def close_c(a, b):
+    return len(a) == len(b) and all(f64eq(x.real, y.real) and f64eq(x.imag, y.imag)
+                                    for x, y in zip(a, b))
+
+
+def close_f(a, b):
+    return len(a) == len(b) and all(f64eq(x, y) for x, y in zip(a, b))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu(gdsp):
+    if gdsp.device_count() < 1:
+        pytest.fail("gpu test without a visible HIP device")
+
+
+# ---- reference known answers (fft/fft_test.go, spectral/*_test.go) ----------
+def test_TestFFT(gdsp, refvec):
+    for case in refvec["fftTests"]:
+        out = cpx(case["out"])
+        assert close_c(gdsp.fft.FFTReal(case["in"]), out), case
+        assert close_c(gdsp.fft.IFFT(out), np.asarray(case["in"], np.complex128)), case
+
+
+def test_TestFFT2(gdsp, refvec):
+    for case in refvec["fft2Tests"]:
+        out = [cpx(r) for r in case["out"]]
+        y = gdsp.fft.FFT2Real(case["in"])
+        assert all(close_c(a, b) for a, b in zip(y, out))
+        yi = gdsp.fft.IFFT2(out)
+        x = np.asarray(case["in"], np.complex128)
+        assert all(close_c(a, b) for a, b in zip(yi, x))
+
+
+def test_ExampleFFTReal(gdsp, refvec):
+    a = [math.sin(2 * math.pi * n / 8.0) + 0.5 * math.sin(2 * math.pi * n / 4.0 + 3 * math.pi / 4)
+         for n in range(8)]
+    X = gdsp.fft.FFTReal(a)
+    for e in refvec["exampleFFTReal"]:
+        z = X[e["k"]]
+        r, th = abs(z), math.degrees(math.atan2(z.imag, z.real))
+        if f64eq(r, 0):
+            th = 0
+        assert f"{r:.1f}" == f"{e['mag']:.1f}" and f"{th:.1f}" == f"{e['deg']:.1f}"
+
+
+def test_TestFFTMulti(gdsp, oracle):
+    # fft/fft_test.go:251-259 (no assertion in the reference; we check it)
+    N = 1 << 8
+    a = np.arange(N) / N
+    assert nrel(gdsp.fft.FFT(a), oracle.fft(a)) < TOL
+
+
+def test_TestPwelch(gdsp, refvec):
+    for c in refvec["pwelchTests"]:
+        p, f = gdsp.spectral.Pwelch(c["x"], c["fs"], gdsp.spectral.PwelchOptions())
+        assert close_f(p, c["p"]) and close_f(f, c["freqs"])
+
+
+# ---- full-precision fixtures and the oracle ----------------------------------
+def test_golden_fft(gdsp, golden_fft):
+    for key in sorted(golden_fft):
+        if not key.startswith("fft_in_"):
+            continue
+        n = key[len("fft_in_"):]
+        x = golden_fft[key]
+        assert nrel(gdsp.fft.FFT(x), golden_fft[f"fft_out_{n}"]) < TOL, n
+        assert nrel(gdsp.fft.IFFT(x), golden_fft[f"ifft_out_{n}"]) < TOL, n
+
+
+def test_golden_fft2(gdsp, golden_fft):
+    for key in sorted(golden_fft):
+        if not key.startswith("fft2_in_"):
+            continue
+        s = key[len("fft2_in_"):]
+        x = golden_fft[key]
+        assert nrel(gdsp.fft.FFT2(x), golden_fft[f"fft2_out_{s}"]) < TOL, s
+        assert nrel(gdsp.fft.IFFT2(x), golden_fft[f"ifft2_out_{s}"]) < TOL, s
+
+
+SIZES = [2, 3, 4, 5, 6, 7, 8, 9, 15, 16, 17, 31, 32, 33, 64, 100, 128, 255, 256, 512, 1000,
+         1024, 2048, 3000, 4096, 4097, 5000, 8192, 10000, 16384, 32768, 65536, 1 << 20]
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_fft_sizes_vs_oracle(gdsp, oracle, n):
+    rng = np.random.default_rng(n)
+    batch = 3 if n <= 65536 else 1
+    x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
+    y = gdsp.fft.FFTBatch(x)
+    yi = gdsp.fft.FFTBatch(x, inverse=True)
+    ref = oracle.fft_rows(x)
+    refi = oracle.ifft_rows(x)
+    assert row_nrel(y, ref) < TOL
+    assert row_nrel(yi, refi) < TOL
+    # single-call API for the first row
+    assert nrel(gdsp.fft.FFT(x[0]), ref[0]) < TOL
+
+
+@pytest.mark.parametrize("n", [1, 2, 8, 1024, 3000, 4096])
+def test_fft_real(gdsp, oracle, n):
+    rng = np.random.default_rng(7 + n)
+    x = rng.uniform(-1, 1, (4, n))
+    assert row_nrel(gdsp.fft.FFTRealBatch(x), oracle.fft_rows(x.astype(np.complex128))) < TOL
+    assert nrel(gdsp.fft.FFTReal(x[0]), oracle.fft_real(x[0])) < TOL
+    assert nrel(gdsp.fft.IFFTReal(x[0]), oracle.ifft_real(x[0])) < TOL
+
+
+def test_batch_4096_vs_oracle(gdsp, oracle):
+    # the headline configuration's transform on a 1024-row sample
+    x = oracle.fill_uniform(2 * 4096 * 1024, 0x5EED).view(np.complex128).reshape(1024, 4096)
+    y = gdsp.fft.FFTBatch(x)
+    assert row_nrel(y, oracle.fft_rows(x)) < TOL
+    assert row_nrel(gdsp.fft.FFTBatch(y, inverse=True), x) < TOL
+
+
+def test_batch_3000_vs_oracle(gdsp, oracle):
+    x = oracle.fill_uniform(2 * 3000 * 256, 0x5EED, 11).view(np.complex128).reshape(256, 3000)
+    assert row_nrel(gdsp.fft.FFTBatch(x), oracle.fft_rows(x)) < TOL
+    assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL
+
+
+@pytest.mark.parametrize("n", [2, 5, 16, 1000, 4096])
+def test_convolve(gdsp, oracle, n):
+    rng = np.random.default_rng(n)
+    x = rng.standard_normal(n) + 1j * rng.standard_normal(n)
+    y = rng.standard_normal(n) + 1j * rng.standard_normal(n)
+    assert nrel(gdsp.fft.Convolve(x, y), oracle.convolve(x, y)) < TOL
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (1, 8), (8, 1), (2, 3), (3, 5), (16, 16), (64, 32),
+                                   (6, 10), (100, 7), (128, 256), (512, 300), (1024, 1024)])
+def test_fft2_vs_oracle(gdsp, oracle, shape):
+    rng = np.random.default_rng(shape[0] * 1000 + shape[1])
+    x = rng.uniform(-1, 1, shape) + 1j * rng.uniform(-1, 1, shape)
+    assert nrel(gdsp.fft.FFT2(x), oracle.fft2(x)) < TOL
+    assert nrel(gdsp.fft.IFFT2(x), oracle.fft2(x, inverse=True)) < TOL
+    xr = rng.uniform(-1, 1, shape)
+    assert nrel(gdsp.fft.FFT2Real(xr), oracle.fft2(xr)) < TOL
+    assert nrel(gdsp.fft.IFFT2Real(xr), oracle.fft2(xr, inverse=True)) < TOL
+
+
+# ---- Pwelch ---------------------------------------------------------------------
+def test_pwelch_golden(gdsp, golden_pwelch):
+    x = golden_pwelch["x"]
+    S = gdsp.spectral
+    cases = {
+        "nfft4096_ov2048": (1.0, S.PwelchOptions(NFFT=4096, Noverlap=2048)),
+        "nfft1024_ov0_fs2": (2.0, S.PwelchOptions(NFFT=1024)),
+        "nfft512_ov256_pad1024": (1.0, S.PwelchOptions(NFFT=512, Noverlap=256, Pad=1024)),
+        "nfft256_hamming_scaleoff": (3.0, S.PwelchOptions(NFFT=256, Noverlap=128,
+                                                          Window=gdsp.window.Hamming,
+                                                          Scale_off=True)),
+    }
+    for name, (fs, o) in cases.items():
+        p, f = S.Pwelch(x, fs, o)
+        assert nrel(p, golden_pwelch[f"{name}_pxx"]) < TOL, name
+        assert nrel(f, golden_pwelch[f"{name}_freqs"]) == 0.0, name
+
+
+WINDOWS = {"hann": "Hann", "hamming": "Hamming", "rectangular": "Rectangular",
+           "bartlett": "Bartlett", "flattop": "FlatTop", "blackman": "Blackman"}
+
+
+@pytest.mark.parametrize("n,nfft,nov,pad,win", [
+    (100, 0, 0, 0, "hann"),            # default options, zero-padded single segment
+    (5000, 256, 128, 0, "hann"),
+    (5001, 256, 100, 0, "hamming"),    # odd segment count
+    (10000, 1024, 512, 4096, "blackman"),
+    (10000, 1024, 0, 512, "hann"),     # Pad < NFFT quirk (pwelch.go:108 vs :124)
+    (7777, 300, 150, 0, "bartlett"),   # non-power-of-2 segment (materialised path)
+    (4000, 8, 4, 0, "flattop"),        # tiny segments
+    (1 << 16, 16384, 8192, 0, "hann"),
+    (4096, 4096, 0, 0, "rectangular"),  # exactly one segment
+])
+def test_pwelch_vs_oracle(gdsp, oracle, n, nfft, nov, pad, win):
+    rng = np.random.default_rng(n + nfft)
+    x = rng.standard_normal(n)
+    o = gdsp.spectral.PwelchOptions(NFFT=nfft, Noverlap=nov, Pad=pad,
+                                    Window=getattr(gdsp.window, WINDOWS[win]))
+    p, f = gdsp.spectral.Pwelch(x, 2.5, o)
+    pr, fr = oracle.pwelch(x, 2.5, nfft=nfft, pad=pad, noverlap=nov, window_kind=win)
+    assert nrel(p, pr) < TOL
+    assert nrel(f, fr) == 0.0
+
+
+# ---- edge cases and conventions --------------------------------------------------
+def test_edge_cases(gdsp):
+    F = gdsp.fft
+    assert F.FFT([]).size == 0
+    assert F.FFT([3 + 4j])[0] == 3 + 4j
+    assert F.IFFT([3 + 4j])[0] == 3 + 4j
+    with pytest.raises(gdsp.Panic):
+        F.IFFT([])
+    with pytest.raises(gdsp.Panic, match="arrays not of equal size"):
+        F.Convolve([1, 2], [1, 2, 3])
+    with pytest.raises(gdsp.Panic, match="empty input array"):
+        F.FFT2([])
+    with pytest.raises(gdsp.Panic, match="ragged input array"):
+        F.FFT2([[1, 2], [3]])
+    p, f = gdsp.spectral.Pwelch([], 0, gdsp.spectral.PwelchOptions())
+    assert p.size == 0 and f.size == 0
+    with pytest.raises(gdsp.Panic):
+        gdsp.spectral.Pwelch([1.0], 1, None)
+
+
+def test_inputs_not_mutated(gdsp):
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal(3000) + 1j * rng.standard_normal(3000)
+    keep = x.copy()
+    gdsp.fft.FFT(x)
+    gdsp.fft.IFFT(x)
+    assert np.array_equal(x, keep)
+
+
+def test_plan_kinds(gdsp):
+    import torch  # noqa: F401  (device plumbing)
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    assert D.plan(1).kind == 0
+    assert D.plan(4096).kind == 1
+    assert D.plan(1 << 16).kind == 2
+    assert D.plan(3000).kind == 3
+    assert D.plan(10000).kind == 4
