@@ -89,6 +89,21 @@ def header_functions() -> list[str]:
     return sorted(set(re.findall(r"\b(gdsp_[a-z0-9_]+)\s*\(", src)))
 
 
+def _preload_torch_hip() -> None:
+    """torch ships its own libamdhip64.so (same SONAME, libamdhip64.so.7). If
+    libgdspfft.so were loaded first, /opt/rocm's runtime would be mapped and
+    torch would then load a second HIP runtime into the process and fail to
+    initialise. Loading torch first makes libgdspfft bind to the one runtime
+    torch uses, so device pointers and streams are shared. Skipped when torch
+    is absent (plain C-ABI users) or GDSP_NO_TORCH_PRELOAD is set."""
+    if os.environ.get("GDSP_NO_TORCH_PRELOAD"):
+        return
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def lib() -> ctypes.CDLL:
     global _lib
     if _lib is None:
@@ -96,6 +111,7 @@ def lib() -> ctypes.CDLL:
             raise ImportError(
                 f"libgdspfft.so not built ({LIB_PATH}); run __graft_entry__.build() "
                 "or make -C go-dsp_amd/csrc")
+        _preload_torch_hip()
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             f = getattr(L, name)

@@ -109,6 +109,81 @@ struct DevBuf {
   }
 };
 
+
+// Host <-> device copies through library-owned pinned staging buffers (two
+// halves, double-buffered). The caller's memory is only touched by memcpy on
+// the host, so pageable (Go / numpy) buffers never reach the HIP runtime and
+// no pointer is retained after the call returns (cgo rule).
+struct Staging {
+  char *buf = nullptr;
+  size_t half = 0;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  ~Staging() {
+    if (buf) (void)hipHostFree(buf);
+    for (auto &e : ev)
+      if (e) (void)hipEventDestroy(e);
+  }
+};
+
+constexpr size_t kStagingHalf = (size_t)32 << 20;
+
+int staging_get(Staging **out) {
+  thread_local std::map<int, Staging> per_dev;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(GDSP_ERR_NO_DEVICE, "hipGetDevice failed");
+  Staging &st = per_dev[dev];
+  if (!st.buf) {
+    HIPCHK(hipHostMalloc((void **)&st.buf, 2 * kStagingHalf, hipHostMallocDefault));
+    st.half = kStagingHalf;
+    for (auto &e : st.ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  *out = &st;
+  return GDSP_OK;
+}
+
+int copy_h2d(void *dst, const void *src, size_t bytes, hipStream_t s) {
+  Staging *st = nullptr;
+  STCHK(staging_get(&st));
+  bool used[2] = {false, false};
+  int h = 0;
+  for (size_t off = 0; off < bytes; off += st->half, h ^= 1) {
+    const size_t c = bytes - off < st->half ? bytes - off : st->half;
+    char *stg = st->buf + (size_t)h * st->half;
+    if (used[h]) HIPCHK(hipEventSynchronize(st->ev[h]));
+    memcpy(stg, (const char *)src + off, c);
+    HIPCHK(hipMemcpyAsync((char *)dst + off, stg, c, hipMemcpyHostToDevice, s));
+    HIPCHK(hipEventRecord(st->ev[h], s));
+    used[h] = true;
+  }
+  // the staging halves stay referenced by queued copies until they complete
+  for (int i = 0; i < 2; ++i)
+    if (used[i]) HIPCHK(hipEventSynchronize(st->ev[i]));
+  return GDSP_OK;
+}
+
+int copy_d2h(void *dst, const void *src, size_t bytes, hipStream_t s) {
+  Staging *st = nullptr;
+  STCHK(staging_get(&st));
+  const size_t nchunk = (bytes + st->half - 1) / st->half;
+  auto issue = [&](size_t i) -> int {
+    const size_t off = i * st->half;
+    const size_t c = bytes - off < st->half ? bytes - off : st->half;
+    HIPCHK(hipMemcpyAsync(st->buf + (i & 1) * st->half, (const char *)src + off, c,
+                          hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(st->ev[i & 1], s));
+    return GDSP_OK;
+  };
+  if (nchunk) STCHK(issue(0));
+  for (size_t i = 0; i < nchunk; ++i) {
+    if (i + 1 < nchunk) STCHK(issue(i + 1));
+    HIPCHK(hipEventSynchronize(st->ev[i & 1]));
+    const size_t off = i * st->half;
+    const size_t c = bytes - off < st->half ? bytes - off : st->half;
+    memcpy((char *)dst + off, st->buf + (i & 1) * st->half, c);
+  }
+  return GDSP_OK;
+}
+
 }  // namespace
 
 enum PlanKind { KIND_TRIVIAL = 0, KIND_LDS = 1, KIND_GLOBAL = 2, KIND_BLUESTEIN = 3,
@@ -138,7 +213,7 @@ int exec_plan(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool i
               hipStream_t s);
 
 // T_n[k] = exp(-2 pi i k/n), evaluated in long double and rounded once.
-int upload_twiddles(int64_t n, cd **dst) {
+int upload_twiddles(int dev, int64_t n, cd **dst) {
   std::vector<cd> h((size_t)n);
   for (int64_t k = 0; k < n; ++k) {
     long double a = -2.0L * 3.141592653589793238462643383279502884L * (long double)k /
@@ -147,7 +222,7 @@ int upload_twiddles(int64_t n, cd **dst) {
     h[(size_t)k].y = (double)sinl(a);
   }
   HIPCHK(hipMalloc((void **)dst, (size_t)n * sizeof(cd)));
-  HIPCHK(hipMemcpy(*dst, h.data(), (size_t)n * sizeof(cd), hipMemcpyHostToDevice));
+  STCHK(copy_h2d(*dst, h.data(), (size_t)n * sizeof(cd), thread_stream(dev)));
   return GDSP_OK;
 }
 
@@ -163,7 +238,7 @@ int build_plan(int dev, int64_t n, gdsp_plan *p) {
   if (is_pow2(n)) {
     p->log2n = ilog2(n);
     p->kind = p->log2n <= gdsp::kMaxLdsLog2 ? KIND_LDS : KIND_GLOBAL;
-    return upload_twiddles(n, &p->tw);
+    return upload_twiddles(dev, n, &p->tw);
   }
   // Bluestein factors, bluestein.go:32-61: w_k = (cos, sin)(Pi/n * k*k),
   // k = 0 exactly 1 (angle not reduced, as the reference computes it).
@@ -187,13 +262,13 @@ int build_plan(int dev, int64_t n, gdsp_plan *p) {
     if (i != 0) b[(size_t)(p->m - i)] = w[(size_t)i];
   }
   HIPCHK(hipMalloc((void **)&p->chirp, (size_t)n * sizeof(cd)));
-  HIPCHK(hipMemcpy(p->chirp, chirp.data(), (size_t)n * sizeof(cd), hipMemcpyHostToDevice));
+  hipStream_t s = thread_stream(dev);
+  STCHK(copy_h2d(p->chirp, chirp.data(), (size_t)n * sizeof(cd), s));
   HIPCHK(hipMalloc((void **)&p->bhat, (size_t)p->m * sizeof(cd)));
   cd *db = nullptr;
   HIPCHK(hipMalloc((void **)&db, (size_t)p->m * sizeof(cd)));
-  HIPCHK(hipMemcpy(db, b.data(), (size_t)p->m * sizeof(cd), hipMemcpyHostToDevice));
+  STCHK(copy_h2d(db, b.data(), (size_t)p->m * sizeof(cd), s));
   // FFT_M(b) on the device with the engine itself, then fold the IFFT's 1/M
-  hipStream_t s = thread_stream(dev);
   int st = exec_plan(p->mplan, db, p->bhat, 1, false, gdsp::LOAD_COMPLEX, s);
   if (st == GDSP_OK) {
     hipError_t e = gdsp::launch_scale(p->bhat, p->m, 1.0 / (double)p->m, s);
@@ -336,9 +411,9 @@ int host_batch(const void *x, size_t in_elem_bytes, double *out, int64_t n, int6
   DevBuf din, dout;
   STCHK(din.alloc(in_bytes, s));
   STCHK(dout.alloc(out_bytes, s));
-  HIPCHK(hipMemcpyAsync(din.p, x, in_bytes, hipMemcpyHostToDevice, s));
+  STCHK(copy_h2d(din.p, x, in_bytes, s));
   STCHK(exec_plan(p, din.p, (cd *)dout.p, batch, inv, load, s));
-  HIPCHK(hipMemcpyAsync(out, dout.p, out_bytes, hipMemcpyDeviceToHost, s));
+  STCHK(copy_d2h(out, dout.p, out_bytes, s));
   HIPCHK(hipStreamSynchronize(s));
   return GDSP_OK;
 }
@@ -440,13 +515,12 @@ int gdsp_convolve(const double *x, const double *y, double *out, int64_t n) {
   DevBuf d;
   STCHK(d.alloc(3 * bytes, s));
   cd *dx = (cd *)d.p, *dy = dx + n, *dz = dy + n;
-  HIPCHK(hipMemcpyAsync(dx, x, bytes, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(dy, y, bytes, hipMemcpyHostToDevice, s));
+  STCHK(copy_h2d(dx, x, bytes, s));
+  STCHK(copy_h2d(dy, y, bytes, s));
   STCHK(exec_plan(p, dx, dx, 2, false, gdsp::LOAD_COMPLEX, s));  // both rows at once
   HIPCHK(gdsp::launch_pointwise_mul(dx, dy, dz, n, s));
   STCHK(exec_plan(p, dz, dz, 1, true, gdsp::LOAD_COMPLEX, s));
-  HIPCHK(hipMemcpyAsync(out, dz, bytes, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  STCHK(copy_d2h(out, dz, bytes, s));
   return GDSP_OK;
 }
 
@@ -492,14 +566,13 @@ static int fft2_host(const double *x, bool real_in, double *out, int64_t rows, i
   if (real_in) {
     DevBuf dr;
     STCHK(dr.alloc(cnt * sizeof(double), s));
-    HIPCHK(hipMemcpyAsync(dr.p, x, cnt * sizeof(double), hipMemcpyHostToDevice, s));
+    STCHK(copy_h2d(dr.p, x, cnt * sizeof(double), s));
     HIPCHK(gdsp::launch_real_to_complex((const double *)dr.p, (cd *)din.p, (int64_t)cnt, s));
   } else {
-    HIPCHK(hipMemcpyAsync(din.p, x, cnt * sizeof(cd), hipMemcpyHostToDevice, s));
+    STCHK(copy_h2d(din.p, x, cnt * sizeof(cd), s));
   }
   STCHK(gdsp_fft2_device(din.p, dout.p, rows, cols, inverse, nullptr, s));
-  HIPCHK(hipMemcpyAsync(out, dout.p, cnt * sizeof(cd), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  STCHK(copy_d2h(out, dout.p, cnt * sizeof(cd), s));
   return GDSP_OK;
 }
 
@@ -663,14 +736,12 @@ int gdsp_pwelch(const double *x, int64_t n, double fs, int64_t nfft, int64_t pad
     STCHK(dw.alloc((size_t)flen * sizeof(double), s));
     STCHK(dacc.alloc((size_t)flen * sizeof(double), s));
     if (lx > n) HIPCHK(hipMemsetAsync(dx.p, 0, (size_t)lx * sizeof(double), s));
-    HIPCHK(hipMemcpyAsync(dx.p, x, (size_t)n * sizeof(double), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(dw.p, win_seg, (size_t)flen * sizeof(double), hipMemcpyHostToDevice, s));
+    STCHK(copy_h2d(dx.p, x, (size_t)n * sizeof(double), s));
+    STCHK(copy_h2d(dw.p, win_seg, (size_t)flen * sizeof(double), s));
     HIPCHK(hipMemsetAsync(dacc.p, 0, (size_t)flen * sizeof(double), s));
     STCHK(gdsp_pwelch_accumulate_device((const double *)dx.p, lx, nfft, pad, noverlap, 0, nsegs,
                                         (const double *)dw.p, (double *)dacc.p, s));
-    HIPCHK(hipMemcpyAsync(acc.data(), dacc.p, (size_t)flen * sizeof(double),
-                          hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    STCHK(copy_d2h(acc.data(), dacc.p, (size_t)flen * sizeof(double), s));
   }
   STCHK(gdsp_pwelch_finalize(acc.data(), flen, nsegs, nfft, pad, win_nfft, fs, scale_off, pxx,
                              freqs));
