@@ -31,26 +31,25 @@ __global__ __launch_bounds__(Geo<LOG2N>::WG) void fft_lds_kernel(
   const int slot = lt / G::T;
   const int t = lt & (G::T - 1);
   const int64_t g = (int64_t)blockIdx.x * G::TPW + slot;
-  const bool valid = g < batch;
+  // Only the last workgroup can hold slots past the batch (TPW > 1); they
+  // load a valid row (clamped) and skip the store, so loads stay
+  // branch-free and the whole workgroup reaches every barrier.
+  const bool valid = G::TPW == 1 || g < batch;
+  const int64_t gl = G::TPW == 1 ? g : (g < batch ? g : batch - 1);
   double *lre = lds + slot * G::STRIDE;
   double *lim = SPLIT ? lre : lds + G::LDS_DOUBLES + slot * G::STRIDE;
   cd v[G::E];
-  if (valid) {
-    if constexpr (LOAD == LOAD_COMPLEX) {
-      const cd *src = reinterpret_cast<const cd *>(in) + g * G::N;
+  if constexpr (LOAD == LOAD_COMPLEX) {
+    const cd *src = reinterpret_cast<const cd *>(in) + gl * G::N;
 #pragma unroll
-      for (int k = 0; k < G::E; ++k) {
-        v[k] = src[t + k * G::T];
-        if constexpr (INV) v[k].y = -v[k].y;
-      }
-    } else {
-      const double *src = reinterpret_cast<const double *>(in) + g * G::N;
-#pragma unroll
-      for (int k = 0; k < G::E; ++k) v[k] = {src[t + k * G::T], 0.0};
+    for (int k = 0; k < G::E; ++k) {
+      v[k] = src[t + k * G::T];
+      if constexpr (INV) v[k].y = -v[k].y;
     }
   } else {
+    const double *src = reinterpret_cast<const double *>(in) + gl * G::N;
 #pragma unroll
-    for (int k = 0; k < G::E; ++k) v[k] = {0.0, 0.0};
+    for (int k = 0; k < G::E; ++k) v[k] = {src[t + k * G::T], 0.0};
   }
   fft_regs<LOG2N, SPLIT>(v, t, tw, lre, lim);
   if (valid) {

@@ -1,0 +1,104 @@
+"""Multi-GPU drivers for the go-dsp hot path: one process per GPU
+(torch.distributed; backend "nccl" = RCCL over xGMI on ROCm).
+
+- Batched FFT (fft.FFT over many rows): rows are independent, so each rank
+  transforms a contiguous row shard; there is no data-path collective.
+- Pwelch (spectral/pwelch.go:74-145): segments [S*r/W, S*(r+1)/W) go to rank
+  r, which needs samples [lo*stride, (hi-1)*stride + nfft) — its slice plus an
+  (nfft - stride)-sample halo. Each rank accumulates per-bin power sums on its
+  GPU; one all-reduce (sum, float64, max(pad, nfft) values) combines them and
+  every rank finalises Pxx on the host (gdsp_pwelch_finalize). The reordered
+  summation changes Pxx only at roundoff (all terms are non-negative).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Optional
+
+import numpy as np
+
+from . import spectral
+
+
+def shard_range(total: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous [lo, hi) share of `total` units for `rank` of `world`."""
+    return total * rank // world, total * (rank + 1) // world
+
+
+@dataclass
+class PwelchShard:
+    seg_lo: int      # first segment of this rank (global index)
+    seg_hi: int      # one past the last segment
+    sample_lo: int   # first sample this rank needs
+    sample_hi: int   # one past the last sample it needs (halo included)
+    nsegs_total: int
+    nfft: int
+    pad: int
+    noverlap: int
+
+    @property
+    def stride(self) -> int:
+        return self.nfft - self.noverlap
+
+    @property
+    def flen(self) -> int:
+        return max(self.pad, self.nfft)
+
+
+def plan_pwelch(n_samples: int, world: int, rank: int, nfft: int = 0, pad: int = 0,
+                noverlap: int = 0) -> PwelchShard:
+    """Segment/sample ranges of `rank` (defaults as pwelch.go:85-95; a signal
+    shorter than nfft is zero-padded to nfft, pwelch.go:97-99)."""
+    nfft = nfft or 256
+    pad = pad or nfft
+    lx = max(n_samples, nfft)
+    nsegs = spectral.segment_count(lx, nfft, noverlap)
+    lo, hi = shard_range(nsegs, world, rank)
+    stride = nfft - noverlap
+    if hi > lo:
+        s_lo, s_hi = lo * stride, (hi - 1) * stride + nfft
+    else:
+        s_lo = s_hi = 0
+    return PwelchShard(lo, hi, s_lo, s_hi, nsegs, nfft, pad, noverlap)
+
+
+def gpu_accumulate(x_local, shard: PwelchShard, win_seg, acc, stream=None):
+    """Per-bin power sums of the rank's segments on its GPU (fused kernel)."""
+    from . import device
+    device.pwelch_accumulate(x_local, shard.nfft, shard.pad, shard.noverlap, 0,
+                             shard.seg_hi - shard.seg_lo, win_seg, acc, stream=stream)
+    return acc
+
+
+def pwelch(x_local, Fs: float, o: spectral.PwelchOptions, shard: PwelchShard, group=None,
+           accumulate: Optional[Callable] = None, stream=None):
+    """Sharded spectral.Pwelch. x_local: this rank's samples
+    [shard.sample_lo, shard.sample_hi) as a float64 tensor on its device
+    (zero-padded to nfft if the whole signal is shorter). Returns (Pxx, freqs)
+    as numpy arrays on every rank."""
+    import torch
+    import torch.distributed as dist
+
+    nfft, pad, noverlap, wf, scaling = spectral.resolve_options(o)
+    assert (nfft, pad, noverlap) == (shard.nfft, shard.pad, shard.noverlap)
+    flen = shard.flen
+    dev = x_local.device
+    win_seg = torch.as_tensor(np.ascontiguousarray(wf(flen)), dtype=torch.float64, device=dev)
+    acc = torch.zeros(flen, dtype=torch.float64, device=dev)
+    if shard.seg_hi > shard.seg_lo:
+        (accumulate or gpu_accumulate)(x_local, shard, win_seg, acc, stream)
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        if stream is not None:
+            with torch.cuda.stream(stream):
+                dist.all_reduce(acc, group=group)
+        else:
+            dist.all_reduce(acc, group=group)
+    return spectral.finalize(acc.cpu().numpy(), shard.nsegs_total, nfft, pad,
+                             np.asarray(wf(nfft), np.float64), Fs, not scaling)
+
+
+def fft_rows_sharded(x_shard, inverse: bool = False, out=None, stream=None):
+    """Batched FFT of this rank's row shard (rows are independent: no
+    collective). x_shard: (rows, n) complex128 tensor on the rank's GPU."""
+    from . import device
+    return device.fft_batch(x_shard, out=out, inverse=inverse, stream=stream)

@@ -1,0 +1,263 @@
+// fftbench.hip — kernel-variant A/B harness for the N=4096 batched transform
+// (development tool; not part of the product library). Builds the same
+// device building blocks as libgdspfft with different load/store policies,
+// occupancy bounds and exchange layouts, times them in interleaved rounds in
+// one process (cdna_hip_programming.md §5.4 rule 24), and checks every
+// variant against variant 0 bit-for-bit-ish (max |diff|).
+//
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -I../go-dsp_amd/csrc fftbench.hip -o fftbench
+//   ./fftbench [batch] [rounds]
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "fft_device.hpp"
+
+using namespace gdsp;
+
+#define CHECK(x)                                                                  \
+  do {                                                                            \
+    hipError_t e = (x);                                                           \
+    if (e != hipSuccess) {                                                        \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+      exit(1);                                                                    \
+    }                                                                             \
+  } while (0)
+
+template <bool NT>
+__device__ __forceinline__ cd ld(const cd *p) {
+  if constexpr (NT) {
+    return {__builtin_nontemporal_load(&p->x), __builtin_nontemporal_load(&p->y)};
+  } else {
+    return *p;
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void st(cd *p, cd v) {
+  if constexpr (NT) {
+    __builtin_nontemporal_store(v.x, &p->x);
+    __builtin_nontemporal_store(v.y, &p->y);
+  } else {
+    *p = v;
+  }
+}
+
+// Variant kernel: LOG2N = 12 (T = 256, one transform per workgroup).
+template <bool SPLIT, bool NTL, bool NTS, int MINW>
+__global__ __launch_bounds__(256, MINW) void fft4096_v(const cd *__restrict__ in,
+                                                        cd *__restrict__ out, int64_t batch,
+                                                        const cd *__restrict__ tw) {
+  using G = Geo<12>;
+  __shared__ double lds[(SPLIT ? 1 : 2) * G::LDS_DOUBLES];
+  const int t = threadIdx.x;
+  const int64_t g = blockIdx.x;
+  double *lre = lds;
+  double *lim = SPLIT ? lds : lds + G::LDS_DOUBLES;
+  cd v[16];
+  const cd *src = in + g * 4096;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = ld<NTL>(src + t + k * 256);
+  fft_regs<12, SPLIT>(v, t, tw, lre, lim);
+  cd *dst = out + g * 4096;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) st<NTS>(dst + t + k * 256, v[k]);
+}
+
+// Same memory pattern, no arithmetic: the ceiling of this access shape.
+template <bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void copy4096(const cd *__restrict__ in, cd *__restrict__ out,
+                                                int64_t batch) {
+  const int t = threadIdx.x;
+  const int64_t g = blockIdx.x;
+  cd v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = ld<NTL>(in + g * 4096 + t + k * 256);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) st<NTS>(out + g * 4096 + t + k * 256, v[k]);
+}
+
+
+// streaming-shape probes (ceilings for 16-B-per-lane read+write streams)
+__global__ __launch_bounds__(256) void copy_one(const cd *__restrict__ in, cd *__restrict__ out,
+                                                int64_t cnt) {
+  const int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x;
+  if (i < cnt) out[i] = in[i];
+}
+template <int U>
+__global__ __launch_bounds__(256) void copy_unroll(const cd *__restrict__ in,
+                                                   cd *__restrict__ out, int64_t cnt) {
+  const int64_t base = blockIdx.x * (int64_t)(256 * U) + threadIdx.x;
+  cd v[U];
+#pragma unroll
+  for (int k = 0; k < U; ++k) v[k] = in[base + k * 256];
+#pragma unroll
+  for (int k = 0; k < U; ++k) out[base + k * 256] = v[k];
+}
+template <int U>
+__global__ __launch_bounds__(256) void copy_gs(const cd *__restrict__ in, cd *__restrict__ out,
+                                               int64_t cnt) {
+  for (int64_t base = blockIdx.x * (int64_t)(256 * U) + threadIdx.x; base < cnt;
+       base += (int64_t)gridDim.x * 256 * U) {
+    cd v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[k] = in[base + k * 256];
+#pragma unroll
+    for (int k = 0; k < U; ++k) out[base + k * 256] = v[k];
+  }
+}
+__global__ __launch_bounds__(256) void read_only(const cd *__restrict__ in, cd *__restrict__ out,
+                                                 int64_t cnt) {
+  const int64_t base = blockIdx.x * (int64_t)(256 * 16) + threadIdx.x;
+  double s = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    cd v = in[base + k * 256];
+    s += v.x + v.y;
+  }
+  if (s == 12345.678) out[0].x = s;
+}
+__global__ __launch_bounds__(256) void write_only(const cd *__restrict__ in, cd *__restrict__ out,
+                                                  int64_t cnt) {
+  const int64_t base = blockIdx.x * (int64_t)(256 * 16) + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) out[base + k * 256] = {1.0 * k, 2.0};
+}
+
+void l_copy_one(const cd *in, cd *out, int64_t b, const cd *, hipStream_t s) {
+  const int64_t cnt = b * 4096;
+  hipLaunchKernelGGL(copy_one, dim3((unsigned)(cnt / 256)), dim3(256), 0, s, in, out, cnt);
+}
+template <int U>
+void l_copy_unroll(const cd *in, cd *out, int64_t b, const cd *, hipStream_t s) {
+  const int64_t cnt = b * 4096;
+  hipLaunchKernelGGL((copy_unroll<U>), dim3((unsigned)(cnt / 256 / U)), dim3(256), 0, s, in, out, cnt);
+}
+template <int U, int G>
+void l_copy_gs(const cd *in, cd *out, int64_t b, const cd *, hipStream_t s) {
+  const int64_t cnt = b * 4096;
+  hipLaunchKernelGGL((copy_gs<U>), dim3(G), dim3(256), 0, s, in, out, cnt);
+}
+void l_read(const cd *in, cd *out, int64_t b, const cd *, hipStream_t s) {
+  hipLaunchKernelGGL(read_only, dim3((unsigned)b), dim3(256), 0, s, in, out, b * 4096);
+}
+void l_write(const cd *in, cd *out, int64_t b, const cd *, hipStream_t s) {
+  hipLaunchKernelGGL(write_only, dim3((unsigned)b), dim3(256), 0, s, in, out, b * 4096);
+}
+
+struct Variant {
+  const char *name;
+  void (*launch)(const cd *, cd *, int64_t, const cd *, hipStream_t);
+  bool is_fft;
+};
+
+template <bool SPLIT, bool NTL, bool NTS, int MINW>
+void launch_v(const cd *in, cd *out, int64_t batch, const cd *tw, hipStream_t s) {
+  hipLaunchKernelGGL((fft4096_v<SPLIT, NTL, NTS, MINW>), dim3((unsigned)batch), dim3(256), 0, s,
+                     in, out, batch, tw);
+}
+template <bool NTL, bool NTS>
+void launch_c(const cd *in, cd *out, int64_t batch, const cd *, hipStream_t s) {
+  hipLaunchKernelGGL((copy4096<NTL, NTS>), dim3((unsigned)batch), dim3(256), 0, s, in, out, batch);
+}
+
+__global__ void fill(double *p, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ULL + 0x5EED;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z ^= z >> 31;
+    p[i] = (double)(z >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0;
+  }
+}
+
+int main(int argc, char **argv) {
+  const int64_t batch = argc > 1 ? atoll(argv[1]) : 65536;
+  const int rounds = argc > 2 ? atoi(argv[2]) : 5;
+  const int64_t n = 4096;
+  const size_t bytes = (size_t)batch * n * sizeof(cd);
+  cd *in, *out, *ref, *tw;
+  CHECK(hipMalloc(&in, bytes));
+  CHECK(hipMalloc(&out, bytes));
+  CHECK(hipMalloc(&ref, bytes));
+  CHECK(hipMalloc(&tw, n * sizeof(cd)));
+  std::vector<cd> h(n);
+  for (int k = 0; k < n; ++k) {
+    long double a = -2.0L * 3.141592653589793238462643383279502884L * k / n;
+    h[k] = {(double)cosl(a), (double)sinl(a)};
+  }
+  CHECK(hipMemcpy(tw, h.data(), n * sizeof(cd), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(fill, dim3(8192), dim3(256), 0, 0, (double *)in, (int64_t)(2 * batch * n));
+  CHECK(hipDeviceSynchronize());
+
+  std::vector<Variant> vs = {
+      {"split", launch_v<true, false, false, 1>, true},
+      {"split_ntl", launch_v<true, true, false, 1>, true},
+      {"split_nts", launch_v<true, false, true, 1>, true},
+      {"split_ntl_nts", launch_v<true, true, true, 1>, true},
+      {"split_w4", launch_v<true, false, false, 4>, true},
+      {"split_w3", launch_v<true, false, false, 3>, true},
+      {"twobuf", launch_v<false, false, false, 1>, true},
+      {"twobuf_w3", launch_v<false, false, false, 3>, true},
+      {"copy", launch_c<false, false>, false},
+      {"copy_ntl_nts", launch_c<true, true>, false},
+      {"copy_one", l_copy_one, false},
+      {"copy_u2", l_copy_unroll<2>, false},
+      {"copy_u4", l_copy_unroll<4>, false},
+      {"copy_u8", l_copy_unroll<8>, false},
+      {"copy_gs4_2048", l_copy_gs<4, 2048>, false},
+      {"copy_gs4_4096", l_copy_gs<4, 4096>, false},
+      {"copy_gs8_1024", l_copy_gs<8, 1024>, false},
+      {"copy_gs1_8192", l_copy_gs<1, 8192>, false},
+      {"read_only(x2)", l_read, false},
+      {"write_only(x2)", l_write, false},
+  };
+  hipStream_t s;
+  CHECK(hipStreamCreate(&s));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  // reference output
+  vs[0].launch(in, ref, batch, tw, s);
+  CHECK(hipStreamSynchronize(s));
+  std::vector<std::vector<float>> times(vs.size());
+  const int reps = 5;
+  for (int r = 0; r < rounds; ++r) {
+    for (size_t i = 0; i < vs.size(); ++i) {
+      vs[i].launch(in, out, batch, tw, s);  // warm
+      CHECK(hipEventRecord(e0, s));
+      for (int k = 0; k < reps; ++k) vs[i].launch(in, out, batch, tw, s);
+      CHECK(hipEventRecord(e1, s));
+      CHECK(hipEventSynchronize(e1));
+      float ms;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      times[i].push_back(ms / reps);
+      CHECK(hipGetLastError());
+    }
+  }
+  // correctness vs variant 0
+  std::vector<cd> a(n * 64), b(n * 64);
+  for (size_t i = 0; i < vs.size(); ++i) {
+    vs[i].launch(in, out, batch, tw, s);
+    CHECK(hipStreamSynchronize(s));
+    double md = 0;
+    if (vs[i].is_fft) {
+      for (int64_t off : {(int64_t)0, batch / 2 * n, (batch - 64) * n}) {
+        CHECK(hipMemcpy(a.data(), out + off, a.size() * sizeof(cd), hipMemcpyDeviceToHost));
+        CHECK(hipMemcpy(b.data(), ref + off, b.size() * sizeof(cd), hipMemcpyDeviceToHost));
+        for (size_t j = 0; j < a.size(); ++j)
+          md = std::max(md, std::max(fabs(a[j].x - b[j].x), fabs(a[j].y - b[j].y)));
+      }
+    }
+    std::vector<float> t = times[i];
+    std::sort(t.begin(), t.end());
+    const double med = t[t.size() / 2];
+    printf("%-16s median %.4f ms  min %.4f ms  %7.1f GB/s  maxdiff %.3g\n", vs[i].name, med, t[0],
+           2.0 * bytes / (med * 1e-3) / 1e9, md);
+  }
+  return 0;
+}
