@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (gpurun_out/pmc_<w>_<C>/)
+into profiles/pmc_<w>.json: HBM bytes per launch of the workload's dominant
+kernel. Units and gfx950 correction per MI355X_MICROARCH.md §HBM: counters are
+in KiB; FETCH_SIZE reports half the bytes of a 16-B/lane streaming read, so it
+is doubled; WRITE_SIZE is exact for 16-B/lane stores."""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNELS = {"radix4096": "fft_lds_kernel<12", "bluestein3000": "bluestein_kernel<13",
+           "pwelch": "pwelch_kernel<12", "fft2_8192": "fft_lds_kernel<13"}
+
+
+def values(w, counter):
+    path = os.path.join(REPO, "gpurun_out", f"pmc_{w}_{counter}", "run_counter_collection.csv")
+    rows = [r for r in csv.DictReader(open(path)) if KERNELS[w] in r["Kernel_Name"]]
+    return [float(r["Counter_Value"]) for r in rows], path
+
+
+def main(w, tag):
+    fetch, pf = values(w, "FETCH_SIZE")
+    write, pw = values(w, "WRITE_SIZE")
+    f_kib, w_kib = statistics.median(fetch), statistics.median(write)
+    out = {
+        "workload": w, "kernel": KERNELS[w], "launches": [len(fetch), len(write)],
+        "fetch_size_kib": f_kib, "write_size_kib": w_kib,
+        "hbm_read_bytes_per_launch": int(2 * f_kib * 1024),
+        "hbm_write_bytes_per_launch": int(w_kib * 1024),
+        "hbm_bytes_per_launch": int((2 * f_kib + w_kib) * 1024),
+        "correction": "FETCH_SIZE x2 (gfx950 16-B/lane streaming reads), KiB -> bytes",
+        "source": f"profiles/{tag}/pmc_{w}_FETCH_SIZE.csv, profiles/{tag}/pmc_{w}_WRITE_SIZE.csv",
+    }
+    dst = os.path.join(REPO, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(pf, os.path.join(dst, f"pmc_{w}_FETCH_SIZE.csv"))
+    shutil.copy(pw, os.path.join(dst, f"pmc_{w}_WRITE_SIZE.csv"))
+    with open(os.path.join(REPO, "profiles", f"pmc_{w}.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    for w in sys.argv[2:]:
+        main(w, sys.argv[1])
