@@ -95,15 +95,17 @@ __global__ __launch_bounds__(Geo<LOG2M>::WG) void bluestein_kernel(
       v[k] = cmul(x, chirp[idx]);
     }
   }
-  fft_regs<LOG2M, SPLIT>(v, t, twm, lre, lim, true);
+  fft_regs<LOG2M, SPLIT, true>(v, t, twm, lre, lim, true);
 #pragma unroll
   for (int k = 0; k < G::E; ++k) v[k] = conjg(cmul(v[k], bhat[t + k * G::T]));
-  fft_regs<LOG2M, SPLIT>(v, t, twm, lre, lim, false);
+  fft_regs<LOG2M, SPLIT, true>(v, t, twm, lre, lim, false);
+  chirp = opaque_ptr(chirp);
+  const int to = opaque_int(t);
   if (valid) {
     cd *dst = out + g * n;
 #pragma unroll
     for (int k = 0; k < G::E; ++k) {
-      const int idx = t + k * G::T;
+      const int idx = to + k * G::T;
       if (idx < n) {
         cd y = cmul(conjg(v[k]), chirp[idx]);
         if constexpr (INV) y = {y.x * scale, -y.y * scale};
@@ -176,9 +178,6 @@ __global__ __launch_bounds__(Geo<LOG2F>::WG) void pwelch_kernel(
   double *lre = lds + slot * G::STRIDE;
   double *lim = SPLIT ? lre : lds + G::LDS_DOUBLES + slot * G::STRIDE;
   const int64_t npairs = (seg_end - seg_begin + 1) / 2;
-  double wv[G::E];
-#pragma unroll
-  for (int k = 0; k < G::E; ++k) wv[k] = win[t + k * G::T];
   double acc[G::E];
 #pragma unroll
   for (int k = 0; k < G::E; ++k) acc[k] = 0.0;
@@ -189,16 +188,21 @@ __global__ __launch_bounds__(Geo<LOG2F>::WG) void pwelch_kernel(
     const bool has1 = active && (s0 + 1 < seg_end);
     const double *x0 = x + s0 * stride;
     const double *x1 = x0 + stride;
+    // the window is re-read every iteration (L1/L2 hits) instead of being
+    // held in 2*E registers across the loop
+    const double *w = opaque_ptr(win);
+    const int tt = opaque_int(t);
     cd v[G::E];
 #pragma unroll
     for (int k = 0; k < G::E; ++k) {
-      const int i = t + k * G::T;
+      const int i = tt + k * G::T;
       const bool in_seg = i < nfft;
+      const double wk = w[i];
       const double a = (active && in_seg) ? x0[i] : 0.0;
       const double b = (has1 && in_seg) ? x1[i] : 0.0;
-      v[k] = {a * wv[k], b * wv[k]};
+      v[k] = {a * wk, b * wk};
     }
-    fft_regs<LOG2F, SPLIT>(v, t, tw, lre, lim, it == 0);
+    fft_regs<LOG2F, SPLIT, true>(v, tt, tw, lre, lim, it == 0);
     if (active) {
 #pragma unroll
       for (int k = 0; k < G::E; ++k) acc[k] += v[k].x * v[k].x + v[k].y * v[k].y;
@@ -211,14 +215,28 @@ __global__ __launch_bounds__(Geo<LOG2F>::WG) void pwelch_kernel(
   }
 }
 
-// acc[k] += sum over workers w < nworkers of partial[w*F + k] (fixed order:
-// deterministic).
-__global__ void reduce_partials_kernel(const double *__restrict__ partial, int64_t nworkers,
-                                       int64_t F, double *__restrict__ acc) {
+// Deterministic two-level reduction of the per-worker partial spectra:
+// level 1 sums fixed chunks of workers per bin (grid: bins x chunks), level 2
+// sums the chunk results in chunk order and adds into acc.
+constexpr int kReduceChunk = 64;
+__global__ void reduce_partials_l1(const double *__restrict__ partial, int64_t nworkers,
+                                   int64_t F, double *__restrict__ chunk_sums) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t c = blockIdx.y;
+  if (k >= F) return;
+  const int64_t w0 = c * kReduceChunk;
+  const int64_t w1 = w0 + kReduceChunk < nworkers ? w0 + kReduceChunk : nworkers;
+  double s = 0.0;
+  for (int64_t w = w0; w < w1; ++w) s += partial[w * F + k];
+  chunk_sums[c * F + k] = s;
+}
+
+__global__ void reduce_partials_l2(const double *__restrict__ chunk_sums, int64_t nchunks,
+                                   int64_t F, double *__restrict__ acc) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= F) return;
   double s = 0.0;
-  for (int64_t w = 0; w < nworkers; ++w) s += partial[w * F + k];
+  for (int64_t c = 0; c < nchunks; ++c) s += chunk_sums[c * F + k];
   acc[k] += s;
 }
 
@@ -503,10 +521,18 @@ hipError_t launch_pwelch(int log2f, const double *x, int64_t nfft, int64_t strid
 }
 
 hipError_t launch_reduce_partials(const double *partial, int64_t nworkers, int64_t F, double *acc,
-                                  hipStream_t s) {
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(blocks_for(F, 256)), dim3(256), 0, s, partial,
-                     nworkers, F, acc);
+                                  double *scratch, hipStream_t s) {
+  // scratch: ceil(nworkers / kReduceChunk) * F doubles
+  const int64_t nchunks = (nworkers + kReduceChunk - 1) / kReduceChunk;
+  hipLaunchKernelGGL(reduce_partials_l1, dim3(blocks_for(F, 256), (unsigned)nchunks), dim3(256), 0,
+                     s, partial, nworkers, F, scratch);
+  hipLaunchKernelGGL(reduce_partials_l2, dim3(blocks_for(F, 256)), dim3(256), 0, s, scratch,
+                     nchunks, F, acc);
   return hipGetLastError();
+}
+
+int64_t reduce_scratch_doubles(int64_t nworkers, int64_t F) {
+  return ((nworkers + kReduceChunk - 1) / kReduceChunk) * F;
 }
 
 hipError_t launch_segments_to_complex(const double *x, int64_t nfft, int64_t flen, int64_t stride,

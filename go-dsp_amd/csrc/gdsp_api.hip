@@ -647,11 +647,13 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
     if (target > npairs) target = npairs;
     const int64_t ppw = (npairs + target - 1) / target;
     const int64_t nworkers = (npairs + ppw - 1) / ppw;
-    DevBuf part;
+    DevBuf part, red;
     STCHK(part.alloc((size_t)nworkers * (size_t)flen * sizeof(double), s));
+    STCHK(red.alloc((size_t)gdsp::reduce_scratch_doubles(nworkers, flen) * sizeof(double), s));
     HIPCHK(gdsp::launch_pwelch(p->log2n, d_x, nfft, stride, seg_begin, seg_end, ppw, nworkers,
                                d_win_seg, p->tw, (double *)part.p, s));
-    HIPCHK(gdsp::launch_reduce_partials((const double *)part.p, nworkers, flen, d_acc, s));
+    HIPCHK(gdsp::launch_reduce_partials((const double *)part.p, nworkers, flen, d_acc,
+                                        (double *)red.p, s));
     return GDSP_OK;
   }
   // materialised path: windowed segments as complex rows, batched FFT, |X|^2

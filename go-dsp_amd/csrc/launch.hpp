@@ -27,7 +27,8 @@ hipError_t launch_pwelch(int log2f, const double *x, int64_t nfft, int64_t strid
                          int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,
                          const double *win, const cd *tw, double *partial, hipStream_t s);
 hipError_t launch_reduce_partials(const double *partial, int64_t nworkers, int64_t F, double *acc,
-                                  hipStream_t s);
+                                  double *scratch, hipStream_t s);
+int64_t reduce_scratch_doubles(int64_t nworkers, int64_t F);
 hipError_t launch_segments_to_complex(const double *x, int64_t nfft, int64_t flen, int64_t stride,
                                       int64_t seg0, int64_t nseg, const double *win, cd *buf,
                                       hipStream_t s);

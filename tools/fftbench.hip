@@ -67,6 +67,59 @@ __global__ __launch_bounds__(256, MINW) void fft4096_v(const cd *__restrict__ in
   for (int k = 0; k < 16; ++k) st<NTS>(dst + t + k * 256, v[k]);
 }
 
+// No HBM traffic: registers seeded from the thread id, store only on an
+// impossible condition (keeps the FFT live): the compute + LDS time alone.
+template <int MINW>
+__global__ __launch_bounds__(256, MINW) void fft4096_compute(const cd *__restrict__ in,
+                                                             cd *__restrict__ out, int64_t batch,
+                                                             const cd *__restrict__ tw) {
+  using G = Geo<12>;
+  __shared__ double lds[G::LDS_DOUBLES];
+  const int t = threadIdx.x;
+  cd v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = {(double)(t + k + blockIdx.x), (double)(t - k)};
+  fft_regs<12, true>(v, t, tw, lds, lds);
+  double s = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) s += v[k].x + v[k].y;
+  if (s == 1.2345e300) out[t] = {s, s};
+}
+
+// Bluestein N=3000 / M=8192 variants (512 threads, 16 elements each)
+template <int MINW, bool SB = false>
+__global__ __launch_bounds__(512, MINW) void blu_v(const cd *__restrict__ in, cd *__restrict__ out,
+                                                   int64_t batch, const cd *__restrict__ twm,
+                                                   const cd *__restrict__ chirp,
+                                                   const cd *__restrict__ bhat) {
+  using G = Geo<13>;
+  __shared__ double lds[G::LDS_DOUBLES];
+  const int t = threadIdx.x;
+  const int64_t g = blockIdx.x;
+  const int n = 3000;
+  cd v[16];
+  const cd *src = in + g * n;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int idx = t + k * 512;
+    v[k] = {0.0, 0.0};
+    if (idx < n) v[k] = cmul(src[idx], chirp[idx]);
+  }
+  fft_regs<13, true>(v, t, twm, lds, lds, true);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = conjg(cmul(v[k], bhat[t + k * 512]));
+  int t2 = t;
+  if constexpr (SB) asm volatile("" : "+s"(twm), "+v"(t2));
+  fft_regs<13, true>(v, t2, twm, lds, lds, false);
+  if constexpr (SB) asm volatile("" : "+s"(chirp), "+v"(t2));
+  cd *dst = out + g * n;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int idx = t2 + k * 512;
+    if (idx < n) dst[idx] = cmul(conjg(v[k]), chirp[idx]);
+  }
+}
+
 // Same memory pattern, no arithmetic: the ceiling of this access shape.
 template <bool NTL, bool NTS>
 __global__ __launch_bounds__(256) void copy4096(const cd *__restrict__ in, cd *__restrict__ out,
@@ -159,6 +212,17 @@ void launch_v(const cd *in, cd *out, int64_t batch, const cd *tw, hipStream_t s)
   hipLaunchKernelGGL((fft4096_v<SPLIT, NTL, NTS, MINW>), dim3((unsigned)batch), dim3(256), 0, s,
                      in, out, batch, tw);
 }
+template <int MINW>
+void launch_comp(const cd *in, cd *out, int64_t batch, const cd *tw, hipStream_t s) {
+  hipLaunchKernelGGL((fft4096_compute<MINW>), dim3((unsigned)batch), dim3(256), 0, s, in, out,
+                     batch, tw);
+}
+cd *g_chirp, *g_bhat, *g_tw8192;
+template <int MINW, bool SB = false>
+void launch_blu(const cd *in, cd *out, int64_t batch, const cd *, hipStream_t s) {
+  hipLaunchKernelGGL((blu_v<MINW, SB>), dim3((unsigned)batch), dim3(512), 0, s, in, out, batch,
+                     g_tw8192, g_chirp, g_bhat);
+}
 template <bool NTL, bool NTS>
 void launch_c(const cd *in, cd *out, int64_t batch, const cd *, hipStream_t s) {
   hipLaunchKernelGGL((copy4096<NTL, NTS>), dim3((unsigned)batch), dim3(256), 0, s, in, out, batch);
@@ -192,6 +256,19 @@ int main(int argc, char **argv) {
   }
   CHECK(hipMemcpy(tw, h.data(), n * sizeof(cd), hipMemcpyHostToDevice));
   hipLaunchKernelGGL(fill, dim3(8192), dim3(256), 0, 0, (double *)in, (int64_t)(2 * batch * n));
+  CHECK(hipMalloc(&g_chirp, 8192 * sizeof(cd)));
+  CHECK(hipMalloc(&g_bhat, 8192 * sizeof(cd)));
+  CHECK(hipMalloc(&g_tw8192, 8192 * sizeof(cd)));
+  {
+    std::vector<cd> t8(8192);
+    for (int k = 0; k < 8192; ++k) {
+      long double a = -2.0L * 3.141592653589793238462643383279502884L * k / 8192;
+      t8[k] = {(double)cosl(a), (double)sinl(a)};
+    }
+    CHECK(hipMemcpy(g_tw8192, t8.data(), 8192 * sizeof(cd), hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(g_chirp, t8.data(), 8192 * sizeof(cd), hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(g_bhat, t8.data(), 8192 * sizeof(cd), hipMemcpyHostToDevice));
+  }
   CHECK(hipDeviceSynchronize());
 
   std::vector<Variant> vs = {
@@ -203,6 +280,13 @@ int main(int argc, char **argv) {
       {"split_w3", launch_v<true, false, false, 3>, true},
       {"twobuf", launch_v<false, false, false, 1>, true},
       {"twobuf_w3", launch_v<false, false, false, 3>, true},
+      {"compute_only", launch_comp<1>, false},
+      {"compute_only_w4", launch_comp<4>, false},
+      {"blu3000", launch_blu<1>, false},
+      {"blu3000_w4", launch_blu<4>, false},
+      {"blu3000_w3", launch_blu<3>, false},
+      {"blu3000_sb", launch_blu<1, true>, false},
+      {"blu3000_sb_w4", launch_blu<4, true>, false},
       {"copy", launch_c<false, false>, false},
       {"copy_ntl_nts", launch_c<true, true>, false},
       {"copy_one", l_copy_one, false},
