@@ -1,0 +1,135 @@
+// reference_tests.cpp — the reference's own tests (fft/fft_test.go,
+// spectral/pwelch_test.go, spectral/spectral_test.go, window/window_test.go)
+// re-expressed against the C++ host mirror (go-dsp_amd/host/gdsp.hpp), so
+// they run through the C ABI on the GPU. The tables come from
+// tests/golden/reference_vectors.json, flattened to text by
+// tests/test_cpp_mirror.py (argv[1]). Exit code 0 = all pass.
+#include <cstdio>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+#include <string>
+
+#include "gdsp.hpp"
+
+using namespace gdsp;
+
+static int failures = 0, checks = 0;
+#define EXPECT(cond, what)                                   \
+  do {                                                       \
+    ++checks;                                                \
+    if (!(cond)) {                                           \
+      ++failures;                                            \
+      std::cerr << "FAIL " << what << " (" #cond ")\n";      \
+    }                                                        \
+  } while (0)
+
+static std::vector<double> readd(std::istream &in, size_t n) {
+  std::vector<double> v(n);
+  for (auto &x : v) in >> x;
+  return v;
+}
+static std::vector<complex> readc(std::istream &in, size_t n) {
+  std::vector<complex> v(n);
+  for (auto &x : v) {
+    double a, b;
+    in >> a >> b;
+    x = {a, b};
+  }
+  return v;
+}
+
+int main(int argc, char **argv) {
+  if (argc < 2) {
+    std::cerr << "usage: reference_tests vectors.txt\n";
+    return 2;
+  }
+  std::ifstream f(argv[1]);
+  std::string line;
+  while (std::getline(f, line)) {
+    std::istringstream in(line);
+    std::string kind;
+    in >> kind;
+    if (kind == "FFT") {  // TestFFT, fft_test.go:197-209
+      size_t n;
+      in >> n;
+      auto x = readd(in, n);
+      auto out = readc(in, n);
+      EXPECT(dsputils::PrettyCloseC(fft::FFTReal(x), out), "FFTReal n=" << n);
+      EXPECT(dsputils::PrettyCloseC(fft::IFFT(out), dsputils::ToComplex(x)), "IFFT n=" << n);
+    } else if (kind == "FFT2") {  // TestFFT2, fft_test.go:211-223
+      size_t r, c;
+      in >> r >> c;
+      std::vector<std::vector<double>> x(r);
+      for (auto &row : x) row = readd(in, c);
+      fft::Matrix out(r);
+      for (auto &row : out) row = readc(in, c);
+      EXPECT(dsputils::PrettyClose2(fft::FFT2Real(x), out), "FFT2Real " << r << "x" << c);
+      EXPECT(dsputils::PrettyClose2(fft::IFFT2(out), dsputils::ToComplex2(x)),
+             "IFFT2 " << r << "x" << c);
+    } else if (kind == "PWELCH") {  // TestPwelch, pwelch_test.go:48-60
+      double fs;
+      size_t n, lp;
+      in >> fs >> n;
+      auto x = readd(in, n);
+      in >> lp;
+      auto p = readd(in, lp), fr = readd(in, lp);
+      spectral::PwelchOptions o;
+      auto res = spectral::Pwelch(x, fs, &o);
+      EXPECT(dsputils::PrettyClose(res.first, p), "Pwelch Pxx n=" << n);
+      EXPECT(dsputils::PrettyClose(res.second, fr), "Pwelch freqs n=" << n);
+    } else if (kind == "SEG") {  // TestSegment, spectral_test.go:58-67
+      size_t xl, nseg;
+      int size, nov;
+      in >> xl;
+      auto x = readd(in, xl);
+      in >> size >> nov >> nseg;
+      auto segs = spectral::Segment(x, size, nov);
+      bool ok = segs.size() == nseg;
+      for (size_t s = 0; s < nseg; ++s) {
+        auto want = readd(in, size);
+        if (ok) ok = dsputils::PrettyClose(segs[s], want);
+      }
+      EXPECT(ok, "Segment size=" << size << " noverlap=" << nov);
+    } else if (kind == "WIN") {  // TestWindowFunctions, window_test.go:61-94
+      int L;
+      in >> L;
+      auto hm = readd(in, L), hn = readd(in, L), bt = readd(in, L), ft = readd(in, L),
+           bk = readd(in, L);
+      EXPECT(dsputils::PrettyClose(window::Hamming(L), hm), "Hamming L=" << L);
+      EXPECT(dsputils::PrettyClose(window::Hann(L), hn), "Hann L=" << L);
+      EXPECT(dsputils::PrettyClose(window::Bartlett(L), bt), "Bartlett L=" << L);
+      auto o = window::Rectangular(L);
+      window::Apply(o, window::Hamming);
+      EXPECT(dsputils::PrettyClose(o, hm), "Apply L=" << L);
+      EXPECT(dsputils::PrettyClose(window::FlatTop(L), ft), "FlatTop L=" << L);
+      EXPECT(dsputils::PrettyClose(window::Blackman(L), bk), "Blackman L=" << L);
+    }
+  }
+  // panics of the reference (fft.go:40,57,126,133) and empty-input conventions
+  auto panics = [](auto fn) {
+    try {
+      fn();
+    } catch (const Panic &) {
+      return true;
+    }
+    return false;
+  };
+  EXPECT(panics([] { fft::Convolve({1, 2}, {1}); }), "Convolve unequal panics");
+  EXPECT(panics([] { fft::IFFT({}); }), "IFFT empty panics");
+  EXPECT(panics([] { fft::FFT2({}); }), "FFT2 empty panics");
+  EXPECT(panics([] { fft::FFT2({{1, 2}, {3}}); }), "FFT2 ragged panics");
+  EXPECT(fft::FFT({}).empty(), "FFT empty returns empty");
+  EXPECT(spectral::Pwelch({}, 1, nullptr).first.empty(), "Pwelch empty returns empty");
+  // TestFFTMulti (fft_test.go:251-259) + a Bluestein batch through FFTBatch
+  std::vector<complex> a(256);
+  for (int i = 0; i < 256; ++i) a[i] = {i / 256.0, 0};
+  auto A = fft::FFT(a);
+  EXPECT(dsputils::ComplexEqual(A[0], complex(127.5, 0)), "FFTMulti DC");
+  std::vector<complex> b(3000 * 4, complex(1, 0));
+  auto B = fft::FFTBatch(b, 3000);
+  EXPECT(dsputils::ComplexEqual(B[3000], complex(3000, 0)) && std::abs(B[3001]) < 1e-9,
+         "FFTBatch Bluestein row 1");
+  std::cout << "checks " << checks << " failures " << failures << "\n";
+  return failures ? 1 : 0;
+}
