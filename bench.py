@@ -171,8 +171,8 @@ def main():
             traffic = json.load(f).get("hbm_bytes_per_launch")
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0 and w in ("radix4096", "bluestein3000"):
-        cpu = cpu_baseline(n, args.cpu_seconds)
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(w, args.cpu_seconds)
 
     if rank == 0:
         line = {
@@ -202,31 +202,53 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(n: int, seconds: float):
-    """Reference algorithm (oracle/ restatement of fft/radix2.go +
-    fft/bluestein.go) with the reference's per-call worker pool of nworkers
-    threads (radix2.go:89-151), one fft.FFT call per row, on a bounded row
-    sample of the same synthetic workload."""
+def cpu_baseline(workload: str, seconds: float):
+    """The reference algorithm on the host (oracle/: C restatement of
+    fft/radix2.go, fft/bluestein.go, spectral/pwelch.go) with the reference's
+    worker pool of min(nproc, 16) threads inside every radix-2 transform
+    (radix2.go:89-151), on a bounded sample of the same synthetic workload."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
     import oracle
     cores = min(os.cpu_count() or 1, 16)  # the GPU box's CPU share is 16
-    rows = 64
+    pool = f"reference worker pool of {cores} threads per radix-2 transform (radix2.go:89-151)"
+    if workload == "pwelch":
+        n = 1 << 20
+        t0 = time.perf_counter()
+        while True:
+            x = oracle.fill_uniform(n, SEED)
+            t1 = time.perf_counter()
+            oracle.pwelch_threaded(x, 1.0, 4096, 2048, cores)
+            dt = time.perf_counter() - t1
+            if dt > seconds / 3 or time.perf_counter() - t0 > seconds:
+                break
+            n *= 2
+        return {"value": round(n / dt / 1e9, 6), "unit": "Gsamples/s", "cores": cores,
+                "kind": "port",
+                "sample": f"spectral.Pwelch on a {n}-sample prefix of the stream "
+                          f"(NFFT 4096, 50% overlap, {dt:.1f} s), {pool}"}
+    n = {"radix4096": 4096, "bluestein3000": 3000, "fft2_8192": 8192}[workload]
+    rows = 64 if n != 8192 else 16
     x = oracle.fill_uniform(2 * n * rows, SEED).view(np.complex128).reshape(rows, n)
     done = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        if n & (n - 1) == 0:
-            oracle.fft_rows_threaded(x, cores)
-        else:
-            oracle.fft_rows(x)
+        oracle.fft_rows_threaded(x, cores)
         done += rows
     dt = time.perf_counter() - t0
-    threaded = n & (n - 1) == 0
+    per_fft = dt / done
+    if workload == "fft2_8192":
+        # computeFFT2 = 8192 column FFTs + 8192 row FFTs of 8192 (fft.go:138-151);
+        # the strided column gather/scatter is not charged (favours the CPU)
+        t_fft2 = 2 * 8192 * per_fft
+        return {"value": round(8192 * 8192 / t_fft2 / 1e9, 6), "unit": "Gsamples/s",
+                "cores": cores, "kind": "port",
+                "sample": f"{done} fft.FFT calls of N=8192 ({dt:.1f} s) extrapolated to the "
+                          f"16384 calls of one 8192x8192 FFT2, {pool}"}
     return {"value": round(done * n / dt / 1e9, 6), "unit": "Gsamples/s",
-            "cores": cores if threaded else 1, "kind": "port",
-            "sample": f"{done} rows x N={n} ({dt:.1f} s), fft.FFT per row, "
-                      f"{'reference worker pool of ' + str(cores) + ' threads' if threaded else 'single thread (Bluestein path is serial in the reference)'}"}
+            "cores": cores, "kind": "port",
+            "sample": f"{done} rows x N={n} ({dt:.1f} s) of the bench's synthetic input, one "
+                      f"fft.FFT call per row, {pool}"}
 
 
 if __name__ == "__main__":

@@ -128,20 +128,23 @@ struct Dft<16> {
 };
 
 // ---------------------------------------------------------------------------
-// Geometry of the one-kernel (LDS-resident) transform of N = 2^LOG2N points.
-template <int LOG2N>
+// Geometry of the one-kernel (LDS-resident) transform of N = 2^LOG2N points
+// with E = 2^LOG2E elements per thread (16 by default; 8 trades one more
+// radix-8 pass for half the data registers).
+template <int LOG2N, int LOG2E = 4>
 struct Geo {
   static constexpr int N = 1 << LOG2N;
-  static constexpr int E = N < 16 ? N : 16;       // elements per thread
-  static constexpr int T = N / E;                 // threads per transform
-  static constexpr int WG = T >= 256 ? T : 256;   // threads per workgroup
-  static constexpr int TPW = WG / T;              // transforms per workgroup
-  static constexpr int NP16 = LOG2N >= 4 ? LOG2N / 4 : 0;
-  static constexpr int REM = LOG2N >= 4 ? LOG2N % 4 : LOG2N;
-  static constexpr int NPASS = NP16 + (REM ? 1 : 0);
-  static constexpr int STRIDE = N + N / 16;       // padded doubles per transform
+  static constexpr int EMAX = 1 << LOG2E;
+  static constexpr int E = N < EMAX ? N : EMAX;    // elements per thread
+  static constexpr int T = N / E;                  // threads per transform
+  static constexpr int WG = T >= 256 ? T : 256;    // threads per workgroup
+  static constexpr int TPW = WG / T;               // transforms per workgroup
+  static constexpr int NPE = LOG2N >= LOG2E ? LOG2N / LOG2E : 0;  // radix-E passes
+  static constexpr int REM = LOG2N >= LOG2E ? LOG2N % LOG2E : LOG2N;
+  static constexpr int NPASS = NPE + (REM ? 1 : 0);
+  static constexpr int STRIDE = N + N / 16;        // padded doubles per transform
   static constexpr int LDS_DOUBLES = NPASS > 1 ? TPW * STRIDE : 1;
-  __host__ __device__ static constexpr int radix(int p) { return p < NP16 ? 16 : (1 << REM); }
+  __host__ __device__ static constexpr int radix(int p) { return p < NPE ? EMAX : (1 << REM); }
   __host__ __device__ static constexpr int ns(int p) { return p == 0 ? 1 : ns(p - 1) * radix(p - 1); }
 };
 
@@ -246,11 +249,15 @@ __device__ __forceinline__ int opaque_int(int v) {
   return v;
 }
 
-template <int LOG2N, bool SPLIT, bool OPAQUE = false, int P = 0>
-__device__ __forceinline__ void fft_regs(cd (&v)[Geo<LOG2N>::E], int t,
+// the thread's register array for a transform of geometry Geo<LOG2N, LOG2E>
+template <int LOG2N, int LOG2E = 4>
+using RegArr = cd[Geo<LOG2N, LOG2E>::E];
+
+template <int LOG2N, bool SPLIT, bool OPAQUE = false, int LOG2E = 4, int P = 0>
+__device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t,
                                          const cd *__restrict__ tw, double *lre, double *lim,
                                          bool first_exchange = true) {
-  using G = Geo<LOG2N>;
+  using G = Geo<LOG2N, LOG2E>;
   if constexpr (OPAQUE && P == 0 && G::NPASS > 1) {
     t = opaque_int(t);
     tw = opaque_ptr(tw);
@@ -265,7 +272,7 @@ __device__ __forceinline__ void fft_regs(cd (&v)[Geo<LOG2N>::E], int t,
       pass_exchange<G::N, G::E, G::T, RP, NSP, SPLIT>(v, t, lre, lim, first_exchange && P == 1);
     }
     pass_compute<G::N, G::E, G::T, R, NS>(v, t, tw);
-    fft_regs<LOG2N, SPLIT, false, P + 1>(v, t, tw, lre, lim, first_exchange);
+    fft_regs<LOG2N, SPLIT, false, LOG2E, P + 1>(v, t, tw, lre, lim, first_exchange);
   }
 }
 

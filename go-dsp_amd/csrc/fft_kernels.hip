@@ -69,12 +69,12 @@ __global__ __launch_bounds__(Geo<LOG2N>::WG) void fft_lds_kernel(
 //   r = IFFT_M(C) = conj(FFT_M(conj(C))) (1/M folded into bhat),
 //   X = r * conj(w), first n.  chirp[k] = conj(w_k) = exp(-i pi k^2/n).
 // Inverse (fft.IFFT of non-power-of-2 length): conj in, conj + 1/n out.
-template <int LOG2M, bool INV, bool SPLIT>
-__global__ __launch_bounds__(Geo<LOG2M>::WG) void bluestein_kernel(
+template <int LOG2M, bool INV, bool SPLIT, int LOG2E = 4>
+__global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
     const cd *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
     const cd *__restrict__ twm, const cd *__restrict__ chirp, const cd *__restrict__ bhat,
     double scale) {
-  using G = Geo<LOG2M>;
+  using G = Geo<LOG2M, LOG2E>;
   __shared__ double lds[(SPLIT ? 1 : 2) * G::LDS_DOUBLES];
   const int lt = threadIdx.x;
   const int slot = lt / G::T;
@@ -95,10 +95,10 @@ __global__ __launch_bounds__(Geo<LOG2M>::WG) void bluestein_kernel(
       v[k] = cmul(x, chirp[idx]);
     }
   }
-  fft_regs<LOG2M, SPLIT, true>(v, t, twm, lre, lim, true);
+  fft_regs<LOG2M, SPLIT, true, LOG2E>(v, t, twm, lre, lim, true);
 #pragma unroll
   for (int k = 0; k < G::E; ++k) v[k] = conjg(cmul(v[k], bhat[t + k * G::T]));
-  fft_regs<LOG2M, SPLIT, true>(v, t, twm, lre, lim, false);
+  fft_regs<LOG2M, SPLIT, true, LOG2E>(v, t, twm, lre, lim, false);
   chirp = opaque_ptr(chirp);
   const int to = opaque_int(t);
   if (valid) {
@@ -164,12 +164,12 @@ __global__ __launch_bounds__(256) void stockham_global_pass(
 // (|Z_k|^2 + |Z_{F-k}|^2)/2, so each thread accumulates |Z_k|^2 for its own
 // bins across all pairs of its worker, in registers; the k / F-k fold is done
 // once in gdsp_pwelch_finalize.
-template <int LOG2F, bool SPLIT>
-__global__ __launch_bounds__(Geo<LOG2F>::WG) void pwelch_kernel(
+template <int LOG2F, bool SPLIT, int LOG2E = 4>
+__global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_kernel(
     const double *__restrict__ x, int64_t nfft, int64_t stride, int64_t seg_begin,
     int64_t seg_end, int64_t pairs_per_worker, const double *__restrict__ win,
     const cd *__restrict__ tw, double *__restrict__ partial) {
-  using G = Geo<LOG2F>;
+  using G = Geo<LOG2F, LOG2E>;
   __shared__ double lds[(SPLIT ? 1 : 2) * G::LDS_DOUBLES];
   const int lt = threadIdx.x;
   const int slot = lt / G::T;
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(Geo<LOG2F>::WG) void pwelch_kernel(
       const double b = (has1 && in_seg) ? x1[i] : 0.0;
       v[k] = {a * wk, b * wk};
     }
-    fft_regs<LOG2F, SPLIT, true>(v, tt, tw, lre, lim, it == 0);
+    fft_regs<LOG2F, SPLIT, true, LOG2E>(v, tt, tw, lre, lim, it == 0);
     if (active) {
 #pragma unroll
       for (int k = 0; k < G::E; ++k) acc[k] += v[k].x * v[k].x + v[k].y * v[k].y;

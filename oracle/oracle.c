@@ -430,10 +430,75 @@ static int radix2_threaded(const cplx *x, cplx *out, int64_t n, int nworkers, po
   return OR_OK;
 }
 
+/* fft.FFT with the reference's worker pool for every radix-2 transform,
+ * including the three inside Bluestein's Convolve (bluestein.go:87 ->
+ * fft.go:60-68 -> radix2.go:80). Same arithmetic as or_fft. */
+static int fft_t(const cplx *x, cplx *out, int64_t n, int nworkers);
+
+static int ifft_t(const cplx *x, cplx *out, int64_t n, int nworkers) {
+  if (n <= 0) return OR_ERR_EMPTY;
+  cplx *r = (cplx *)malloc((size_t)n * sizeof(cplx));
+  if (!r) return OR_ERR_NOMEM;
+  r[0] = x[0];
+  for (int64_t i = 1; i < n; i++) r[i] = x[n - i];
+  int st = fft_t(r, out, n, nworkers);
+  free(r);
+  if (st) return st;
+  for (int64_t i = 0; i < n; i++) {
+    out[i].re /= (double)n;
+    out[i].im /= (double)n;
+  }
+  return OR_OK;
+}
+
+static int bluestein_t(const cplx *x, cplx *out, int64_t n, int nworkers) {
+  int64_t m = or_next_pow2(n * 2 - 1);
+  cplx *wi = (cplx *)malloc((size_t)n * sizeof(cplx));
+  cplx *a = (cplx *)calloc((size_t)m, sizeof(cplx));
+  cplx *b = (cplx *)calloc((size_t)m, sizeof(cplx));
+  cplx *fa = (cplx *)malloc((size_t)m * sizeof(cplx));
+  cplx *fb = (cplx *)malloc((size_t)m * sizeof(cplx));
+  cplx *r = (cplx *)malloc((size_t)m * sizeof(cplx));
+  int st = OR_ERR_NOMEM;
+  if (wi && a && b && fa && fb && r) {
+    for (int64_t i = 0; i < n; i++) {
+      double sn = 0, cs = 1;
+      if (i != 0) sincos(M_PI / (double)n * (double)(i * i), &sn, &cs);
+      wi[i] = (cplx){cs, -sn};
+      b[i] = (cplx){cs, sn};
+      if (i != 0) b[m - i] = b[i];
+    }
+    for (int64_t i = 0; i < n; i++) a[i] = cmul(x[i], wi[i]);
+    st = fft_t(a, fa, m, nworkers);
+    if (!st) st = fft_t(b, fb, m, nworkers);
+    if (!st) {
+      for (int64_t i = 0; i < m; i++) fa[i] = cmul(fa[i], fb[i]);
+      st = ifft_t(fa, r, m, nworkers);
+    }
+    if (!st)
+      for (int64_t i = 0; i < n; i++) out[i] = cmul(r[i], wi[i]);
+  }
+  free(wi);
+  free(a);
+  free(b);
+  free(fa);
+  free(fb);
+  free(r);
+  return st;
+}
+
+static int fft_t(const cplx *x, cplx *out, int64_t n, int nworkers) {
+  if (n <= 1) {
+    if (n == 1) out[0] = x[0];
+    return OR_OK;
+  }
+  if (or_is_pow2(n)) return radix2_threaded(x, out, n, nworkers, get_pool(nworkers));
+  return bluestein_t(x, out, n, nworkers);
+}
+
 int or_fft_threaded(const double *x, double *out, int64_t n, int nworkers) {
   if (nworkers <= 0) nworkers = 1;
-  if (n <= 1 || !or_is_pow2(n)) return or_fft(x, out, n);
-  return radix2_threaded((const cplx *)x, (cplx *)out, n, nworkers, get_pool(nworkers));
+  return fft_t((const cplx *)x, (cplx *)out, n, nworkers);
 }
 
 int or_fft_rows_threaded(const double *x, double *out, int64_t n, int64_t rows,
@@ -511,9 +576,27 @@ int64_t or_segment_count(int64_t lx, int64_t size, int64_t noverlap) {
 }
 
 /* ---- spectral/pwelch.go:74-145 ------------------------------------------- */
+static int pwelch_impl(const double *x_in, int64_t n, double fs, int64_t nfft, int64_t pad,
+                       int64_t noverlap, int window_kind, int scale_off, double *pxx,
+                       double *freqs, int64_t *lp_out, int nworkers);
+
 int or_pwelch(const double *x_in, int64_t n, double fs, int64_t nfft, int64_t pad,
               int64_t noverlap, int window_kind, int scale_off, double *pxx,
               double *freqs, int64_t *lp_out) {
+  return pwelch_impl(x_in, n, fs, nfft, pad, noverlap, window_kind, scale_off, pxx, freqs,
+                     lp_out, 0);
+}
+
+int or_pwelch_threaded(const double *x_in, int64_t n, double fs, int64_t nfft, int64_t pad,
+                       int64_t noverlap, int window_kind, int scale_off, double *pxx,
+                       double *freqs, int64_t *lp_out, int nworkers) {
+  return pwelch_impl(x_in, n, fs, nfft, pad, noverlap, window_kind, scale_off, pxx, freqs,
+                     lp_out, nworkers < 1 ? 1 : nworkers);
+}
+
+static int pwelch_impl(const double *x_in, int64_t n, double fs, int64_t nfft, int64_t pad,
+                       int64_t noverlap, int window_kind, int scale_off, double *pxx,
+                       double *freqs, int64_t *lp_out, int nworkers) {
   if (n == 0) {
     *lp_out = 0;
     return OR_OK;
@@ -542,10 +625,12 @@ int or_pwelch(const double *x_in, int64_t n, double fs, int64_t nfft, int64_t pa
   double *seg = (double *)malloc((size_t)flen * sizeof(double));
   double *win = (double *)malloc((size_t)flen * sizeof(double));
   double *pg = (double *)malloc((size_t)flen * 2 * sizeof(double));
-  if (!seg || !win || !pg) {
+  double *cbuf = (double *)malloc((size_t)flen * 2 * sizeof(double));
+  if (!seg || !win || !pg || !cbuf) {
     free(seg);
     free(win);
     free(pg);
+    free(cbuf);
     free(xpad);
     return OR_ERR_NOMEM;
   }
@@ -556,7 +641,15 @@ int or_pwelch(const double *x_in, int64_t n, double fs, int64_t nfft, int64_t pa
     memcpy(seg, x + s * stride, (size_t)nfft * sizeof(double));
     for (int64_t i = nfft; i < flen; i++) seg[i] = 0;
     for (int64_t i = 0; i < flen; i++) seg[i] *= win[i];
-    or_fft_real(seg, pg, flen);
+    if (nworkers > 0) { /* FFTReal (ToComplex + FFT) with the reference's worker pool */
+      for (int64_t i = 0; i < flen; i++) {
+        cbuf[2 * i] = seg[i];
+        cbuf[2 * i + 1] = 0;
+      }
+      or_fft_threaded(cbuf, pg, flen, nworkers);
+    } else {
+      or_fft_real(seg, pg, flen);
+    }
     for (int64_t j = 0; j < lp; j++) {
       double a = pg[2 * j], b = pg[2 * j + 1];
       /* real(conj(z)*z) = a*a - (-b)*b */
@@ -579,6 +672,7 @@ int or_pwelch(const double *x_in, int64_t n, double fs, int64_t nfft, int64_t pa
   free(seg);
   free(win);
   free(pg);
+  free(cbuf);
   free(xpad);
   return OR_OK;
 }

@@ -84,6 +84,12 @@ int or_pwelch(const double *x, int64_t n, double fs, int64_t nfft, int64_t pad,
               int64_t noverlap, int window_kind, int scale_off, double *pxx,
               double *freqs, int64_t *lp_out);
 
+/* or_pwelch with the reference's worker pool inside every FFTReal (the CPU
+ * baseline of bench.py). */
+int or_pwelch_threaded(const double *x, int64_t n, double fs, int64_t nfft, int64_t pad,
+                       int64_t noverlap, int window_kind, int scale_off, double *pxx,
+                       double *freqs, int64_t *lp_out, int nworkers);
+
 /* Counter-based synthetic input generator shared with the device generator
  * (splitmix64; see DESIGN.md §Synthetic data): uniform [-1, 1). */
 void or_fill_uniform(double *out, int64_t count, uint64_t seed, uint64_t offset);

@@ -51,6 +51,9 @@ def lib():
             f = getattr(L, name)
             f.argtypes = args
             f.restype = ctypes.c_int
+        L.or_pwelch_threaded.argtypes = [P, I64, ctypes.c_double, I64, I64, I64, ctypes.c_int,
+                                         ctypes.c_int, P, P, P, ctypes.c_int]
+        L.or_pwelch_threaded.restype = ctypes.c_int
         L.or_segment_count.argtypes = [I64, I64, I64]
         L.or_segment_count.restype = I64
         L.or_reverse_bits.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
@@ -213,6 +216,19 @@ def pwelch(x, fs: float, nfft: int = 0, pad: int = 0, noverlap: int = 0,
                            WINDOWS[window_kind], int(scale_off), _p(pxx), _p(freqs),
                            ctypes.byref(lpo)), "pwelch")
     return pxx[:lpo.value].copy(), freqs[:lpo.value].copy()
+
+
+def pwelch_threaded(x, fs: float, nfft: int, noverlap: int, nworkers: int):
+    """spectral.Pwelch with the reference's worker pool in every FFT (CPU
+    baseline only)."""
+    x = _f(x)
+    lp = (nfft or 256) // 2 + 1
+    pxx = np.empty(lp, np.float64)
+    freqs = np.empty(lp, np.float64)
+    lpo = ctypes.c_int64(0)
+    _check(lib().or_pwelch_threaded(_p(x), x.size, float(fs), nfft, 0, noverlap, 0, 0, _p(pxx),
+                                    _p(freqs), ctypes.byref(lpo), nworkers), "pwelch_threaded")
+    return pxx, freqs
 
 
 def fill_uniform(count: int, seed: int, offset: int = 0) -> np.ndarray:

@@ -6,7 +6,7 @@ timeout -k 10 900 python -m pytest tests -m gpu -q -rf --timeout 300 > gpurun_ou
 echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 for w in radix4096 bluestein3000 fft2_8192 pwelch; do
-  cs=0; [ $w = radix4096 ] && cs=10
+  cs=10
   timeout -k 10 300 python bench.py --workload $w --steps 20 --warmup 3 --cpu-seconds $cs > gpurun_out/bench_$w.json 2> gpurun_out/bench_$w.err; rc=$?
   echo "== $w rc=$rc"; cat gpurun_out/bench_$w.json; [ $rc -eq 0 ] || { tail -20 gpurun_out/bench_$w.err; exit $rc; }
 done

@@ -15,7 +15,7 @@
 #include <algorithm>
 #include <vector>
 
-#include "fft_device.hpp"
+#include "fft_kernels.hip"
 
 using namespace gdsp;
 
@@ -162,6 +162,63 @@ __global__ __launch_bounds__(256) void copy_gs(const cd *__restrict__ in, cd *__
     for (int k = 0; k < U; ++k) out[base + k * 256] = v[k];
   }
 }
+// 64 KiB per workgroup, each wave owning a contiguous 16 KiB quarter
+__global__ __launch_bounds__(256) void copy_wave_contig(const cd *__restrict__ in,
+                                                        cd *__restrict__ out, int64_t cnt) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int64_t base = blockIdx.x * (int64_t)4096 + w * 1024 + l;
+  cd v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = in[base + k * 64];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) out[base + k * 64] = v[k];
+}
+// our shape with an XCD-aware row map: the blocks one XCD runs (b % 8 equal)
+// take consecutive rows
+__global__ __launch_bounds__(256) void copy_xcd(const cd *__restrict__ in, cd *__restrict__ out,
+                                                int64_t cnt) {
+  const int64_t nb = gridDim.x;
+  const int64_t row = (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8;
+  const int64_t base = row * 4096 + threadIdx.x;
+  cd v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = in[base + k * 256];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) out[base + k * 256] = v[k];
+}
+// two rows per 512-thread workgroup, 16 loads per thread
+__global__ __launch_bounds__(512) void copy_two(const cd *__restrict__ in, cd *__restrict__ out,
+                                                int64_t cnt) {
+  const int64_t base = (blockIdx.x * (int64_t)2 + (threadIdx.x >> 8)) * 4096 + (threadIdx.x & 255);
+  cd v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = in[base + k * 256];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) out[base + k * 256] = v[k];
+}
+// our shape, stores in reverse k order (changes read/write interleaving)
+__global__ __launch_bounds__(256) void copy_revst(const cd *__restrict__ in, cd *__restrict__ out,
+                                                  int64_t cnt) {
+  const int64_t base = blockIdx.x * (int64_t)4096 + threadIdx.x;
+  cd v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = in[base + k * 256];
+#pragma unroll
+  for (int k = 15; k >= 0; --k) out[base + k * 256] = v[k];
+}
+void l_cwc(const cd *in, cd *out, int64_t b, const cd *, hipStream_t s) {
+  hipLaunchKernelGGL(copy_wave_contig, dim3((unsigned)b), dim3(256), 0, s, in, out, b * 4096);
+}
+void l_cxcd(const cd *in, cd *out, int64_t b, const cd *, hipStream_t s) {
+  hipLaunchKernelGGL(copy_xcd, dim3((unsigned)b), dim3(256), 0, s, in, out, b * 4096);
+}
+void l_ctwo(const cd *in, cd *out, int64_t b, const cd *, hipStream_t s) {
+  hipLaunchKernelGGL(copy_two, dim3((unsigned)(b / 2)), dim3(512), 0, s, in, out, b * 4096);
+}
+void l_crev(const cd *in, cd *out, int64_t b, const cd *, hipStream_t s) {
+  hipLaunchKernelGGL(copy_revst, dim3((unsigned)b), dim3(256), 0, s, in, out, b * 4096);
+}
+
 __global__ __launch_bounds__(256) void read_only(const cd *__restrict__ in, cd *__restrict__ out,
                                                  int64_t cnt) {
   const int64_t base = blockIdx.x * (int64_t)(256 * 16) + threadIdx.x;
@@ -201,6 +258,29 @@ void l_write(const cd *in, cd *out, int64_t b, const cd *, hipStream_t s) {
   hipLaunchKernelGGL(write_only, dim3((unsigned)b), dim3(256), 0, s, in, out, b * 4096);
 }
 
+// production Pwelch / Bluestein kernels at different elements-per-thread
+double *g_x1g, *g_win, *g_part;
+cd *g_chirp, *g_bhat, *g_tw8192;
+template <int LOG2E>
+void l_pwelch(const cd *in, cd *out, int64_t b, const cd *tw, hipStream_t s) {
+  // 2^29 samples (the 4 GiB input buffer viewed as float64), NFFT 4096, 50 %
+  using G = Geo<12, LOG2E>;
+  const int64_t nsamp = (int64_t)1 << 29, nfft = 4096, stride = 2048;  // the 4 GiB input buffer
+  const int64_t nseg = (nsamp - nfft) / stride + 1, npairs = (nseg + 1) / 2;
+  const int64_t nworkers = 2048 * G::TPW;
+  const int64_t ppw = (npairs + nworkers - 1) / nworkers;
+  const int64_t nw = (npairs + ppw - 1) / ppw;
+  hipLaunchKernelGGL((pwelch_kernel<12, true, LOG2E>), dim3((unsigned)((nw + G::TPW - 1) / G::TPW)),
+                     dim3(G::WG), 0, s, (const double *)in, nfft, stride, (int64_t)0, nseg, ppw,
+                     (const double *)g_win, tw, g_part);
+}
+template <int LOG2E>
+void l_blu_prod(const cd *in, cd *out, int64_t b, const cd *, hipStream_t s) {
+  using G = Geo<13, LOG2E>;
+  hipLaunchKernelGGL((bluestein_kernel<13, false, true, LOG2E>), dim3((unsigned)((b + G::TPW - 1) / G::TPW)),
+                     dim3(G::WG), 0, s, in, out, (int64_t)3000, b, g_tw8192, g_chirp, g_bhat, 1.0);
+}
+
 struct Variant {
   const char *name;
   void (*launch)(const cd *, cd *, int64_t, const cd *, hipStream_t);
@@ -217,7 +297,6 @@ void launch_comp(const cd *in, cd *out, int64_t batch, const cd *tw, hipStream_t
   hipLaunchKernelGGL((fft4096_compute<MINW>), dim3((unsigned)batch), dim3(256), 0, s, in, out,
                      batch, tw);
 }
-cd *g_chirp, *g_bhat, *g_tw8192;
 template <int MINW, bool SB = false>
 void launch_blu(const cd *in, cd *out, int64_t batch, const cd *, hipStream_t s) {
   hipLaunchKernelGGL((blu_v<MINW, SB>), dim3((unsigned)batch), dim3(512), 0, s, in, out, batch,
@@ -268,6 +347,11 @@ int main(int argc, char **argv) {
     CHECK(hipMemcpy(g_tw8192, t8.data(), 8192 * sizeof(cd), hipMemcpyHostToDevice));
     CHECK(hipMemcpy(g_chirp, t8.data(), 8192 * sizeof(cd), hipMemcpyHostToDevice));
     CHECK(hipMemcpy(g_bhat, t8.data(), 8192 * sizeof(cd), hipMemcpyHostToDevice));
+    std::vector<double> w(4096);
+    for (int i = 0; i < 4096; ++i) w[i] = 0.5 * (1 - cos(2 * M_PI * i / 4095.0));
+    CHECK(hipMalloc(&g_win, 4096 * sizeof(double)));
+    CHECK(hipMemcpy(g_win, w.data(), 4096 * sizeof(double), hipMemcpyHostToDevice));
+    CHECK(hipMalloc(&g_part, (size_t)2 * 2048 * 4096 * sizeof(double)));
   }
   CHECK(hipDeviceSynchronize());
 
@@ -282,6 +366,10 @@ int main(int argc, char **argv) {
       {"twobuf_w3", launch_v<false, false, false, 3>, true},
       {"compute_only", launch_comp<1>, false},
       {"compute_only_w4", launch_comp<4>, false},
+      {"pwelch_e16", l_pwelch<4>, false},
+      {"pwelch_e8", l_pwelch<3>, false},
+      {"blu_prod_e16", l_blu_prod<4>, false},
+      {"blu_prod_e8", l_blu_prod<3>, false},
       {"blu3000", launch_blu<1>, false},
       {"blu3000_w4", launch_blu<4>, false},
       {"blu3000_w3", launch_blu<3>, false},
@@ -290,6 +378,10 @@ int main(int argc, char **argv) {
       {"copy", launch_c<false, false>, false},
       {"copy_ntl_nts", launch_c<true, true>, false},
       {"copy_one", l_copy_one, false},
+      {"copy_wave_contig", l_cwc, false},
+      {"copy_xcd", l_cxcd, false},
+      {"copy_two", l_ctwo, false},
+      {"copy_revst", l_crev, false},
       {"copy_u2", l_copy_unroll<2>, false},
       {"copy_u4", l_copy_unroll<4>, false},
       {"copy_u8", l_copy_unroll<8>, false},
