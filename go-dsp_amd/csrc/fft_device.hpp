@@ -148,6 +148,17 @@ struct Geo {
   __host__ __device__ static constexpr int ns(int p) { return p == 0 ? 1 : ns(p - 1) * radix(p - 1); }
 };
 
+// XCD-aware workgroup -> row-group map. Workgroups are dealt round-robin
+// over the 8 XCDs (b and b+8 share one), so this gives each XCD a contiguous
+// run of rows: the rows an XCD streams at any moment are neighbours in HBM.
+// Speed only (MI355X_MICROARCH.md: placement is never a correctness
+// property); measured +8.5 % on a 64 KiB-per-workgroup copy and +3 % on the
+// N = 4096 batch. Bijective: the tail past a multiple of 8 maps to itself.
+__device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nb) {
+  const int64_t full = nb & ~(int64_t)7;
+  return b < full ? (b & 7) * (full >> 3) + (b >> 3) : b;
+}
+
 // one padding slot every 16 doubles keeps the stride-16 writes of pass 0
 // conflict-free for ds_write_b64 (bank = (addr/4) mod 32 per 16-lane group)
 __device__ __forceinline__ int padi(int i) { return i + (i >> 4); }

@@ -30,7 +30,7 @@ __global__ __launch_bounds__(Geo<LOG2N>::WG) void fft_lds_kernel(
   const int lt = threadIdx.x;
   const int slot = lt / G::T;
   const int t = lt & (G::T - 1);
-  const int64_t g = (int64_t)blockIdx.x * G::TPW + slot;
+  const int64_t g = xcd_remap(blockIdx.x, gridDim.x) * G::TPW + slot;
   // Only the last workgroup can hold slots past the batch (TPW > 1); they
   // load a valid row (clamped) and skip the store, so loads stay
   // branch-free and the whole workgroup reaches every barrier.
@@ -79,7 +79,7 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
   const int lt = threadIdx.x;
   const int slot = lt / G::T;
   const int t = lt & (G::T - 1);
-  const int64_t g = (int64_t)blockIdx.x * G::TPW + slot;
+  const int64_t g = xcd_remap(blockIdx.x, gridDim.x) * G::TPW + slot;
   const bool valid = g < batch;
   double *lre = lds + slot * G::STRIDE;
   double *lim = SPLIT ? lre : lds + G::LDS_DOUBLES + slot * G::STRIDE;

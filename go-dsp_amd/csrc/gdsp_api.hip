@@ -530,10 +530,9 @@ int gdsp_fft2_device(const void *d_in, void *d_out, int64_t rows, int64_t cols, 
   if (rows <= 0) return fail(GDSP_ERR_EMPTY, "empty input array");
   if (cols < 0) return fail(GDSP_ERR_INVALID, "negative size");
   if (cols == 0) return GDSP_OK;
-  hipStream_t s = (hipStream_t)stream;
+  hipStream_t s = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
   int dev = 0;
   STCHK(current_device(&dev));
-  if (!s) s = thread_stream(dev);
   gdsp_plan *pr = nullptr, *pc = nullptr;
   STCHK(get_plan(rows, &pr));
   STCHK(get_plan(cols, &pc));
@@ -571,7 +570,7 @@ static int fft2_host(const double *x, bool real_in, double *out, int64_t rows, i
   } else {
     STCHK(copy_h2d(din.p, x, cnt * sizeof(cd), s));
   }
-  STCHK(gdsp_fft2_device(din.p, dout.p, rows, cols, inverse, nullptr, s));
+  STCHK(gdsp_fft2_device(din.p, dout.p, rows, cols, inverse, nullptr, (void *)s));
   STCHK(copy_d2h(out, dout.p, cnt * sizeof(cd), s));
   return GDSP_OK;
 }
@@ -617,9 +616,8 @@ int gdsp_fft_batch_device(const gdsp_plan *plan, const void *d_in, void *d_out, 
                           int inverse, void *stream) {
   if (!plan || batch < 0) return fail(GDSP_ERR_INVALID, "bad argument");
   if (plan->n == 0 && inverse) return fail(GDSP_ERR_EMPTY, "IFFT of an empty slice");
-  hipStream_t s = (hipStream_t)stream;
-  if (!s) s = thread_stream(plan->device);
-  return exec_plan(plan, d_in, (cd *)d_out, batch, inverse != 0, gdsp::LOAD_COMPLEX, s);
+  return exec_plan(plan, d_in, (cd *)d_out, batch, inverse != 0, gdsp::LOAD_COMPLEX,
+                   (hipStream_t)stream);
 }
 
 int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, int64_t pad,
@@ -632,10 +630,7 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
   if ((seg_end - 1) * stride + nfft > n && seg_end > 1)
     return fail(GDSP_ERR_INVALID, "segments exceed the signal");
   const int64_t flen = pad > nfft ? pad : nfft;
-  int dev = 0;
-  STCHK(current_device(&dev));
-  hipStream_t s = (hipStream_t)stream;
-  if (!s) s = thread_stream(dev);
+  hipStream_t s = (hipStream_t)stream;  // NULL = the null stream
   gdsp_plan *p = nullptr;
   STCHK(get_plan(flen, &p));
   const int64_t nseg = seg_end - seg_begin;
@@ -754,13 +749,9 @@ int gdsp_pwelch(const double *x, int64_t n, double fs, int64_t nfft, int64_t pad
 int gdsp_fill_uniform_device(double *d_out, int64_t count, uint64_t seed, uint64_t offset,
                              void *stream) {
   if (count < 0 || (!d_out && count)) return fail(GDSP_ERR_INVALID, "bad argument");
-  hipStream_t s = (hipStream_t)stream;
-  if (!s) {
-    int dev = 0;
-    STCHK(current_device(&dev));
-    s = thread_stream(dev);
-  }
-  HIPCHK(gdsp::launch_fill_uniform(d_out, count, seed, offset, s));
+  int dev = 0;
+  STCHK(current_device(&dev));
+  HIPCHK(gdsp::launch_fill_uniform(d_out, count, seed, offset, (hipStream_t)stream));
   return GDSP_OK;
 }
 

@@ -18,8 +18,8 @@
  *    the reference's message (gdsp_status_string);
  *  - host-pointer entry points are synchronous and thread-safe; device-pointer
  *    entry points ("_device") are stream-ordered on the given hipStream_t
- *    (passed as void*, NULL = the library's per-thread stream) and run on the
- *    calling thread's current HIP device.
+ *    (passed as void*; NULL = the null/default stream, as in HIP) and run on
+ *    the calling thread's current HIP device.
  */
 #ifndef GDSP_FFT_H
 #define GDSP_FFT_H
@@ -136,7 +136,8 @@ typedef struct gdsp_plan gdsp_plan;
 int gdsp_plan_create(int64_t n, gdsp_plan **plan);
 int gdsp_plan_destroy(gdsp_plan *plan);
 /* Which algorithm a plan runs: 0 trivial (n<=1), 1 one-kernel LDS Stockham,
- * 2 multi-pass global Stockham (large power of 2), 3 fused Bluestein. */
+ * 2 multi-pass global Stockham (large power of 2), 3 fused Bluestein,
+ * 4 composed Bluestein (M > 16384). */
 int gdsp_plan_kind(const gdsp_plan *plan);
 
 /* Batched C2C on device buffers: d_in/d_out hold batch*n complex128 (may

@@ -105,7 +105,10 @@ def test_pwelch_fullsize(dev, oracle):
         dev.pwelch_accumulate(x[s2.sample_lo:s2.sample_hi], nfft, nfft, nov, 0,
                               s2.seg_hi - s2.seg_lo, win, two)
     a, b = one.cpu().numpy(), two.cpu().numpy()
-    assert np.linalg.norm(a - b) / np.linalg.norm(a) < 1e-12
+    # packed segment pairs: only acc[k] + acc[F-k] = 2 sum(|X_s,k|^2) is
+    # pairing-independent (a shard boundary at an odd segment re-pairs them)
+    fold = lambda v: v + np.roll(v[::-1], 1)  # noqa: E731
+    assert np.linalg.norm(fold(a) - fold(b)) / np.linalg.norm(fold(a)) < 1e-12
     p, _ = gdsp.spectral.finalize(a, S, nfft, nfft, gdsp.window.Hann(nfft), 1.0, False)
     assert np.all(np.isfinite(p)) and p.size == nfft // 2 + 1
     # the uniform[-1,1) stream is white: Pxx ~ variance(1/3) * 2 / Fs in the interior

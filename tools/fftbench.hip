@@ -47,14 +47,18 @@ __device__ __forceinline__ void st(cd *p, cd v) {
 }
 
 // Variant kernel: LOG2N = 12 (T = 256, one transform per workgroup).
-template <bool SPLIT, bool NTL, bool NTS, int MINW>
+template <bool SPLIT, bool NTL, bool NTS, int MINW, bool XCD = false>
 __global__ __launch_bounds__(256, MINW) void fft4096_v(const cd *__restrict__ in,
                                                         cd *__restrict__ out, int64_t batch,
                                                         const cd *__restrict__ tw) {
   using G = Geo<12>;
   __shared__ double lds[(SPLIT ? 1 : 2) * G::LDS_DOUBLES];
   const int t = threadIdx.x;
-  const int64_t g = blockIdx.x;
+  int64_t g = blockIdx.x;
+  if constexpr (XCD) {
+    const int64_t nb = gridDim.x, full = nb & ~(int64_t)7;
+    if (g < full) g = (g & 7) * (full >> 3) + (g >> 3);
+  }
   double *lre = lds;
   double *lim = SPLIT ? lds : lds + G::LDS_DOUBLES;
   cd v[16];
@@ -287,9 +291,9 @@ struct Variant {
   bool is_fft;
 };
 
-template <bool SPLIT, bool NTL, bool NTS, int MINW>
+template <bool SPLIT, bool NTL, bool NTS, int MINW, bool XCD = false>
 void launch_v(const cd *in, cd *out, int64_t batch, const cd *tw, hipStream_t s) {
-  hipLaunchKernelGGL((fft4096_v<SPLIT, NTL, NTS, MINW>), dim3((unsigned)batch), dim3(256), 0, s,
+  hipLaunchKernelGGL((fft4096_v<SPLIT, NTL, NTS, MINW, XCD>), dim3((unsigned)batch), dim3(256), 0, s,
                      in, out, batch, tw);
 }
 template <int MINW>
@@ -357,6 +361,9 @@ int main(int argc, char **argv) {
 
   std::vector<Variant> vs = {
       {"split", launch_v<true, false, false, 1>, true},
+      {"split_xcd", launch_v<true, false, false, 1, true>, true},
+      {"twobuf_xcd", launch_v<false, false, false, 1, true>, true},
+      {"split_w3_xcd", launch_v<true, false, false, 3, true>, true},
       {"split_ntl", launch_v<true, true, false, 1>, true},
       {"split_nts", launch_v<true, false, true, 1>, true},
       {"split_ntl_nts", launch_v<true, true, true, 1>, true},
