@@ -206,7 +206,16 @@ __device__ __forceinline__ void pass_compute(cd (&v)[E], int t, const cd *__rest
 // goes to (j/NS)*NS*R + j%NS + r*NS, then every thread reads back t + k*T.
 // SPLIT: real and imaginary halves go through one N-double buffer in turn
 // (half the LDS, two more barriers); otherwise two buffers.
-template <int N, int E, int T, int R, int NS, bool SPLIT>
+// LDS offset of element i of a transform: padded contiguous (ILV = 0), or
+// interleaved with ILV transforms (element-major, transform-minor: the
+// column tiles of FFT2, where neighbouring lanes are neighbouring columns).
+template <int ILV>
+__device__ __forceinline__ int lds_off(int i) {
+  if constexpr (ILV == 0) return padi(i);
+  else return i * ILV;
+}
+
+template <int N, int E, int T, int R, int NS, bool SPLIT, int ILV = 0>
 __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, double *lim,
                                               bool first) {
   constexpr int B = E / R;
@@ -216,7 +225,7 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
     const int j = t + b * T;
     const int base = (j / NS) * (NS * R) + (j & (NS - 1));
 #pragma unroll
-    for (int r = 0; r < R; ++r) dst[b + r * B] = padi(base + r * NS);
+    for (int r = 0; r < R; ++r) dst[b + r * B] = lds_off<ILV>(base + r * NS);
   }
   if (!first) __syncthreads();
   if constexpr (SPLIT) {
@@ -224,13 +233,13 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
     for (int k = 0; k < E; ++k) lre[dst[k]] = v[k].x;
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < E; ++k) v[k].x = lre[padi(t + k * T)];
+    for (int k = 0; k < E; ++k) v[k].x = lre[lds_off<ILV>(t + k * T)];
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < E; ++k) lre[dst[k]] = v[k].y;
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < E; ++k) v[k].y = lre[padi(t + k * T)];
+    for (int k = 0; k < E; ++k) v[k].y = lre[lds_off<ILV>(t + k * T)];
   } else {
 #pragma unroll
     for (int k = 0; k < E; ++k) {
@@ -239,7 +248,8 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < E; ++k) v[k] = {lre[padi(t + k * T)], lim[padi(t + k * T)]};
+    for (int k = 0; k < E; ++k)
+      v[k] = {lre[lds_off<ILV>(t + k * T)], lim[lds_off<ILV>(t + k * T)]};
   }
 }
 
@@ -264,7 +274,7 @@ __device__ __forceinline__ int opaque_int(int v) {
 template <int LOG2N, int LOG2E = 4>
 using RegArr = cd[Geo<LOG2N, LOG2E>::E];
 
-template <int LOG2N, bool SPLIT, bool OPAQUE = false, int LOG2E = 4, int P = 0>
+template <int LOG2N, bool SPLIT, bool OPAQUE = false, int LOG2E = 4, int ILV = 0, int P = 0>
 __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t,
                                          const cd *__restrict__ tw, double *lre, double *lim,
                                          bool first_exchange = true) {
@@ -280,10 +290,11 @@ __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t,
       // exchange after the previous pass
       constexpr int RP = G::radix(P - 1);
       constexpr int NSP = G::ns(P - 1);
-      pass_exchange<G::N, G::E, G::T, RP, NSP, SPLIT>(v, t, lre, lim, first_exchange && P == 1);
+      pass_exchange<G::N, G::E, G::T, RP, NSP, SPLIT, ILV>(v, t, lre, lim,
+                                                            first_exchange && P == 1);
     }
     pass_compute<G::N, G::E, G::T, R, NS>(v, t, tw);
-    fft_regs<LOG2N, SPLIT, false, LOG2E, P + 1>(v, t, tw, lre, lim, first_exchange);
+    fft_regs<LOG2N, SPLIT, false, LOG2E, ILV, P + 1>(v, t, tw, lre, lim, first_exchange);
   }
 }
 

@@ -267,6 +267,52 @@ __global__ void power_accumulate_kernel(const cd *__restrict__ buf, int64_t nseg
   acc[k] += s;
 }
 
+// ----------------------------------------------------------------------------
+// FFT2 column pass on tiles of L rows x CW columns of a row-major matrix with
+// row length C (fft/fft.go:138-147 without the gather/scatter copies). Thread
+// (c, t), c fastest, owns column blockIdx.x*CW + c and tile elements
+// j = t + k*T, so every load/store wave-instruction covers whole 128..1024-B
+// row segments. Tile row j of row group q is matrix row q*step + j*stride
+// (in and out separately), which expresses both steps of the four-step split
+// R = R1*R2 used for long columns:
+//   A: q = n2 < R2, rows n2 + R2*j, DFT_R1, times W_R^(n2*k1), in place;
+//   B: q = k1 < R1, rows R2*k1 + j, DFT_R2, out rows k1 + R1*k2.
+template <int LOG2L, bool CONJ_IN, bool TWIDDLE, bool CONJ_SCALE_OUT>
+__global__ __launch_bounds__(256) void colfft_tile_kernel(
+    const cd *__restrict__ in, cd *__restrict__ out, int64_t C, int64_t in_step,
+    int64_t in_stride, int64_t out_step, int64_t out_stride, const cd *__restrict__ twl,
+    const cd *__restrict__ twr, int log2r, double scale) {
+  using G = Geo<LOG2L>;
+  static_assert(G::T <= 256, "tile column length too large");
+  constexpr int CW = 256 / G::T;
+  __shared__ double lds[G::NPASS > 1 ? CW * G::N : 1];
+  const int lt = threadIdx.x;
+  const int c = lt & (CW - 1);
+  const int t = lt / CW;
+  const int64_t col = (int64_t)blockIdx.x * CW + c;
+  const int64_t cl = col < C ? col : C - 1;  // partial last block: load a valid column
+  const int64_t q = blockIdx.y;
+  const cd *src = in + q * in_step * C + cl;
+  cd v[G::E];
+#pragma unroll
+  for (int k = 0; k < G::E; ++k) {
+    v[k] = src[(int64_t)(t + k * G::T) * in_stride * C];
+    if constexpr (CONJ_IN) v[k].y = -v[k].y;
+  }
+  fft_regs<LOG2L, true, false, 4, CW>(v, t, twl, lds + c, lds + c);
+  if (col < C) {
+    cd *dst = out + q * out_step * C + col;
+#pragma unroll
+    for (int k = 0; k < G::E; ++k) {
+      const int64_t j = t + k * G::T;
+      cd o = v[k];
+      if constexpr (TWIDDLE) o = cmul(o, twr[(q * j) & (((int64_t)1 << log2r) - 1)]);
+      if constexpr (CONJ_SCALE_OUT) o = {o.x * scale, -o.y * scale};
+      dst[j * out_stride * C] = o;
+    }
+  }
+}
+
 // out[c*rows + r] = in[r*cols + c] through a 32x33 LDS tile (complex128).
 __global__ __launch_bounds__(256) void transpose_kernel(const cd *__restrict__ in,
                                                         cd *__restrict__ out, int64_t rows,
@@ -548,6 +594,47 @@ hipError_t launch_power_accumulate(const cd *buf, int64_t nseg, int64_t flen, do
   hipLaunchKernelGGL(power_accumulate_kernel, dim3(blocks_for(flen, 256)), dim3(256), 0, s, buf,
                      nseg, flen, acc);
   return hipGetLastError();
+}
+
+template <int LOG2L>
+static hipError_t launch_colfft_t(bool conj_in, bool twiddle, bool conj_scale_out, const cd *in,
+                                  cd *out, int64_t C, int64_t ngroups, int64_t in_step,
+                                  int64_t in_stride, int64_t out_step, int64_t out_stride,
+                                  const cd *twl, const cd *twr, int log2r, double scale,
+                                  hipStream_t s) {
+  constexpr int CW = 256 / Geo<LOG2L>::T;
+  const dim3 grid((unsigned)((C + CW - 1) / CW), (unsigned)ngroups);
+#define GDSP_CF(A, B, D)                                                                      \
+  hipLaunchKernelGGL((colfft_tile_kernel<LOG2L, A, B, D>), grid, dim3(256), 0, s, in, out, C, \
+                     in_step, in_stride, out_step, out_stride, twl, twr, log2r, scale)
+  if (twiddle) {
+    if (conj_in) GDSP_CF(true, true, false);
+    else GDSP_CF(false, true, false);
+  } else if (conj_in) {
+    if (conj_scale_out) GDSP_CF(true, false, true);
+    else GDSP_CF(true, false, false);
+  } else {
+    if (conj_scale_out) GDSP_CF(false, false, true);
+    else GDSP_CF(false, false, false);
+  }
+#undef GDSP_CF
+  return hipGetLastError();
+}
+
+hipError_t launch_colfft(int log2l, bool conj_in, bool twiddle, bool conj_scale_out, const cd *in,
+                         cd *out, int64_t C, int64_t ngroups, int64_t in_step, int64_t in_stride,
+                         int64_t out_step, int64_t out_stride, const cd *twl, const cd *twr,
+                         int log2r, double scale, hipStream_t s) {
+  if (twiddle && conj_scale_out) return hipErrorInvalidValue;
+  switch (log2l) {
+#define GDSP_CFC(L)                                                                           \
+  case L:                                                                                     \
+    return launch_colfft_t<L>(conj_in, twiddle, conj_scale_out, in, out, C, ngroups, in_step, \
+                              in_stride, out_step, out_stride, twl, twr, log2r, scale, s);
+    GDSP_CFC(4) GDSP_CFC(5) GDSP_CFC(6) GDSP_CFC(7) GDSP_CFC(8) GDSP_CFC(9)
+#undef GDSP_CFC
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_transpose(const cd *in, cd *out, int64_t rows, int64_t cols, hipStream_t s) {

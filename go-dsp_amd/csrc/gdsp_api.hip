@@ -543,6 +543,29 @@ int gdsp_fft2_device(const void *d_in, void *d_out, int64_t rows, int64_t cols, 
     work = (cd *)w.p;
   }
   const bool inv = inverse != 0;
+  const int lr = ilog2(rows);
+  if (is_pow2(rows) && lr >= gdsp::kColMinLog2 && lr <= 2 * gdsp::kColMaxLog2) {
+    // row pass (contiguous rows, any length) -> work; column pass on
+    // row-segment tiles: one kernel for rows <= 512, otherwise the four-step
+    // split rows = R1*R2 (A in place on work, B from work into out)
+    STCHK(exec_plan(pc, d_in, work, rows, inv, gdsp::LOAD_COMPLEX, s));
+    const double sc = 1.0 / (double)rows;
+    if (lr <= gdsp::kColMaxLog2) {
+      HIPCHK(gdsp::launch_colfft(lr, inv, false, inv, work, (cd *)d_out, cols, 1, 0, 1, 0, 1,
+                                 pr->tw, nullptr, lr, sc, s));
+    } else {
+      const int l1 = lr / 2, l2 = lr - l1;  // R1 <= R2
+      gdsp_plan *p1 = nullptr, *p2 = nullptr;
+      STCHK(get_plan((int64_t)1 << l1, &p1));
+      STCHK(get_plan((int64_t)1 << l2, &p2));
+      const int64_t R1 = (int64_t)1 << l1, R2 = (int64_t)1 << l2;
+      HIPCHK(gdsp::launch_colfft(l1, inv, true, false, work, work, cols, R2, 1, R2, 1, R2, p1->tw,
+                                 pr->tw, lr, 1.0, s));
+      HIPCHK(gdsp::launch_colfft(l2, false, false, inv, work, (cd *)d_out, cols, R1, R2, 1, 1, R1,
+                                 p2->tw, nullptr, lr, sc, s));
+    }
+    return GDSP_OK;
+  }
   HIPCHK(gdsp::launch_transpose((const cd *)d_in, work, rows, cols, s));
   STCHK(exec_plan(pr, work, work, cols, inv, gdsp::LOAD_COMPLEX, s));
   HIPCHK(gdsp::launch_transpose(work, (cd *)d_out, cols, rows, s));

@@ -34,6 +34,12 @@ hipError_t launch_segments_to_complex(const double *x, int64_t nfft, int64_t fle
                                       hipStream_t s);
 hipError_t launch_power_accumulate(const cd *buf, int64_t nseg, int64_t flen, double *acc,
                                    hipStream_t s);
+// FFT2 column pass on row-segment tiles; 4 <= log2l <= 9 (see fft_kernels.hip)
+constexpr int kColMinLog2 = 4, kColMaxLog2 = 9;
+hipError_t launch_colfft(int log2l, bool conj_in, bool twiddle, bool conj_scale_out, const cd *in,
+                         cd *out, int64_t C, int64_t ngroups, int64_t in_step, int64_t in_stride,
+                         int64_t out_step, int64_t out_stride, const cd *twl, const cd *twr,
+                         int log2r, double scale, hipStream_t s);
 hipError_t launch_transpose(const cd *in, cd *out, int64_t rows, int64_t cols, hipStream_t s);
 hipError_t launch_real_to_complex(const double *in, cd *out, int64_t count, hipStream_t s);
 hipError_t launch_chirp_premul(const cd *in, cd *a, int64_t n, int64_t m, int64_t batch,

@@ -12,6 +12,7 @@
 """
 from __future__ import annotations
 
+import contextlib
 from dataclasses import dataclass
 from typing import Callable, Optional
 
@@ -83,17 +84,21 @@ def pwelch(x_local, Fs: float, o: spectral.PwelchOptions, shard: PwelchShard, gr
     assert (nfft, pad, noverlap) == (shard.nfft, shard.pad, shard.noverlap)
     flen = shard.flen
     dev = x_local.device
-    win_seg = torch.as_tensor(np.ascontiguousarray(wf(flen)), dtype=torch.float64, device=dev)
-    acc = torch.zeros(flen, dtype=torch.float64, device=dev)
-    if shard.seg_hi > shard.seg_lo:
-        (accumulate or gpu_accumulate)(x_local, shard, win_seg, acc, stream)
-    if dist.is_initialized() and dist.get_world_size(group) > 1:
-        if stream is not None:
-            with torch.cuda.stream(stream):
-                dist.all_reduce(acc, group=group)
-        else:
+    # every torch op below (window upload, zeroing, the host copy) is ordered
+    # on the same stream as the library's kernels
+    ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+    with ctx:
+        win_seg = torch.as_tensor(np.ascontiguousarray(wf(flen)), dtype=torch.float64,
+                                  device=dev)
+        acc = torch.zeros(flen, dtype=torch.float64, device=dev)
+        if shard.seg_hi > shard.seg_lo:
+            (accumulate or gpu_accumulate)(x_local, shard, win_seg, acc, stream)
+        if dist.is_initialized() and dist.get_world_size(group) > 1:
+            if acc.is_cuda and dist.get_backend(group) != "nccl":
+                acc = acc.cpu()  # gloo (rehearsal of the N>1 path): reduce a host copy
             dist.all_reduce(acc, group=group)
-    return spectral.finalize(acc.cpu().numpy(), shard.nsegs_total, nfft, pad,
+        host = acc.cpu().numpy()
+    return spectral.finalize(host, shard.nsegs_total, nfft, pad,
                              np.asarray(wf(nfft), np.float64), Fs, not scaling)
 
 

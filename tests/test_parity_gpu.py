@@ -153,7 +153,8 @@ def test_convolve(gdsp, oracle, n):
 
 
 @pytest.mark.parametrize("shape", [(1, 1), (1, 8), (8, 1), (2, 3), (3, 5), (16, 16), (64, 32),
-                                   (6, 10), (100, 7), (128, 256), (512, 300), (1024, 1024)])
+                                   (6, 10), (100, 7), (128, 256), (512, 300), (1024, 1024),
+                                   (16, 1000), (2048, 48), (4096, 33), (65536, 8), (32, 5)])
 def test_fft2_vs_oracle(gdsp, oracle, shape):
     rng = np.random.default_rng(shape[0] * 1000 + shape[1])
     x = rng.uniform(-1, 1, shape) + 1j * rng.uniform(-1, 1, shape)
