@@ -62,6 +62,38 @@ __device__ __forceinline__ cd rot16(cd x, int m) {
   return {x.x * c + x.y * s, x.y * c - x.x * s};
 }
 
+// cos/sin(pi/16) and cos/sin(3 pi/16)
+#define GDSP_C16 0.98078528040323044913
+#define GDSP_S16 0.19509032201612826785
+#define GDSP_C316 0.83146961230254523708
+#define GDSP_S316 0.55557023301960222474
+
+// x * exp(-2*pi*i*m/32) (m compile-time after unrolling); even m -> rot16.
+__device__ __forceinline__ cd rot32(cd x, int m) {
+  m &= 31;
+  if ((m & 1) == 0) return rot16(x, m >> 1);
+  double c, s;  // w = c - i s, c = cos(pi m/16), s = sin(pi m/16)
+  switch (m) {
+    case 1: c = GDSP_C16; s = GDSP_S16; break;
+    case 3: c = GDSP_C316; s = GDSP_S316; break;
+    case 5: c = GDSP_S316; s = GDSP_C316; break;
+    case 7: c = GDSP_S16; s = GDSP_C16; break;
+    case 9: c = -GDSP_S16; s = GDSP_C16; break;
+    case 11: c = -GDSP_S316; s = GDSP_C316; break;
+    case 13: c = -GDSP_C316; s = GDSP_S316; break;
+    case 15: c = -GDSP_C16; s = GDSP_S16; break;
+    case 17: c = -GDSP_C16; s = -GDSP_S16; break;
+    case 19: c = -GDSP_C316; s = -GDSP_S316; break;
+    case 21: c = -GDSP_S316; s = -GDSP_C316; break;
+    case 23: c = -GDSP_S16; s = -GDSP_C16; break;
+    case 25: c = GDSP_S16; s = -GDSP_C16; break;
+    case 27: c = GDSP_S316; s = -GDSP_C316; break;
+    case 29: c = GDSP_C316; s = -GDSP_S316; break;
+    default: c = GDSP_C16; s = -GDSP_S16; break;  // 31
+  }
+  return {x.x * c + x.y * s, x.y * c - x.x * s};
+}
+
 // In-register forward DFT of size R (natural order in, natural order out).
 template <int R>
 struct Dft;
@@ -105,7 +137,7 @@ __device__ __forceinline__ void dft_split(cd (&a)[R1 * R2]) {
     for (int n1 = 0; n1 < R1; ++n1) tmp[n1] = a[R2 * n1 + n2];
     Dft<R1>::run(tmp);
 #pragma unroll
-    for (int k1 = 0; k1 < R1; ++k1) y[n2][k1] = rot16(tmp[k1], n2 * k1 * (16 / R));
+    for (int k1 = 0; k1 < R1; ++k1) y[n2][k1] = rot32(tmp[k1], n2 * k1 * (32 / R));
   }
 #pragma unroll
   for (int k1 = 0; k1 < R1; ++k1) {
@@ -125,6 +157,10 @@ struct Dft<8> {
 template <>
 struct Dft<16> {
   __device__ __forceinline__ static void run(cd (&a)[16]) { dft_split<4, 4>(a); }
+};
+template <>
+struct Dft<32> {
+  __device__ __forceinline__ static void run(cd (&a)[32]) { dft_split<8, 4>(a); }
 };
 
 // ---------------------------------------------------------------------------

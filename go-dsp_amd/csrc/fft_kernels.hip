@@ -215,6 +215,95 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_kernel(
   }
 }
 
+// Half-overlap specialisation (Noverlap = NFFT/2, Pad = NFFT: the BASELINE
+// configuration and Welch's usual choice). With stride = F/2 and thread t
+// owning samples t + k*T of a segment, segment s0+1's element k is segment
+// s0's element k + E/2, and the next pair's first segment starts where
+// s0+1's second half does. So per pair a thread loads only E new samples and
+// carries E/2 across iterations: every sample is read from HBM/L2 once, and
+// the window stays in registers.
+// WMODE: where the window lives — 0 registers, 1 re-read from global (L1/L2)
+// every iteration, 2 an LDS table shared by the workgroup.
+template <int LOG2F, int WMODE = 2, int MINW = 1>
+__global__ __launch_bounds__(Geo<LOG2F>::WG, MINW) void pwelch_half_kernel(
+    const double *__restrict__ x, int64_t seg_begin, int64_t seg_end, int64_t pairs_per_worker,
+    const double *__restrict__ win, const cd *__restrict__ tw, double *__restrict__ partial) {
+  using G = Geo<LOG2F>;
+  constexpr int E = G::E, H = E / 2;
+  constexpr int64_t STRIDE = G::N / 2;
+  __shared__ double lds[G::LDS_DOUBLES + (WMODE == 2 ? G::N : 0)];
+  const int lt = threadIdx.x;
+  const int slot = lt / G::T;
+  const int t = lt & (G::T - 1);
+  const int64_t worker = (int64_t)blockIdx.x * G::TPW + slot;
+  double *lre = lds + slot * G::STRIDE;
+  const int64_t npairs = (seg_end - seg_begin + 1) / 2;
+  double wv[E];
+  double *wl = lds + G::LDS_DOUBLES;
+  if constexpr (WMODE == 0) {
+#pragma unroll
+    for (int k = 0; k < E; ++k) wv[k] = win[t + k * G::T];
+  } else if constexpr (WMODE == 2) {
+    for (int i = lt; i < G::N; i += G::WG) wl[i] = win[i];
+    __syncthreads();
+  }
+  double acc[E];
+#pragma unroll
+  for (int k = 0; k < E; ++k) acc[k] = 0.0;
+  const int64_t p0 = worker * pairs_per_worker;
+  // carried samples: the first half of the next pair's first segment
+  double carry[H];
+  {
+    const int64_t s0 = seg_begin + 2 * (p0 < npairs ? p0 : 0);
+    const double *b = x + s0 * STRIDE + t;
+#pragma unroll
+    for (int k = 0; k < H; ++k) carry[k] = (p0 < npairs) ? b[k * G::T] : 0.0;
+  }
+  for (int64_t it = 0; it < pairs_per_worker; ++it) {
+    const int64_t p = p0 + it;
+    const bool active = p < npairs;
+    const int64_t s0 = seg_begin + 2 * p;
+    const bool has1 = active && (s0 + 1 < seg_end);
+    // samples of this pair: a[0..H) = carry, a[H..E) (shared with seg s0+1),
+    // c[0..H) = second half of seg s0+1 (= first half of the next pair)
+    const double *b = opaque_ptr(x) + s0 * STRIDE + t;
+    double a2[H], c2[H];
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      a2[k] = active ? b[(H + k) * G::T] : 0.0;
+      c2[k] = has1 ? b[(E + k) * G::T] : 0.0;
+    }
+    if constexpr (WMODE == 1) {
+      const double *w = opaque_ptr(win) + t;
+#pragma unroll
+      for (int k = 0; k < E; ++k) wv[k] = w[k * G::T];
+    } else if constexpr (WMODE == 2) {
+      const int tw2 = opaque_int(t);
+#pragma unroll
+      for (int k = 0; k < E; ++k) wv[k] = wl[tw2 + k * G::T];
+    }
+    cd v[E];
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      // an unpaired last segment (odd count) has a zero partner
+      v[k] = {carry[k] * wv[k], has1 ? a2[k] * wv[k] : 0.0};
+      v[H + k] = {a2[k] * wv[H + k], c2[k] * wv[H + k]};
+    }
+#pragma unroll
+    for (int k = 0; k < H; ++k) carry[k] = c2[k];
+    fft_regs<LOG2F, true, true>(v, opaque_int(t), tw, lre, lre, it == 0);
+    if (active) {
+#pragma unroll
+      for (int k = 0; k < E; ++k) acc[k] += v[k].x * v[k].x + v[k].y * v[k].y;
+    }
+  }
+  if (p0 < npairs) {
+    double *dst = partial + worker * G::N;
+#pragma unroll
+    for (int k = 0; k < E; ++k) dst[t + k * G::T] = acc[k];
+  }
+}
+
 // Deterministic two-level reduction of the per-worker partial spectra:
 // level 1 sums fixed chunks of workers per bin (grid: bins x chunks), level 2
 // sums the chunk results in chunk order and adds into acc.
@@ -541,6 +630,33 @@ static hipError_t launch_pw_t(const double *x, int64_t nfft, int64_t stride, int
   hipLaunchKernelGGL((pwelch_kernel<LOG2F, true>), dim3((unsigned)nblk), dim3(G::WG), 0, s, x,
                      nfft, stride, seg_begin, seg_end, ppw, win, tw, partial);
   return hipGetLastError();
+}
+
+template <int LOG2F, int WMODE = 2, int MINW = 1>
+static hipError_t launch_pwh_t(const double *x, int64_t seg_begin, int64_t seg_end, int64_t ppw,
+                               int64_t nworkers, const double *win, const cd *tw, double *partial,
+                               hipStream_t s) {
+  using G = Geo<LOG2F>;
+  const int64_t nblk = (nworkers + G::TPW - 1) / G::TPW;
+  hipLaunchKernelGGL((pwelch_half_kernel<LOG2F, WMODE, MINW>), dim3((unsigned)nblk), dim3(G::WG), 0, s,
+                     x, seg_begin, seg_end, ppw, win, tw, partial);
+  return hipGetLastError();
+}
+
+hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int64_t seg_end,
+                              int64_t ppw, int64_t nworkers, const double *win, const cd *tw,
+                              double *partial, hipStream_t s) {
+  switch (log2f) {
+#define GDSP_PWH(L) \
+  case L: return launch_pwh_t<L>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
+    GDSP_PWH(5) GDSP_PWH(6) GDSP_PWH(7) GDSP_PWH(8) GDSP_PWH(9) GDSP_PWH(10) GDSP_PWH(11)
+    GDSP_PWH(12) GDSP_PWH(13)
+#undef GDSP_PWH
+    // F = 16384: the exchange buffer alone takes 136 KiB, so the window is
+    // re-read from L1/L2 instead of living in LDS
+    case 14: return launch_pwh_t<14, 1>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 int pwelch_workers_per_block(int log2f) {

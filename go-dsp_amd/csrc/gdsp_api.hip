@@ -88,27 +88,57 @@ bool lds_split_default() {
   return v != 0;
 }
 
-// RAII for stream-ordered device scratch.
+// Scratch device memory: a grow-only buffer per (device, stream, use-site
+// slot), allocated with hipMalloc. Reuse is ordered by the stream itself: a
+// slot is only ever used by work queued on its stream, so a later call can
+// overwrite it only after the earlier kernels on that stream ran. Growing a
+// slot synchronises its stream before freeing the old buffer.
+// (Stream-ordered hipMallocAsync/hipFreeAsync lost kernel output
+// intermittently under the ROCm 7.2 runtime here — tests/cpp reproduced it —
+// so the library does not use it.) Device-API callers must not drive one
+// stream from two host threads at once.
+enum Slot {
+  SLOT_IN = 0, SLOT_OUT, SLOT_AUX, SLOT_AUX2, SLOT_GLOBAL, SLOT_GLOBAL_IN, SLOT_REAL,
+  SLOT_BLU, SLOT_FFT2, SLOT_PW_PART, SLOT_PW_RED, SLOT_PW_BUF, SLOT_COUNT
+};
+
+struct Workspace {
+  void *buf[SLOT_COUNT] = {};
+  size_t cap[SLOT_COUNT] = {};
+};
+
+std::mutex g_ws_mu;
+std::map<std::pair<int, hipStream_t>, Workspace> g_ws;
+
 struct DevBuf {
   void *p = nullptr;
-  hipStream_t s = nullptr;
   DevBuf() = default;
   DevBuf(const DevBuf &) = delete;
-  ~DevBuf() {
-    if (p) (void)hipFreeAsync(p, s);
-  }
-  int alloc(size_t bytes, hipStream_t st) {
-    s = st;
+  int alloc(size_t bytes, hipStream_t st, Slot slot) {
     if (bytes == 0) bytes = 16;
-    hipError_t e = hipMallocAsync(&p, bytes, st);
-    if (e != hipSuccess) {
-      p = nullptr;
-      return fail(GDSP_ERR_NOMEM, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return fail(GDSP_ERR_NO_DEVICE, "hipGetDevice failed");
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    Workspace &w = g_ws[std::make_pair(dev, st)];
+    if (w.cap[slot] < bytes) {
+      if (w.buf[slot]) {
+        HIPCHK(hipStreamSynchronize(st));  // queued users of the old buffer
+        HIPCHK(hipFree(w.buf[slot]));
+        w.buf[slot] = nullptr;
+        w.cap[slot] = 0;
+      }
+      const size_t want = bytes + bytes / 4;  // headroom against regrowth
+      hipError_t e = hipMalloc(&w.buf[slot], want);
+      if (e != hipSuccess) {
+        w.buf[slot] = nullptr;
+        return fail(GDSP_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+      }
+      w.cap[slot] = want;
     }
+    p = w.buf[slot];
     return GDSP_OK;
   }
 };
-
 
 // Host <-> device copies through library-owned pinned staging buffers (two
 // halves, double-buffered). The caller's memory is only touched by memcpy on
@@ -317,10 +347,10 @@ int exec_global(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool
   const int np = (int)radix.size();
   const size_t bytes = (size_t)batch * (size_t)p->n * sizeof(cd);
   DevBuf scratch, inbuf;
-  STCHK(scratch.alloc(bytes, s));
+  STCHK(scratch.alloc(bytes, s, SLOT_GLOBAL));
   const void *src = in;
   if (in == (const void *)out && ((np - 1) % 2 == 0)) {
-    STCHK(inbuf.alloc(bytes, s));
+    STCHK(inbuf.alloc(bytes, s, SLOT_GLOBAL_IN));
     HIPCHK(hipMemcpyAsync(inbuf.p, in, bytes, hipMemcpyDeviceToDevice, s));
     src = inbuf.p;
   }
@@ -339,7 +369,7 @@ int exec_global(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool
 int exec_bluestein_composed(const gdsp_plan *p, const cd *in, cd *out, int64_t batch, bool inv,
                             hipStream_t s) {
   DevBuf a;
-  STCHK(a.alloc((size_t)batch * (size_t)p->m * sizeof(cd), s));
+  STCHK(a.alloc((size_t)batch * (size_t)p->m * sizeof(cd), s, SLOT_BLU));
   cd *da = (cd *)a.p;
   HIPCHK(gdsp::launch_chirp_premul(in, da, p->n, p->m, batch, p->chirp, inv, s));
   STCHK(exec_plan(p->mplan, da, da, batch, false, gdsp::LOAD_COMPLEX, s));
@@ -377,7 +407,7 @@ int exec_plan(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool i
       const cd *src = (const cd *)in;
       DevBuf tmp;
       if (load == gdsp::LOAD_REAL) {
-        STCHK(tmp.alloc((size_t)batch * (size_t)p->n * sizeof(cd), s));
+        STCHK(tmp.alloc((size_t)batch * (size_t)p->n * sizeof(cd), s, SLOT_REAL));
         HIPCHK(gdsp::launch_real_to_complex((const double *)in, (cd *)tmp.p, batch * p->n, s));
         src = (const cd *)tmp.p;
       }
@@ -409,8 +439,8 @@ int host_batch(const void *x, size_t in_elem_bytes, double *out, int64_t n, int6
   const size_t in_bytes = (size_t)batch * (size_t)n * in_elem_bytes;
   const size_t out_bytes = (size_t)batch * (size_t)n * sizeof(cd);
   DevBuf din, dout;
-  STCHK(din.alloc(in_bytes, s));
-  STCHK(dout.alloc(out_bytes, s));
+  STCHK(din.alloc(in_bytes, s, SLOT_IN));
+  STCHK(dout.alloc(out_bytes, s, SLOT_OUT));
   STCHK(copy_h2d(din.p, x, in_bytes, s));
   STCHK(exec_plan(p, din.p, (cd *)dout.p, batch, inv, load, s));
   STCHK(copy_d2h(out, dout.p, out_bytes, s));
@@ -513,7 +543,7 @@ int gdsp_convolve(const double *x, const double *y, double *out, int64_t n) {
   hipStream_t s = thread_stream(p->device);
   const size_t bytes = (size_t)n * sizeof(cd);
   DevBuf d;
-  STCHK(d.alloc(3 * bytes, s));
+  STCHK(d.alloc(3 * bytes, s, SLOT_IN));
   cd *dx = (cd *)d.p, *dy = dx + n, *dz = dy + n;
   STCHK(copy_h2d(dx, x, bytes, s));
   STCHK(copy_h2d(dy, y, bytes, s));
@@ -539,7 +569,7 @@ int gdsp_fft2_device(const void *d_in, void *d_out, int64_t rows, int64_t cols, 
   DevBuf w;
   cd *work = (cd *)d_work;
   if (!work) {
-    STCHK(w.alloc((size_t)rows * (size_t)cols * sizeof(cd), s));
+    STCHK(w.alloc((size_t)rows * (size_t)cols * sizeof(cd), s, SLOT_FFT2));
     work = (cd *)w.p;
   }
   const bool inv = inverse != 0;
@@ -583,11 +613,11 @@ static int fft2_host(const double *x, bool real_in, double *out, int64_t rows, i
   hipStream_t s = thread_stream(dev);
   const size_t cnt = (size_t)rows * (size_t)cols;
   DevBuf din, dout;
-  STCHK(din.alloc(cnt * sizeof(cd), s));
-  STCHK(dout.alloc(cnt * sizeof(cd), s));
+  STCHK(din.alloc(cnt * sizeof(cd), s, SLOT_IN));
+  STCHK(dout.alloc(cnt * sizeof(cd), s, SLOT_OUT));
   if (real_in) {
     DevBuf dr;
-    STCHK(dr.alloc(cnt * sizeof(double), s));
+    STCHK(dr.alloc(cnt * sizeof(double), s, SLOT_AUX));
     STCHK(copy_h2d(dr.p, x, cnt * sizeof(double), s));
     HIPCHK(gdsp::launch_real_to_complex((const double *)dr.p, (cd *)din.p, (int64_t)cnt, s));
   } else {
@@ -666,10 +696,17 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
     const int64_t ppw = (npairs + target - 1) / target;
     const int64_t nworkers = (npairs + ppw - 1) / ppw;
     DevBuf part, red;
-    STCHK(part.alloc((size_t)nworkers * (size_t)flen * sizeof(double), s));
-    STCHK(red.alloc((size_t)gdsp::reduce_scratch_doubles(nworkers, flen) * sizeof(double), s));
-    HIPCHK(gdsp::launch_pwelch(p->log2n, d_x, nfft, stride, seg_begin, seg_end, ppw, nworkers,
-                               d_win_seg, p->tw, (double *)part.p, s));
+    STCHK(part.alloc((size_t)nworkers * (size_t)flen * sizeof(double), s, SLOT_PW_PART));
+    STCHK(red.alloc((size_t)gdsp::reduce_scratch_doubles(nworkers, flen) * sizeof(double), s,
+                    SLOT_PW_RED));
+    if (2 * noverlap == nfft && flen == nfft && p->log2n >= 5) {
+      // half overlap: each sample loaded once, window in LDS
+      HIPCHK(gdsp::launch_pwelch_half(p->log2n, d_x, seg_begin, seg_end, ppw, nworkers, d_win_seg,
+                                      p->tw, (double *)part.p, s));
+    } else {
+      HIPCHK(gdsp::launch_pwelch(p->log2n, d_x, nfft, stride, seg_begin, seg_end, ppw, nworkers,
+                                 d_win_seg, p->tw, (double *)part.p, s));
+    }
     HIPCHK(gdsp::launch_reduce_partials((const double *)part.p, nworkers, flen, d_acc,
                                         (double *)red.p, s));
     return GDSP_OK;
@@ -679,7 +716,7 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
   if (chunk < 1) chunk = 1;
   if (chunk > nseg) chunk = nseg;
   DevBuf buf;
-  STCHK(buf.alloc((size_t)chunk * (size_t)flen * sizeof(cd), s));
+  STCHK(buf.alloc((size_t)chunk * (size_t)flen * sizeof(cd), s, SLOT_PW_BUF));
   for (int64_t s0 = seg_begin; s0 < seg_end; s0 += chunk) {
     const int64_t ns = (seg_end - s0) < chunk ? (seg_end - s0) : chunk;
     HIPCHK(gdsp::launch_segments_to_complex(d_x, nfft, flen, stride, s0, ns, d_win_seg,
@@ -752,9 +789,9 @@ int gdsp_pwelch(const double *x, int64_t n, double fs, int64_t nfft, int64_t pad
     STCHK(current_device(&dev));
     hipStream_t s = thread_stream(dev);
     DevBuf dx, dw, dacc;
-    STCHK(dx.alloc((size_t)lx * sizeof(double), s));
-    STCHK(dw.alloc((size_t)flen * sizeof(double), s));
-    STCHK(dacc.alloc((size_t)flen * sizeof(double), s));
+    STCHK(dx.alloc((size_t)lx * sizeof(double), s, SLOT_IN));
+    STCHK(dw.alloc((size_t)flen * sizeof(double), s, SLOT_AUX));
+    STCHK(dacc.alloc((size_t)flen * sizeof(double), s, SLOT_AUX2));
     if (lx > n) HIPCHK(hipMemsetAsync(dx.p, 0, (size_t)lx * sizeof(double), s));
     STCHK(copy_h2d(dx.p, x, (size_t)n * sizeof(double), s));
     STCHK(copy_h2d(dw.p, win_seg, (size_t)flen * sizeof(double), s));

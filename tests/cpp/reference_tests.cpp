@@ -55,7 +55,10 @@ int main(int argc, char **argv) {
       in >> n;
       auto x = readd(in, n);
       auto out = readc(in, n);
-      EXPECT(dsputils::PrettyCloseC(fft::FFTReal(x), out), "FFTReal n=" << n);
+      auto got = fft::FFTReal(x);
+      std::ostringstream vals;
+      for (auto &z : got) vals << z << " ";
+      EXPECT(dsputils::PrettyCloseC(got, out), "FFTReal n=" << n << " got " << vals.str());
       EXPECT(dsputils::PrettyCloseC(fft::IFFT(out), dsputils::ToComplex(x)), "IFFT n=" << n);
     } else if (kind == "FFT2") {  // TestFFT2, fft_test.go:211-223
       size_t r, c;

@@ -52,3 +52,29 @@ def test_cpp_mirror_reference_tables(refvec, tmp_path):
     r = subprocess.run([BIN, str(vec)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "failures 0" in r.stdout
+
+
+@pytest.mark.gpu
+def test_python_api_on_rocm_runtime():
+    """The host-pointer path under /opt/rocm's HIP runtime (torch not loaded
+    first): repeated small calls, where stream-ordered allocation once lost
+    kernel output (see gdsp_api.hip, Workspace)."""
+    code = r'''
+import importlib, os, sys
+sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
+import numpy as np, oracle
+g = importlib.import_module("go-dsp_amd")
+assert "torch" not in sys.modules
+rng = np.random.default_rng(1)
+for rep in range(20):
+    for n in (2, 3, 8, 100, 1024, 3000, 4096):
+        x = rng.standard_normal((3, n)) + 1j * rng.standard_normal((3, n))
+        y = g.fft.FFTBatch(x)
+        ref = oracle.fft_rows(x)
+        err = max(np.linalg.norm(a - b) / np.linalg.norm(b) for a, b in zip(y, ref))
+        assert err < 1e-9, (rep, n, err)
+print("ok")
+'''
+    env = dict(os.environ, GDSP_NO_TORCH_PRELOAD="1", REPO=REPO)
+    r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr

@@ -197,6 +197,13 @@ WINDOWS = {"hann": "Hann", "hamming": "Hamming", "rectangular": "Rectangular",
     (4000, 8, 4, 0, "flattop"),        # tiny segments
     (1 << 16, 16384, 8192, 0, "hann"),
     (4096, 4096, 0, 0, "rectangular"),  # exactly one segment
+    # half overlap (the carried-sample kernel): even/odd segment counts, Pad < NFFT
+    (40960, 4096, 2048, 0, "hann"),
+    (38913, 4096, 2048, 0, "hann"),
+    (20000, 64, 32, 0, "blackman"),
+    (20000, 32, 16, 16, "hann"),
+    (100000, 8192, 4096, 2048, "hamming"),
+    (8191, 8192, 4096, 0, "hann"),     # shorter than NFFT: one zero-padded segment
 ])
 def test_pwelch_vs_oracle(gdsp, oracle, n, nfft, nov, pad, win):
     rng = np.random.default_rng(n + nfft)

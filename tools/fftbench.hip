@@ -18,6 +18,7 @@
 #include "fft_kernels.hip"
 
 using namespace gdsp;
+cd *g_chirp, *g_bhat, *g_tw8192;
 
 #define CHECK(x)                                                                  \
   do {                                                                            \
@@ -122,6 +123,25 @@ __global__ __launch_bounds__(512, MINW) void blu_v(const cd *__restrict__ in, cd
     const int idx = t2 + k * 512;
     if (idx < n) dst[idx] = cmul(conjg(v[k]), chirp[idx]);
   }
+}
+
+// compute-only FFT-8192 (512 threads) and Bluestein-shaped double FFT
+template <int NFFT, int LOG2E = 4>
+__global__ __launch_bounds__((Geo<13, LOG2E>::WG)) void fft8192_compute(const cd *__restrict__ in,
+                                                       cd *__restrict__ out, int64_t batch,
+                                                       const cd *__restrict__ tw) {
+  using G = Geo<13, LOG2E>;
+  __shared__ double lds[G::LDS_DOUBLES];
+  const int t = threadIdx.x;
+  cd v[G::E];
+#pragma unroll
+  for (int k = 0; k < G::E; ++k) v[k] = {(double)(t + k + blockIdx.x), (double)(t - k)};
+  fft_regs<13, true, true, LOG2E>(v, t, tw, lds, lds);
+  if constexpr (NFFT == 2) fft_regs<13, true, true, LOG2E>(v, t, tw, lds, lds, false);
+  double s = 0;
+#pragma unroll
+  for (int k = 0; k < G::E; ++k) s += v[k].x + v[k].y;
+  if (s == 1.2345e300) out[t] = {s, s};
 }
 
 // Same memory pattern, no arithmetic: the ceiling of this access shape.
@@ -264,7 +284,6 @@ void l_write(const cd *in, cd *out, int64_t b, const cd *, hipStream_t s) {
 
 // production Pwelch / Bluestein kernels at different elements-per-thread
 double *g_x1g, *g_win, *g_part;
-cd *g_chirp, *g_bhat, *g_tw8192;
 template <int LOG2E>
 void l_pwelch(const cd *in, cd *out, int64_t b, const cd *tw, hipStream_t s) {
   // 2^29 samples (the 4 GiB input buffer viewed as float64), NFFT 4096, 50 %
@@ -277,6 +296,15 @@ void l_pwelch(const cd *in, cd *out, int64_t b, const cd *tw, hipStream_t s) {
   hipLaunchKernelGGL((pwelch_kernel<12, true, LOG2E>), dim3((unsigned)((nw + G::TPW - 1) / G::TPW)),
                      dim3(G::WG), 0, s, (const double *)in, nfft, stride, (int64_t)0, nseg, ppw,
                      (const double *)g_win, tw, g_part);
+}
+template <int WM, int MINW = 1>
+void l_pwelch_half(const cd *in, cd *out, int64_t b, const cd *tw, hipStream_t s) {
+  const int64_t nsamp = (int64_t)1 << 29, nfft = 4096, stride = 2048;
+  const int64_t nseg = (nsamp - nfft) / stride + 1, npairs = (nseg + 1) / 2;
+  const int64_t nworkers = 2048;
+  const int64_t ppw = (npairs + nworkers - 1) / nworkers;
+  const int64_t nw = (npairs + ppw - 1) / ppw;
+  launch_pwh_t<12, WM, MINW>((const double *)in, 0, nseg, ppw, nw, (const double *)g_win, tw, g_part, s);
 }
 template <int LOG2E>
 void l_blu_prod(const cd *in, cd *out, int64_t b, const cd *, hipStream_t s) {
@@ -295,6 +323,11 @@ template <bool SPLIT, bool NTL, bool NTS, int MINW, bool XCD = false>
 void launch_v(const cd *in, cd *out, int64_t batch, const cd *tw, hipStream_t s) {
   hipLaunchKernelGGL((fft4096_v<SPLIT, NTL, NTS, MINW, XCD>), dim3((unsigned)batch), dim3(256), 0, s,
                      in, out, batch, tw);
+}
+template <int NF, int LOG2E = 4>
+void launch_comp8192(const cd *in, cd *out, int64_t batch, const cd *tw, hipStream_t s) {
+  hipLaunchKernelGGL((fft8192_compute<NF, LOG2E>), dim3((unsigned)batch),
+                     dim3(Geo<13, LOG2E>::WG), 0, s, in, out, batch, g_tw8192);
 }
 template <int MINW>
 void launch_comp(const cd *in, cd *out, int64_t batch, const cd *tw, hipStream_t s) {
@@ -373,8 +406,18 @@ int main(int argc, char **argv) {
       {"twobuf_w3", launch_v<false, false, false, 3>, true},
       {"compute_only", launch_comp<1>, false},
       {"compute_only_w4", launch_comp<4>, false},
+      {"comp8192_x1", launch_comp8192<1>, false},
+      {"comp8192_x2", launch_comp8192<2>, false},
+      {"comp8192_x1_e32", launch_comp8192<1, 5>, false},
+      {"comp8192_x2_e32", launch_comp8192<2, 5>, false},
+      {"blu_prod_e32", l_blu_prod<5>, false},
       {"pwelch_e16", l_pwelch<4>, false},
       {"pwelch_e8", l_pwelch<3>, false},
+      {"pwelch_half_wreg", l_pwelch_half<0>, false},
+      {"pwelch_half_wglb", l_pwelch_half<1>, false},
+      {"pwelch_half_wlds", l_pwelch_half<2>, false},
+      {"pwelch_half_wlds_w3", l_pwelch_half<2, 3>, false},
+      {"pwelch_half_wlds_w4", l_pwelch_half<2, 4>, false},
       {"blu_prod_e16", l_blu_prod<4>, false},
       {"blu_prod_e8", l_blu_prod<3>, false},
       {"blu3000", launch_blu<1>, false},
