@@ -3,10 +3,25 @@ tables are generated on the host, once per call (the reference recomputes them
 per segment, window.go:25-29); the GPU Pwelch kernel applies them."""
 from __future__ import annotations
 
+import ctypes
+import functools
 import math
 from typing import Callable
 
 import numpy as np
+
+from . import _lib
+
+
+def _cached(fn):
+    """Window tables depend only on L: compute once (the reference recomputes
+    them for every segment, window.go:25-29) and hand out copies."""
+    table = functools.lru_cache(maxsize=64)(lambda L: fn(L))
+
+    @functools.wraps(fn)
+    def wrapper(L: int) -> np.ndarray:
+        return table(int(L)).copy()
+    return wrapper
 
 
 def Apply(x: np.ndarray, windowFunction: Callable[[int], np.ndarray]) -> None:
@@ -16,6 +31,7 @@ def Apply(x: np.ndarray, windowFunction: Callable[[int], np.ndarray]) -> None:
         x[i] *= w[i]
 
 
+@_cached
 def Rectangular(L: int) -> np.ndarray:
     """window.go:32-40."""
     return np.ones(L, np.float64)
@@ -32,16 +48,21 @@ def _sym(L: int, f) -> np.ndarray:
     return r
 
 
+@_cached
 def Hamming(L: int) -> np.ndarray:
     """window.go:44-58."""
     return _sym(L, lambda n, N: 0.54 - 0.46 * math.cos(math.pi * 2 / float(N) * float(n)))
 
 
+@_cached
 def Hann(L: int) -> np.ndarray:
-    """window.go:62-76."""
-    return _sym(L, lambda n, N: 0.5 * (1 - math.cos(2 * math.pi / float(N) * float(n))))
+    """window.go:62-76 (the C ABI's host generator, gdsp_window_hann)."""
+    out = np.empty(max(L, 0), np.float64)
+    _lib.check(_lib.lib().gdsp_window_hann(L, out.ctypes.data_as(ctypes.c_void_p)), "Hann")
+    return out
 
 
+@_cached
 def Bartlett(L: int) -> np.ndarray:
     """window.go:80-98."""
     r = np.zeros(L, np.float64)
@@ -60,6 +81,7 @@ def Bartlett(L: int) -> np.ndarray:
     return r
 
 
+@_cached
 def FlatTop(L: int) -> np.ndarray:
     """window.go:102-135."""
     a0, a1, a2, a3, a4 = 0.21557895, 0.41663158, 0.277263158, 0.083578947, 0.006947368
@@ -71,6 +93,7 @@ def FlatTop(L: int) -> np.ndarray:
     return _sym(L, f)
 
 
+@_cached
 def Blackman(L: int) -> np.ndarray:
     """window.go:138-152."""
     return _sym(L, lambda n, N: 0.42 + (-0.5 * math.cos(2 * math.pi * float(n) / float(N)))

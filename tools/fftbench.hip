@@ -210,6 +210,33 @@ __global__ __launch_bounds__(256) void copy_xcd(const cd *__restrict__ in, cd *_
 #pragma unroll
   for (int k = 0; k < 16; ++k) out[base + k * 256] = v[k];
 }
+// XCD map + each wave owning a contiguous 16 KiB quarter of the row
+__global__ __launch_bounds__(256) void copy_xcd_wc(const cd *__restrict__ in, cd *__restrict__ out,
+                                                   int64_t cnt) {
+  const int64_t row = xcd_remap(blockIdx.x, gridDim.x);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int64_t base = row * 4096 + w * 1024 + l;
+  cd v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = in[base + k * 64];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) out[base + k * 64] = v[k];
+}
+// XCD map, loads in two halves (8 in flight, then 8)
+__global__ __launch_bounds__(256) void copy_xcd_half(const cd *__restrict__ in,
+                                                     cd *__restrict__ out, int64_t cnt) {
+  const int64_t row = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t base = row * 4096 + threadIdx.x;
+  cd v[16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = in[base + k * 256];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) out[base + k * 256] = v[k];
+#pragma unroll
+  for (int k = 8; k < 16; ++k) v[k] = in[base + k * 256];
+#pragma unroll
+  for (int k = 8; k < 16; ++k) out[base + k * 256] = v[k];
+}
 // two rows per 512-thread workgroup, 16 loads per thread
 __global__ __launch_bounds__(512) void copy_two(const cd *__restrict__ in, cd *__restrict__ out,
                                                 int64_t cnt) {
@@ -235,6 +262,12 @@ void l_cwc(const cd *in, cd *out, int64_t b, const cd *, hipStream_t s) {
 }
 void l_cxcd(const cd *in, cd *out, int64_t b, const cd *, hipStream_t s) {
   hipLaunchKernelGGL(copy_xcd, dim3((unsigned)b), dim3(256), 0, s, in, out, b * 4096);
+}
+void l_cxwc(const cd *in, cd *out, int64_t b, const cd *, hipStream_t s) {
+  hipLaunchKernelGGL(copy_xcd_wc, dim3((unsigned)b), dim3(256), 0, s, in, out, b * 4096);
+}
+void l_cxh(const cd *in, cd *out, int64_t b, const cd *, hipStream_t s) {
+  hipLaunchKernelGGL(copy_xcd_half, dim3((unsigned)b), dim3(256), 0, s, in, out, b * 4096);
 }
 void l_ctwo(const cd *in, cd *out, int64_t b, const cd *, hipStream_t s) {
   hipLaunchKernelGGL(copy_two, dim3((unsigned)(b / 2)), dim3(512), 0, s, in, out, b * 4096);
@@ -430,6 +463,8 @@ int main(int argc, char **argv) {
       {"copy_one", l_copy_one, false},
       {"copy_wave_contig", l_cwc, false},
       {"copy_xcd", l_cxcd, false},
+      {"copy_xcd_wc", l_cxwc, false},
+      {"copy_xcd_half", l_cxh, false},
       {"copy_two", l_ctwo, false},
       {"copy_revst", l_crev, false},
       {"copy_u2", l_copy_unroll<2>, false},
