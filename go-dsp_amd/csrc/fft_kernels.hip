@@ -366,13 +366,17 @@ __global__ void power_accumulate_kernel(const cd *__restrict__ buf, int64_t nseg
 // R = R1*R2 used for long columns:
 //   A: q = n2 < R2, rows n2 + R2*j, DFT_R1, times W_R^(n2*k1), in place;
 //   B: q = k1 < R1, rows R2*k1 + j, DFT_R2, out rows k1 + R1*k2.
-template <int LOG2L, bool CONJ_IN, bool TWIDDLE, bool CONJ_SCALE_OUT>
+// TWIDDLE: 0 none; 1 times W_R^(q*j) (FFT2 four-step, q = row group);
+// 2 times W_R^(col*j) (1-D four-step: the column is the n2 index).
+template <int LOG2L, bool CONJ_IN, int TWIDDLE, bool CONJ_SCALE_OUT>
 __global__ __launch_bounds__(256) void colfft_tile_kernel(
     const cd *__restrict__ in, cd *__restrict__ out, int64_t C, int64_t in_step,
     int64_t in_stride, int64_t out_step, int64_t out_stride, const cd *__restrict__ twl,
-    const cd *__restrict__ twr, int log2r, double scale) {
+    const cd *__restrict__ twr, int log2r, double scale, int64_t mat_stride) {
   using G = Geo<LOG2L>;
   static_assert(G::T <= 256, "tile column length too large");
+  in += (int64_t)blockIdx.z * mat_stride;
+  out += (int64_t)blockIdx.z * mat_stride;
   constexpr int CW = 256 / G::T;
   __shared__ double lds[G::NPASS > 1 ? CW * G::N : 1];
   const int lt = threadIdx.x;
@@ -395,7 +399,8 @@ __global__ __launch_bounds__(256) void colfft_tile_kernel(
     for (int k = 0; k < G::E; ++k) {
       const int64_t j = t + k * G::T;
       cd o = v[k];
-      if constexpr (TWIDDLE) o = cmul(o, twr[(q * j) & (((int64_t)1 << log2r) - 1)]);
+      if constexpr (TWIDDLE == 1) o = cmul(o, twr[(q * j) & (((int64_t)1 << log2r) - 1)]);
+      if constexpr (TWIDDLE == 2) o = cmul(o, twr[(col * j) & (((int64_t)1 << log2r) - 1)]);
       if constexpr (CONJ_SCALE_OUT) o = {o.x * scale, -o.y * scale};
       dst[j * out_stride * C] = o;
     }
@@ -405,8 +410,11 @@ __global__ __launch_bounds__(256) void colfft_tile_kernel(
 // out[c*rows + r] = in[r*cols + c] through a 32x33 LDS tile (complex128).
 __global__ __launch_bounds__(256) void transpose_kernel(const cd *__restrict__ in,
                                                         cd *__restrict__ out, int64_t rows,
-                                                        int64_t cols) {
+                                                        int64_t cols, int conj_scale,
+                                                        double scale) {
   __shared__ cd tile[32][33];
+  in += (int64_t)blockIdx.y * rows * cols;
+  out += (int64_t)blockIdx.y * rows * cols;
   const int64_t tiles_c = (cols + 31) / 32;
   const int64_t tiles_r = (rows + 31) / 32;
   for (int64_t tb = blockIdx.x; tb < tiles_c * tiles_r; tb += gridDim.x) {
@@ -421,7 +429,11 @@ __global__ __launch_bounds__(256) void transpose_kernel(const cd *__restrict__ i
 #pragma unroll
     for (int i = 0; i < 32; i += 8) {
       const int64_t c = tc * 32 + ty + i, r = tr * 32 + tx;
-      if (r < rows && c < cols) out[c * rows + r] = tile[tx][ty + i];
+      if (r < rows && c < cols) {
+        cd o = tile[tx][ty + i];
+        if (conj_scale) o = {o.x * scale, -o.y * scale};
+        out[c * rows + r] = o;
+      }
     }
     __syncthreads();
   }
@@ -713,50 +725,60 @@ hipError_t launch_power_accumulate(const cd *buf, int64_t nseg, int64_t flen, do
 }
 
 template <int LOG2L>
-static hipError_t launch_colfft_t(bool conj_in, bool twiddle, bool conj_scale_out, const cd *in,
+static hipError_t launch_colfft_t(bool conj_in, int twiddle, bool conj_scale_out, const cd *in,
                                   cd *out, int64_t C, int64_t ngroups, int64_t in_step,
                                   int64_t in_stride, int64_t out_step, int64_t out_stride,
                                   const cd *twl, const cd *twr, int log2r, double scale,
-                                  hipStream_t s) {
+                                  int64_t batch, int64_t mat_stride, hipStream_t s) {
   constexpr int CW = 256 / Geo<LOG2L>::T;
-  const dim3 grid((unsigned)((C + CW - 1) / CW), (unsigned)ngroups);
+  const dim3 grid((unsigned)((C + CW - 1) / CW), (unsigned)ngroups, (unsigned)batch);
 #define GDSP_CF(A, B, D)                                                                      \
   hipLaunchKernelGGL((colfft_tile_kernel<LOG2L, A, B, D>), grid, dim3(256), 0, s, in, out, C, \
-                     in_step, in_stride, out_step, out_stride, twl, twr, log2r, scale)
-  if (twiddle) {
-    if (conj_in) GDSP_CF(true, true, false);
-    else GDSP_CF(false, true, false);
+                     in_step, in_stride, out_step, out_stride, twl, twr, log2r, scale,         \
+                     mat_stride)
+  if (twiddle == 1) {
+    if (conj_in) GDSP_CF(true, 1, false);
+    else GDSP_CF(false, 1, false);
+  } else if (twiddle == 2) {
+    if (conj_in) GDSP_CF(true, 2, false);
+    else GDSP_CF(false, 2, false);
   } else if (conj_in) {
-    if (conj_scale_out) GDSP_CF(true, false, true);
-    else GDSP_CF(true, false, false);
+    if (conj_scale_out) GDSP_CF(true, 0, true);
+    else GDSP_CF(true, 0, false);
   } else {
-    if (conj_scale_out) GDSP_CF(false, false, true);
-    else GDSP_CF(false, false, false);
+    if (conj_scale_out) GDSP_CF(false, 0, true);
+    else GDSP_CF(false, 0, false);
   }
 #undef GDSP_CF
   return hipGetLastError();
 }
 
-hipError_t launch_colfft(int log2l, bool conj_in, bool twiddle, bool conj_scale_out, const cd *in,
+hipError_t launch_colfft(int log2l, bool conj_in, int twiddle, bool conj_scale_out, const cd *in,
                          cd *out, int64_t C, int64_t ngroups, int64_t in_step, int64_t in_stride,
                          int64_t out_step, int64_t out_stride, const cd *twl, const cd *twr,
-                         int log2r, double scale, hipStream_t s) {
+                         int log2r, double scale, int64_t batch, int64_t mat_stride,
+                         hipStream_t s) {
   if (twiddle && conj_scale_out) return hipErrorInvalidValue;
+  if (batch < 1 || batch > 65535) return hipErrorInvalidValue;
   switch (log2l) {
 #define GDSP_CFC(L)                                                                           \
   case L:                                                                                     \
     return launch_colfft_t<L>(conj_in, twiddle, conj_scale_out, in, out, C, ngroups, in_step, \
-                              in_stride, out_step, out_stride, twl, twr, log2r, scale, s);
+                              in_stride, out_step, out_stride, twl, twr, log2r, scale, batch, \
+                              mat_stride, s);
     GDSP_CFC(4) GDSP_CFC(5) GDSP_CFC(6) GDSP_CFC(7) GDSP_CFC(8) GDSP_CFC(9)
 #undef GDSP_CFC
     default: return hipErrorInvalidValue;
   }
 }
 
-hipError_t launch_transpose(const cd *in, cd *out, int64_t rows, int64_t cols, hipStream_t s) {
+hipError_t launch_transpose(const cd *in, cd *out, int64_t rows, int64_t cols, hipStream_t s,
+                            int64_t batch, bool conj_scale, double scale) {
+  if (batch < 1 || batch > 65535) return hipErrorInvalidValue;
   const int64_t tiles = ((rows + 31) / 32) * ((cols + 31) / 32);
   const unsigned nb = (unsigned)(tiles < 65536 ? tiles : 65536);
-  hipLaunchKernelGGL(transpose_kernel, dim3(nb), dim3(256), 0, s, in, out, rows, cols);
+  hipLaunchKernelGGL(transpose_kernel, dim3(nb, (unsigned)batch), dim3(256), 0, s, in, out, rows,
+                     cols, (int)conj_scale, scale);
   return hipGetLastError();
 }
 

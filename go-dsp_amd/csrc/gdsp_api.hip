@@ -99,7 +99,8 @@ bool lds_split_default() {
 // stream from two host threads at once.
 enum Slot {
   SLOT_IN = 0, SLOT_OUT, SLOT_AUX, SLOT_AUX2, SLOT_GLOBAL, SLOT_GLOBAL_IN, SLOT_REAL,
-  SLOT_BLU, SLOT_FFT2, SLOT_PW_PART, SLOT_PW_RED, SLOT_PW_BUF, SLOT_COUNT
+  SLOT_BLU, SLOT_FFT2, SLOT_PW_PART, SLOT_PW_RED, SLOT_PW_BUF, SLOT_FS0, SLOT_FS1, SLOT_FS2,
+  SLOT_FS3, SLOT_COUNT
 };
 
 struct Workspace {
@@ -236,7 +237,9 @@ struct gdsp_plan {
 
 namespace {
 
-std::mutex g_plan_mu;
+// recursive: building a Bluestein plan runs FFT_M(b), whose four-step path
+// fetches sub-plans from this cache on the same thread
+std::recursive_mutex g_plan_mu;
 std::map<std::pair<int, int64_t>, gdsp_plan *> g_plans;
 
 int exec_plan(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
@@ -330,7 +333,7 @@ int get_plan_locked(int dev, int64_t n, gdsp_plan **out) {
 int get_plan(int64_t n, gdsp_plan **out) {
   int dev = 0;
   STCHK(current_device(&dev));
-  std::lock_guard<std::mutex> lk(g_plan_mu);
+  std::lock_guard<std::recursive_mutex> lk(g_plan_mu);
   return get_plan_locked(dev, n, out);
 }
 
@@ -366,6 +369,55 @@ int exec_global(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool
   return GDSP_OK;
 }
 
+// Large power of 2, N = R*C (x as R rows x C columns, n = C*n1 + n2):
+//   A  column DFT_R over n1 for every n2, times W_N^(n2*k1)  (tile kernel, into work)
+//   B  row DFT_C over n2 for every k1, contiguous rows        (LDS kernel / recursion)
+//   C  X[k1 + R*k2] = Y[k1][k2]: transpose R x C -> C x R      (into out)
+// Three HBM round trips for N <= 2^22 (vs one per radix-16 pass), any batch.
+int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv,
+                    int load, hipStream_t s, int depth);
+
+int exec_fourstep(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
+                  hipStream_t s, int depth) {
+  const int ln = p->log2n;
+  int lr, lc;
+  if (ln - 13 >= gdsp::kColMinLog2 && ln - 13 <= gdsp::kColMaxLog2) {
+    lc = 13;
+    lr = ln - 13;
+  } else if (ln - 13 < gdsp::kColMinLog2) {
+    lr = gdsp::kColMinLog2;
+    lc = ln - lr;
+  } else {
+    lr = gdsp::kColMaxLog2;
+    lc = ln - lr;  // rows longer than 8192 recurse
+  }
+  if (depth >= 4) return fail(GDSP_ERR_UNSUPPORTED, "transform too long");
+  gdsp_plan *pr = nullptr, *pcol = nullptr;
+  STCHK(get_plan((int64_t)1 << lr, &pr));
+  STCHK(get_plan((int64_t)1 << lc, &pcol));
+  const int64_t N = p->n, R = (int64_t)1 << lr, C = (int64_t)1 << lc;
+  DevBuf work;
+  STCHK(work.alloc((size_t)batch * (size_t)N * sizeof(cd), s, (Slot)(SLOT_FS0 + depth)));
+  cd *w = (cd *)work.p;
+  const cd *src = (const cd *)in;
+  if (load == gdsp::LOAD_REAL) {
+    HIPCHK(gdsp::launch_real_to_complex((const double *)in, w, batch * N, s));
+    src = w;
+  }
+  for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+    const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+    HIPCHK(gdsp::launch_colfft(lr, inv, 2, false, src + b0 * N, w + b0 * N, C, 1, 0, 1, 0, 1,
+                               pr->tw, p->tw, ln, 1.0, nb, N, s));
+  }
+  STCHK(exec_plan_depth(pcol, w, w, batch * R, false, gdsp::LOAD_COMPLEX, s, depth + 1));
+  for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+    const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+    HIPCHK(gdsp::launch_transpose(w + b0 * N, out + b0 * N, R, C, s, nb, inv,
+                                  1.0 / (double)N));
+  }
+  return GDSP_OK;
+}
+
 int exec_bluestein_composed(const gdsp_plan *p, const cd *in, cd *out, int64_t batch, bool inv,
                             hipStream_t s) {
   DevBuf a;
@@ -384,6 +436,11 @@ int exec_bluestein_composed(const gdsp_plan *p, const cd *in, cd *out, int64_t b
 // reads float64 rows (fft.FFTReal); in == out is allowed.
 int exec_plan(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
               hipStream_t s) {
+  return exec_plan_depth(p, in, out, batch, inv, load, s, 0);
+}
+
+int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv,
+                    int load, hipStream_t s, int depth) {
   if (batch <= 0) return GDSP_OK;
   const double scale = 1.0 / (double)(p->n > 0 ? p->n : 1);
   switch (p->kind) {
@@ -401,6 +458,8 @@ int exec_plan(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool i
                                   scale, s));
       return GDSP_OK;
     case KIND_GLOBAL:
+      if (p->log2n <= 13 + 3 * gdsp::kColMaxLog2)
+        return exec_fourstep(p, in, out, batch, inv, load, s, depth);
       return exec_global(p, in, out, batch, inv, load, s);
     case KIND_BLUESTEIN:
     case KIND_BLUESTEIN_COMPOSED: {
@@ -581,18 +640,18 @@ int gdsp_fft2_device(const void *d_in, void *d_out, int64_t rows, int64_t cols, 
     STCHK(exec_plan(pc, d_in, work, rows, inv, gdsp::LOAD_COMPLEX, s));
     const double sc = 1.0 / (double)rows;
     if (lr <= gdsp::kColMaxLog2) {
-      HIPCHK(gdsp::launch_colfft(lr, inv, false, inv, work, (cd *)d_out, cols, 1, 0, 1, 0, 1,
-                                 pr->tw, nullptr, lr, sc, s));
+      HIPCHK(gdsp::launch_colfft(lr, inv, 0, inv, work, (cd *)d_out, cols, 1, 0, 1, 0, 1,
+                                 pr->tw, nullptr, lr, sc, 1, 0, s));
     } else {
       const int l1 = lr / 2, l2 = lr - l1;  // R1 <= R2
       gdsp_plan *p1 = nullptr, *p2 = nullptr;
       STCHK(get_plan((int64_t)1 << l1, &p1));
       STCHK(get_plan((int64_t)1 << l2, &p2));
       const int64_t R1 = (int64_t)1 << l1, R2 = (int64_t)1 << l2;
-      HIPCHK(gdsp::launch_colfft(l1, inv, true, false, work, work, cols, R2, 1, R2, 1, R2, p1->tw,
-                                 pr->tw, lr, 1.0, s));
-      HIPCHK(gdsp::launch_colfft(l2, false, false, inv, work, (cd *)d_out, cols, R1, R2, 1, 1, R1,
-                                 p2->tw, nullptr, lr, sc, s));
+      HIPCHK(gdsp::launch_colfft(l1, inv, 1, false, work, work, cols, R2, 1, R2, 1, R2, p1->tw,
+                                 pr->tw, lr, 1.0, 1, 0, s));
+      HIPCHK(gdsp::launch_colfft(l2, false, 0, inv, work, (cd *)d_out, cols, R1, R2, 1, 1, R1,
+                                 p2->tw, nullptr, lr, sc, 1, 0, s));
     }
     return GDSP_OK;
   }

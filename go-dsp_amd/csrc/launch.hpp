@@ -40,11 +40,15 @@ hipError_t launch_power_accumulate(const cd *buf, int64_t nseg, int64_t flen, do
                                    hipStream_t s);
 // FFT2 column pass on row-segment tiles; 4 <= log2l <= 9 (see fft_kernels.hip)
 constexpr int kColMinLog2 = 4, kColMaxLog2 = 9;
-hipError_t launch_colfft(int log2l, bool conj_in, bool twiddle, bool conj_scale_out, const cd *in,
+// twiddle: 0 none, 1 W_R^(group*j), 2 W_R^(col*j)
+hipError_t launch_colfft(int log2l, bool conj_in, int twiddle, bool conj_scale_out, const cd *in,
                          cd *out, int64_t C, int64_t ngroups, int64_t in_step, int64_t in_stride,
                          int64_t out_step, int64_t out_stride, const cd *twl, const cd *twr,
-                         int log2r, double scale, hipStream_t s);
-hipError_t launch_transpose(const cd *in, cd *out, int64_t rows, int64_t cols, hipStream_t s);
+                         int log2r, double scale, int64_t batch, int64_t mat_stride,
+                         hipStream_t s);
+// batch <= 65535 matrices of rows x cols, consecutive
+hipError_t launch_transpose(const cd *in, cd *out, int64_t rows, int64_t cols, hipStream_t s,
+                            int64_t batch = 1, bool conj_scale = false, double scale = 1.0);
 hipError_t launch_real_to_complex(const double *in, cd *out, int64_t count, hipStream_t s);
 hipError_t launch_chirp_premul(const cd *in, cd *a, int64_t n, int64_t m, int64_t batch,
                                const cd *chirp, bool conj_in, hipStream_t s);

@@ -103,7 +103,8 @@ def test_golden_fft2(gdsp, golden_fft):
 
 
 SIZES = [2, 3, 4, 5, 6, 7, 8, 9, 15, 16, 17, 31, 32, 33, 64, 100, 128, 255, 256, 512, 1000,
-         1024, 2048, 3000, 4096, 4097, 5000, 8192, 10000, 16384, 32768, 65536, 1 << 20]
+         1024, 2048, 3000, 4096, 4097, 5000, 8192, 10000, 16384, 32768, 65536, 1 << 17,
+         1 << 20, 1 << 22, 1 << 24, 100000]
 
 
 @pytest.mark.parametrize("n", SIZES)
@@ -121,7 +122,7 @@ def test_fft_sizes_vs_oracle(gdsp, oracle, n):
     assert nrel(gdsp.fft.FFT(x[0]), ref[0]) < TOL
 
 
-@pytest.mark.parametrize("n", [1, 2, 8, 1024, 3000, 4096])
+@pytest.mark.parametrize("n", [1, 2, 8, 1024, 3000, 4096, 1 << 18])
 def test_fft_real(gdsp, oracle, n):
     rng = np.random.default_rng(7 + n)
     x = rng.uniform(-1, 1, (4, n))
