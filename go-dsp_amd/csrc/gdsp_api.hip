@@ -100,7 +100,7 @@ bool lds_split_default() {
 enum Slot {
   SLOT_IN = 0, SLOT_OUT, SLOT_AUX, SLOT_AUX2, SLOT_GLOBAL, SLOT_GLOBAL_IN, SLOT_REAL,
   SLOT_BLU, SLOT_FFT2, SLOT_PW_PART, SLOT_PW_RED, SLOT_PW_BUF, SLOT_FS0, SLOT_FS1, SLOT_FS2,
-  SLOT_FS3, SLOT_COUNT
+  SLOT_FS3, SLOT_FFTN, SLOT_COUNT
 };
 
 struct Workspace {
@@ -662,6 +662,79 @@ int gdsp_fft2_device(const void *d_in, void *d_out, int64_t rows, int64_t cols, 
   return GDSP_OK;
 }
 
+// fft.FFTN / IFFTN (fft/fft.go:157-192): the 1-D transform along every line
+// of dimension 0, then 1, ... of a row-major array. Per axis (length L,
+// `inner` elements after it, `outer` before): contiguous lines (inner = 1) go
+// to the batched row kernels; strided power-of-2 lines to the column-tile
+// kernels batched over `outer` (one pass for L <= 512, the four-step split
+// above); anything else through a batched transpose, the row kernels and a
+// transpose back.
+static int fftn_device(const cd *in, cd *out, const int64_t *dims, int ndims, bool inv,
+                       hipStream_t s) {
+  if (ndims < 1 || !dims) return fail(GDSP_ERR_INVALID, "no dimensions");
+  int64_t total = 1;
+  for (int i = 0; i < ndims; ++i) {
+    if (dims[i] < 1) return fail(GDSP_ERR_INVALID, "invalid dimensions");  // matrix.go:43
+    total *= dims[i];
+  }
+  if (in != out)
+    HIPCHK(hipMemcpyAsync(out, in, (size_t)total * sizeof(cd), hipMemcpyDeviceToDevice, s));
+  DevBuf work;
+  STCHK(work.alloc((size_t)total * sizeof(cd), s, SLOT_FFTN));
+  cd *cur = out, *other = (cd *)work.p;
+  int64_t inner = total;
+  for (int d = 0; d < ndims; ++d) {
+    const int64_t L = dims[d];
+    inner /= L;
+    const int64_t outer = total / (L * inner);
+    if (L == 1) continue;
+    gdsp_plan *pl = nullptr;
+    STCHK(get_plan(L, &pl));
+    if (inner == 1) {
+      STCHK(exec_plan(pl, cur, cur, outer, inv, gdsp::LOAD_COMPLEX, s));
+      continue;
+    }
+    const int lL = ilog2(L);
+    const double sc = 1.0 / (double)L;
+    if (is_pow2(L) && lL >= gdsp::kColMinLog2 && lL <= 2 * gdsp::kColMaxLog2) {
+      const int l1 = lL <= gdsp::kColMaxLog2 ? lL : lL / 2, l2 = lL - l1;
+      gdsp_plan *p1 = nullptr, *p2 = nullptr;
+      STCHK(get_plan((int64_t)1 << l1, &p1));
+      if (l2) STCHK(get_plan((int64_t)1 << l2, &p2));
+      const int64_t R1 = (int64_t)1 << l1, R2 = (int64_t)1 << l2;
+      for (int64_t o0 = 0; o0 < outer; o0 += 65535) {
+        const int64_t nb = outer - o0 < 65535 ? outer - o0 : 65535;
+        cd *c0 = cur + o0 * L * inner, *t0 = other + o0 * L * inner;
+        if (!l2) {
+          HIPCHK(gdsp::launch_colfft(lL, inv, 0, inv, c0, c0, inner, 1, 0, 1, 0, 1, pl->tw,
+                                     nullptr, lL, sc, nb, L * inner, s));
+        } else {
+          HIPCHK(gdsp::launch_colfft(l1, inv, 1, false, c0, c0, inner, R2, 1, R2, 1, R2, p1->tw,
+                                     pl->tw, lL, 1.0, nb, L * inner, s));
+          HIPCHK(gdsp::launch_colfft(l2, false, 0, inv, c0, t0, inner, R1, R2, 1, 1, R1, p2->tw,
+                                     nullptr, lL, sc, nb, L * inner, s));
+        }
+      }
+      if (l2) std::swap(cur, other);
+      continue;
+    }
+    for (int64_t o0 = 0; o0 < outer; o0 += 65535) {
+      const int64_t nb = outer - o0 < 65535 ? outer - o0 : 65535;
+      HIPCHK(gdsp::launch_transpose(cur + o0 * L * inner, other + o0 * L * inner, L, inner, s,
+                                    nb));
+    }
+    STCHK(exec_plan(pl, other, other, outer * inner, inv, gdsp::LOAD_COMPLEX, s));
+    for (int64_t o0 = 0; o0 < outer; o0 += 65535) {
+      const int64_t nb = outer - o0 < 65535 ? outer - o0 : 65535;
+      HIPCHK(gdsp::launch_transpose(other + o0 * L * inner, cur + o0 * L * inner, inner, L, s,
+                                    nb));
+    }
+  }
+  if (cur != out)
+    HIPCHK(hipMemcpyAsync(out, cur, (size_t)total * sizeof(cd), hipMemcpyDeviceToDevice, s));
+  return GDSP_OK;
+}
+
 static int fft2_host(const double *x, bool real_in, double *out, int64_t rows, int64_t cols,
                      int inverse) {
   if (rows <= 0) return fail(GDSP_ERR_EMPTY, "empty input array");
@@ -693,6 +766,34 @@ int gdsp_fft2(const double *x, double *out, int64_t rows, int64_t cols, int inve
 
 int gdsp_fft2_real(const double *x, double *out, int64_t rows, int64_t cols, int inverse) {
   return fft2_host(x, true, out, rows, cols, inverse);
+}
+
+int gdsp_fftn_device(const void *d_in, void *d_out, const int64_t *dims, int ndims, int inverse,
+                     void *stream) {
+  int dev = 0;
+  STCHK(current_device(&dev));
+  return fftn_device((const cd *)d_in, (cd *)d_out, dims, ndims, inverse != 0,
+                     (hipStream_t)stream);
+}
+
+int gdsp_fftn(const double *x, double *out, const int64_t *dims, int ndims, int inverse) {
+  if (ndims < 1 || !dims || !x || !out) return fail(GDSP_ERR_INVALID, "bad argument");
+  int64_t total = 1;
+  for (int i = 0; i < ndims; ++i) {
+    if (dims[i] < 1) return fail(GDSP_ERR_INVALID, "invalid dimensions");
+    total *= dims[i];
+  }
+  int dev = 0;
+  STCHK(current_device(&dev));
+  hipStream_t s = thread_stream(dev);
+  const size_t bytes = (size_t)total * sizeof(cd);
+  DevBuf din, dout;
+  STCHK(din.alloc(bytes, s, SLOT_IN));
+  STCHK(dout.alloc(bytes, s, SLOT_OUT));
+  STCHK(copy_h2d(din.p, x, bytes, s));
+  STCHK(fftn_device((const cd *)din.p, (cd *)dout.p, dims, ndims, inverse != 0, s));
+  STCHK(copy_d2h(out, dout.p, bytes, s));
+  return GDSP_OK;
 }
 
 int gdsp_ensure_plan(int64_t n) {

@@ -88,3 +88,119 @@ def PrettyClose2(a, b) -> bool:
 def PrettyClose2F(a, b) -> bool:
     """compare.go:70-81."""
     return len(a) == len(b) and all(PrettyClose(c, d) for c, d in zip(a, b))
+
+
+class Matrix:
+    """dsputils.Matrix — dsputils/matrix.go:21-216: an N-D row-major complex128
+    array with whole-axis get/set (the container fft.FFTN transforms)."""
+
+    def __init__(self, lst: np.ndarray, dims, offsets):
+        self.list = lst
+        self.dims = list(dims)
+        self.offsets = list(offsets)
+
+    def offset(self, dims) -> int:
+        """matrix.go:93-107 (an index of -1 is used as is, like the reference)."""
+        if len(dims) != len(self.dims):
+            raise _panic("incorrect dimensions")
+        i = 0
+        for n, v in enumerate(dims):
+            if v > self.dims[n]:
+                raise _panic("incorrect dimensions")
+            i += v * self.offsets[n]
+        return i
+
+    def indexes(self, dims):
+        """matrix.go:110-142."""
+        i = -1
+        for n, v in enumerate(dims):
+            if v == -1:
+                if i >= 0:
+                    raise _panic("only one dimension index allowed")
+                i = n
+            elif v >= self.dims[n]:
+                raise _panic("dimension out of bounds")
+        if i == -1:
+            raise _panic("must specify one dimension index")
+        x = sum(self.offsets[n] * v for n, v in enumerate(dims) if v >= 0)
+        return x + self.offsets[i] * np.arange(self.dims[i])
+
+    def Dimensions(self):
+        """matrix.go:144-149."""
+        return list(self.dims)
+
+    def Dim(self, dims) -> np.ndarray:
+        """matrix.go:156-164."""
+        return self.list[self.indexes(dims)].copy()
+
+    def SetDim(self, x, dims) -> None:
+        """matrix.go:166-177."""
+        inds = self.indexes(dims)
+        x = np.asarray(x, np.complex128)
+        if x.size != inds.size:
+            raise _panic("incorrect array length")
+        self.list[inds] = x
+
+    def Value(self, dims) -> complex:
+        """matrix.go:179-183."""
+        return complex(self.list[self.offset(dims)])
+
+    def SetValue(self, x, dims) -> None:
+        """matrix.go:185-189."""
+        self.list[self.offset(dims)] = x
+
+    def To2D(self):
+        """matrix.go:191-205."""
+        if len(self.dims) != 2:
+            raise _panic("can only convert 2-D Matrixes")
+        return [self.list[i * self.dims[1]:(i + 1) * self.dims[1]].copy()
+                for i in range(self.dims[0])]
+
+    def Copy(self) -> "Matrix":
+        """matrix.go:75-80."""
+        return Matrix(self.list.copy(), self.dims, self.offsets)
+
+    def PrettyClose(self, n: "Matrix") -> bool:
+        """matrix.go:207-216."""
+        if any(v != n.dims[i] for i, v in enumerate(self.dims)):
+            return False
+        return PrettyCloseC(self.list, n.list)
+
+
+def _panic(msg: str):
+    from ._lib import GDSP_ERR_INVALID, Panic
+    return Panic(GDSP_ERR_INVALID, msg)
+
+
+def MakeMatrix(x, dims) -> Matrix:
+    """matrix.go:37-57 (x is used as the backing store, not copied)."""
+    length = 1
+    offsets = [0] * len(dims)
+    for i in range(len(dims) - 1, -1, -1):
+        if dims[i] < 1:
+            raise _panic("invalid dimensions")
+        offsets[i] = length
+        length *= dims[i]
+    x = np.asarray(x)
+    if x.dtype != np.complex128:
+        x = x.astype(np.complex128)
+    x = x.reshape(-1)
+    if x.size != length:
+        raise _panic("incorrect dimensions")
+    return Matrix(x, list(dims), offsets)
+
+
+def MakeMatrix2(x) -> Matrix:
+    """matrix.go:60-73."""
+    dims = [len(x), len(x[0])]
+    r = np.zeros(dims[0] * dims[1], np.complex128)
+    for n, v in enumerate(x):
+        if len(v) != dims[1]:
+            raise _panic("ragged array")
+        r[n * dims[1]:(n + 1) * dims[1]] = v
+    return MakeMatrix(r, dims)
+
+
+def MakeEmptyMatrix(dims) -> Matrix:
+    """matrix.go:83-90."""
+    return MakeMatrix(np.zeros(int(np.prod(dims)), np.complex128), dims)

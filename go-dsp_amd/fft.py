@@ -136,6 +136,26 @@ def IFFT2Real(x) -> np.ndarray:
     return _fft2(x, True, True)
 
 
+def _fftn(m, inverse: bool):
+    from .dsputils import MakeMatrix
+    x = np.ascontiguousarray(m.list, dtype=np.complex128)
+    dims = np.ascontiguousarray(np.asarray(m.dims, dtype=np.int64))
+    out = np.empty_like(x)
+    check(lib().gdsp_fftn(_p(x), _p(out), _p(dims), dims.size, int(inverse)), "FFTN")
+    return MakeMatrix(out, list(m.dims))
+
+
+def FFTN(m):
+    """fft.FFTN — fft/fft.go:157-159 (computeFFTN :166-192): N-D DFT of a
+    dsputils.Matrix; returns a new Matrix."""
+    return _fftn(m, False)
+
+
+def IFFTN(m):
+    """fft.IFFTN — fft/fft.go:162-164."""
+    return _fftn(m, True)
+
+
 def SetWorkerPoolSize(n: int) -> None:
     """fft.SetWorkerPoolSize — fft/fft.go:95-101 (recorded; the GPU path has no
     goroutine pool)."""

@@ -89,6 +89,69 @@ inline bool PrettyClose2(const std::vector<std::vector<complex>> &a,
   return true;
 }
 
+// dsputils.Matrix — dsputils/matrix.go:21-216 (row-major N-D complex128).
+struct Matrix {
+  std::vector<complex> list;
+  std::vector<int> dims, offsets;
+
+  int offset(const std::vector<int> &d) const {  // :93-107
+    if (d.size() != dims.size()) throw Panic(GDSP_ERR_INVALID, "incorrect dimensions");
+    int i = 0;
+    for (size_t n = 0; n < d.size(); ++n) {
+      if (d[n] > dims[n]) throw Panic(GDSP_ERR_INVALID, "incorrect dimensions");
+      i += d[n] * offsets[n];
+    }
+    return i;
+  }
+  std::vector<int> indexes(const std::vector<int> &d) const {  // :110-142
+    int ax = -1;
+    for (size_t n = 0; n < d.size(); ++n) {
+      if (d[n] == -1) {
+        if (ax >= 0) throw Panic(GDSP_ERR_INVALID, "only one dimension index allowed");
+        ax = (int)n;
+      } else if (d[n] >= dims[n]) {
+        throw Panic(GDSP_ERR_INVALID, "dimension out of bounds");
+      }
+    }
+    if (ax == -1) throw Panic(GDSP_ERR_INVALID, "must specify one dimension index");
+    int x = 0;
+    for (size_t n = 0; n < d.size(); ++n)
+      if (d[n] >= 0) x += offsets[n] * d[n];
+    std::vector<int> r(dims[ax]);
+    for (int j = 0; j < dims[ax]; ++j) r[j] = x + offsets[ax] * j;
+    return r;
+  }
+  std::vector<int> Dimensions() const { return dims; }
+  std::vector<complex> Dim(const std::vector<int> &d) const {
+    std::vector<complex> r;
+    for (int i : indexes(d)) r.push_back(list[i]);
+    return r;
+  }
+  void SetDim(const std::vector<complex> &x, const std::vector<int> &d) {
+    auto inds = indexes(d);
+    if (x.size() != inds.size()) throw Panic(GDSP_ERR_INVALID, "incorrect array length");
+    for (size_t n = 0; n < inds.size(); ++n) list[inds[n]] = x[n];
+  }
+  complex Value(const std::vector<int> &d) const { return list[offset(d)]; }
+  void SetValue(complex v, const std::vector<int> &d) { list[offset(d)] = v; }
+  bool PrettyClose(const Matrix &n) const { return dims == n.dims && PrettyCloseC(list, n.list); }
+};
+
+inline Matrix MakeMatrix(const std::vector<complex> &x, const std::vector<int> &dims) {  // :37-57
+  Matrix m;
+  m.offsets.assign(dims.size(), 0);
+  int length = 1;
+  for (int i = (int)dims.size() - 1; i >= 0; --i) {
+    if (dims[i] < 1) throw Panic(GDSP_ERR_INVALID, "invalid dimensions");
+    m.offsets[i] = length;
+    length *= dims[i];
+  }
+  if ((int)x.size() != length) throw Panic(GDSP_ERR_INVALID, "incorrect dimensions");
+  m.list = x;
+  m.dims = dims;
+  return m;
+}
+
 }  // namespace dsputils
 
 namespace fft {  // fft/fft.go
@@ -177,6 +240,16 @@ inline std::vector<complex> FFTBatch(const std::vector<complex> &x, size_t n, bo
         "FFTBatch");
   return r;
 }
+
+// fft.FFTN / IFFTN — fft.go:157-192
+inline dsputils::Matrix fftn(const dsputils::Matrix &m, int inverse) {
+  std::vector<int64_t> d(m.dims.begin(), m.dims.end());
+  std::vector<complex> o(m.list.size());
+  check(gdsp_fftn(cp(m.list), mp(o), d.data(), (int)d.size(), inverse), "FFTN");
+  return dsputils::MakeMatrix(o, m.dims);
+}
+inline dsputils::Matrix FFTN(const dsputils::Matrix &m) { return fftn(m, 0); }
+inline dsputils::Matrix IFFTN(const dsputils::Matrix &m) { return fftn(m, 1); }
 
 inline void SetWorkerPoolSize(int n) { gdsp_set_worker_pool_size(n); }  // fft.go:95-101
 inline void EnsureRadix2Factors(int input_len) {                        // radix2.go:35-37

@@ -93,6 +93,12 @@ int gdsp_fft2(const double *x, double *out, int64_t rows, int64_t cols, int inve
  * float64. */
 int gdsp_fft2_real(const double *x, double *out, int64_t rows, int64_t cols, int inverse);
 
+/* fft.FFTN / fft.IFFTN — fft/fft.go:157-192 (computeFFTN): the N-D DFT of a
+ * row-major dsputils.Matrix (dsputils/matrix.go:21-57) with dims[0..ndims),
+ * each >= 1 ("invalid dimensions" otherwise, GDSP_ERR_INVALID). x, out:
+ * prod(dims) complex128. */
+int gdsp_fftn(const double *x, double *out, const int64_t *dims, int ndims, int inverse);
+
 /* fft.EnsureRadix2Factors — fft/radix2.go:35-37: pre-build (and cache) the
  * device plan for length n on the current device. Works for any n >= 2. */
 int gdsp_ensure_plan(int64_t n);
@@ -149,6 +155,10 @@ int gdsp_fft_batch_device(const gdsp_plan *plan, const void *d_in, void *d_out,
  * rows*cols complex128 (may be NULL: the library allocates stream-ordered). */
 int gdsp_fft2_device(const void *d_in, void *d_out, int64_t rows, int64_t cols,
                      int inverse, void *d_work, void *stream);
+
+/* FFTN/IFFTN on a device array (dims on the host). */
+int gdsp_fftn_device(const void *d_in, void *d_out, const int64_t *dims, int ndims, int inverse,
+                     void *stream);
 
 /* Pwelch partial accumulation over segments [seg_begin, seg_end) of a device
  * signal d_x (n float64, sample 0 = sample 0 of segment 0). Adds into

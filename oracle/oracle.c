@@ -308,6 +308,47 @@ int or_fft2(const double *xd, double *outd, int64_t rows, int64_t cols, int inve
   return st;
 }
 
+/* ---- fft.go:157-192 computeFFTN: fftFunc along every line of dimension 0,
+ * then 1, ... (Matrix.Dim/SetDim, dsputils/matrix.go:110-177). The decrDim
+ * enumeration order (fft.go:197-224) does not change any value. */
+int or_fftn(const double *xd, double *outd, const int64_t *dims, int ndims, int inverse) {
+  int64_t total = 1;
+  for (int i = 0; i < ndims; i++) {
+    if (dims[i] < 1) return OR_ERR_INVALID; /* "invalid dimensions" matrix.go:43 */
+    total *= dims[i];
+  }
+  cplx *cur = (cplx *)outd;
+  memcpy(cur, xd, (size_t)total * sizeof(cplx));
+  int (*f)(const cplx *, cplx *, int64_t) = inverse ? ifft_c : fft_c;
+  for (int d = 0; d < ndims; d++) {
+    int64_t L = dims[d], inner = 1;
+    for (int e = d + 1; e < ndims; e++) inner *= dims[e];
+    int64_t outer = total / (L * inner);
+    cplx *line = (cplx *)malloc((size_t)L * sizeof(cplx));
+    cplx *res = (cplx *)malloc((size_t)L * sizeof(cplx));
+    if (!line || !res) {
+      free(line);
+      free(res);
+      return OR_ERR_NOMEM;
+    }
+    for (int64_t o = 0; o < outer; o++)
+      for (int64_t i = 0; i < inner; i++) {
+        cplx *base = cur + o * L * inner + i;
+        for (int64_t j = 0; j < L; j++) line[j] = base[j * inner];
+        int st = f(line, res, L);
+        if (st) {
+          free(line);
+          free(res);
+          return st;
+        }
+        for (int64_t j = 0; j < L; j++) base[j * inner] = res[j];
+      }
+    free(line);
+    free(res);
+  }
+  return OR_OK;
+}
+
 /* ---- Reference-threaded radix-2 (radix2.go:89-151) ------------------------
  * A persistent pool of spinning workers stands in for the goroutines the
  * reference spawns per call (a goroutine hand-off costs well under a

@@ -64,6 +64,9 @@ int or_convolve(const double *x, const double *y, double *out, int64_t n);
 /* fft.go:104-154: x is rows*cols complex, row-major (x[j][i] at j*cols+i). */
 int or_fft2(const double *x, double *out, int64_t rows, int64_t cols, int inverse);
 
+/* fft.go:157-192 (FFTN / IFFTN over a row-major Matrix of dims[0..ndims)). */
+int or_fftn(const double *x, double *out, const int64_t *dims, int ndims, int inverse);
+
 /* Reference-threaded radix-2 (radix2.go:89-151 structure: nworkers workers,
  * contiguous butterfly ranges of >= n/nworkers, one barrier per stage). Used
  * only as bench.py's cpu_baseline. Same arithmetic as or_fft. */

@@ -54,6 +54,8 @@ def lib():
         L.or_pwelch_threaded.argtypes = [P, I64, ctypes.c_double, I64, I64, I64, ctypes.c_int,
                                          ctypes.c_int, P, P, P, ctypes.c_int]
         L.or_pwelch_threaded.restype = ctypes.c_int
+        L.or_fftn.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int]
+        L.or_fftn.restype = ctypes.c_int
         L.or_segment_count.argtypes = [I64, I64, I64]
         L.or_segment_count.restype = I64
         L.or_reverse_bits.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
@@ -160,6 +162,16 @@ def fft2(x, inverse: bool = False) -> np.ndarray:
         raise OracleError("empty input array")
     out = np.empty_like(x)
     _check(lib().or_fft2(_p(x), _p(out), x.shape[0], x.shape[1], int(inverse)), "fft2")
+    return out
+
+
+def fftn(x, dims, inverse: bool = False) -> np.ndarray:
+    """fft.FFTN / IFFTN, fft/fft.go:157-192, on the flat row-major data of a
+    Matrix of the given dims."""
+    x = _c(x).ravel()
+    d = np.ascontiguousarray(np.asarray(dims, dtype=np.int64))
+    out = np.empty_like(x)
+    _check(lib().or_fftn(_p(x), _p(out), _p(d), d.size, int(inverse)), "fftn")
     return out
 
 

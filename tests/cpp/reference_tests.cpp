@@ -70,6 +70,20 @@ int main(int argc, char **argv) {
       EXPECT(dsputils::PrettyClose2(fft::FFT2Real(x), out), "FFT2Real " << r << "x" << c);
       EXPECT(dsputils::PrettyClose2(fft::IFFT2(out), dsputils::ToComplex2(x)),
              "IFFT2 " << r << "x" << c);
+    } else if (kind == "FFTN") {  // TestFFTN, fft_test.go:225-239
+      size_t nd;
+      in >> nd;
+      std::vector<int> dims(nd);
+      size_t n = 1;
+      for (auto &d : dims) {
+        in >> d;
+        n *= d;
+      }
+      auto x = dsputils::ToComplex(readd(in, n));
+      auto out = readc(in, n);
+      auto m = dsputils::MakeMatrix(x, dims), o = dsputils::MakeMatrix(out, dims);
+      EXPECT(fft::FFTN(m).PrettyClose(o), "FFTN");
+      EXPECT(fft::IFFTN(o).PrettyClose(m), "IFFTN");
     } else if (kind == "PWELCH") {  // TestPwelch, pwelch_test.go:48-60
       double fs;
       size_t n, lp;
@@ -124,6 +138,21 @@ int main(int argc, char **argv) {
   EXPECT(panics([] { fft::FFT2({{1, 2}, {3}}); }), "FFT2 ragged panics");
   EXPECT(fft::FFT({}).empty(), "FFT empty returns empty");
   EXPECT(spectral::Pwelch({}, 1, nullptr).first.empty(), "Pwelch empty returns empty");
+  // TestMakeMatrix, dsputils/matrix_test.go:23-47
+  {
+    std::vector<complex> v;
+    for (double d : {1, 2, 3, 4, 5, 6, 7, 8, 9, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 0, 4, 3, 2, 1})
+      v.push_back(d);
+    auto m = dsputils::MakeMatrix(v, {2, 3, 4});
+    EXPECT(dsputils::PrettyCloseC(m.Dim({1, 0, -1}), dsputils::ToComplex({3, 4, 5, 6})), "Dim 1");
+    EXPECT(dsputils::PrettyCloseC(m.Dim({0, -1, 2}), dsputils::ToComplex({3, 7, 1})), "Dim 2");
+    EXPECT(dsputils::PrettyCloseC(m.Dim({-1, 1, 3}), dsputils::ToComplex({8, 0})), "Dim 3");
+    auto s3 = dsputils::ToComplex({10, 11, 12});
+    m.SetDim(s3, {1, -1, 3});
+    EXPECT(dsputils::PrettyCloseC(m.Dim({1, -1, 3}), s3), "SetDim");
+    m.SetValue(complex(14, 0), {1, -1, 3});
+    EXPECT(dsputils::ComplexEqual(m.Value({1, -1, 3}), complex(14, 0)), "SetValue");
+  }
   // TestFFTMulti (fft_test.go:251-259) + a Bluestein batch through FFTBatch
   std::vector<complex> a(256);
   for (int i = 0; i < 256; ++i) a[i] = {i / 256.0, 0};

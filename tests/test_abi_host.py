@@ -111,3 +111,26 @@ def test_worker_pool_size_recorded(gdsp):
     assert gdsp._lib.lib().gdsp_worker_pool_size() == 0
     gdsp.fft.SetWorkerPoolSize(4)
     assert gdsp._lib.lib().gdsp_worker_pool_size() == 4
+
+
+def test_matrix_reference_table(gdsp):
+    # dsputils/matrix_test.go:23-47 (TestMakeMatrix)
+    U = gdsp.dsputils
+    m = U.MakeMatrix([1, 2, 3, 4, 5, 6, 7, 8, 9, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 0, 4, 3, 2, 1],
+                     [2, 3, 4])
+    assert U.PrettyCloseC(m.Dim([1, 0, -1]), U.ToComplex([3, 4, 5, 6]))
+    assert U.PrettyCloseC(m.Dim([0, -1, 2]), U.ToComplex([3, 7, 1]))
+    assert U.PrettyCloseC(m.Dim([-1, 1, 3]), U.ToComplex([8, 0]))
+    s = U.ToComplex([10, 11, 12])
+    i = [1, -1, 3]
+    m.SetDim(s, i)
+    assert U.PrettyCloseC(m.Dim(i), s)
+    m.SetValue(14 + 0j, i)
+    assert U.ComplexEqual(m.Value(i), 14 + 0j)
+    with pytest.raises(gdsp.Panic):
+        U.MakeMatrix([1, 2, 3], [2, 2])
+    with pytest.raises(gdsp.Panic):
+        U.MakeMatrix([], [0])
+    with pytest.raises(gdsp.Panic):
+        m.Dim([-1, -1, 0])
+    assert [list(r) for r in U.MakeMatrix2([[1, 2], [3, 4]]).To2D()] == [[1, 2], [3, 4]]

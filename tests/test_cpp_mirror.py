@@ -21,6 +21,10 @@ def _write_vectors(refvec, path):
         lines.append(" ".join(["FFT2", str(r), str(k)]
                               + [repr(float(v)) for row in c["in"] for v in row]
                               + [repr(float(v)) for row in c["out"] for p in row for v in p]))
+    for c in refvec["fftnTests"]:
+        lines.append(" ".join(["FFTN", str(len(c["dim"]))] + [str(d) for d in c["dim"]]
+                              + [repr(float(v)) for v in c["in"]]
+                              + [repr(float(v)) for p in c["out"] for v in p]))
     for c in refvec["pwelchTests"]:
         if not c["x"]:
             continue

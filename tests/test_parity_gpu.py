@@ -254,3 +254,25 @@ def test_plan_kinds(gdsp):
     assert D.plan(1 << 16).kind == 2
     assert D.plan(3000).kind == 3
     assert D.plan(10000).kind == 4
+
+
+def test_TestFFTN(gdsp, refvec):
+    # fft/fft_test.go:225-239
+    U = gdsp.dsputils
+    for c in refvec["fftnTests"]:
+        m = U.MakeMatrix(U.ToComplex(c["in"]), c["dim"])
+        o = U.MakeMatrix(cpx(c["out"]), c["dim"])
+        assert gdsp.fft.FFTN(m).PrettyClose(o)
+        assert gdsp.fft.IFFTN(o).PrettyClose(m)
+
+
+@pytest.mark.parametrize("dims", [[2, 2, 3], [5], [16, 16], [3, 5, 7], [64, 1, 32], [32, 16, 8, 4],
+                                  [1024, 16], [2048, 9], [7, 100, 3], [4, 4096], [2, 3, 3000],
+                                  [600, 20], [2, 1, 1, 2]])
+def test_fftn_vs_oracle(gdsp, oracle, dims):
+    rng = np.random.default_rng(sum(dims))
+    n = int(np.prod(dims))
+    x = rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)
+    m = gdsp.dsputils.MakeMatrix(x, dims)
+    assert nrel(gdsp.fft.FFTN(m).list, oracle.fftn(x, dims)) < TOL
+    assert nrel(gdsp.fft.IFFTN(m).list, oracle.fftn(x, dims, inverse=True)) < TOL
