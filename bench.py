@@ -10,6 +10,9 @@ independent). value = samples of all ranks / max-over-ranks wall time.
 
 Other workloads (--workload): bluestein3000, fft2_8192, pwelch (the other
 BASELINE configs; pwelch uses one RCCL all-reduce of the PSD accumulators).
+bluestein3000 is fft.FFT of N = 3000 through the production dispatch (the
+mixed-radix 8*5*5*5*3 kernel); chirpz3000 times the same workload through the
+reference's algorithm (forced Bluestein plan, gdsp_plan_create_chirpz).
 
 roofline.achieved = algorithmic bytes of one launch (32 B/sample: 16 B read +
 16 B written) / the launch's average duration, measured with
@@ -41,7 +44,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="radix4096",
-                    choices=["radix4096", "bluestein3000", "fft2_8192", "pwelch"])
+                    choices=["radix4096", "bluestein3000", "chirpz3000", "fft2_8192", "pwelch"])
     ap.add_argument("--batch", type=int, default=0, help="rows per GPU (0 = config default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU seconds for the cpu_baseline sample (0 disables)")
@@ -78,21 +81,27 @@ def main():
             dist.barrier()
 
     w = args.workload
-    if w in ("radix4096", "bluestein3000"):
+    if w in ("radix4096", "bluestein3000", "chirpz3000"):
         n = 4096 if w == "radix4096" else 3000
+        chirpz = w == "chirpz3000"
         batch = args.batch or 65536
         x = torch.empty((batch, n), dtype=torch.complex128, device=dev)
         y = torch.empty_like(x)
         D.fill_uniform(x, SEED, offset=rank * batch * n * 2, stream=stream)
+        kind = D.plan(n, chirpz).kind
 
         def step():
-            D.fft_batch(x, y, stream=stream)
+            D.fft_batch(x, y, stream=stream, chirpz=chirpz)
 
         samples_per_step = batch * n
         alg_bytes = 32 * samples_per_step
+        algo = {1: "Stockham radix-16 (one kernel)", 3: "Bluestein chirp-z (fused, M=8192)",
+                5: "mixed-radix Stockham 8*5*5*5*3 (one kernel)"}.get(kind, str(kind))
         cfg = {"workload": f"fft.FFT batched complex128 N={n} x {batch} rows per GPU",
-               "n": n, "batch_per_gpu": batch, "parallelism": f"shard{world}"}
-        kernel = "fft_lds_kernel<12>" if n == 4096 else "bluestein_kernel<13>"
+               "n": n, "batch_per_gpu": batch, "parallelism": f"shard{world}",
+               "algorithm": algo}
+        kernel = {1: "fft_lds_kernel<12>", 3: "bluestein_kernel<13>",
+                  5: "fft_mixed_kernel"}.get(kind, str(kind))
         metric = "Gsamples/s + % HBM roofline, batched N=4096 complex128 FFT at 1/2/4/8 GPUs"
     elif w == "fft2_8192":
         rows = cols = 8192
@@ -127,7 +136,7 @@ def main():
         alg_bytes = 8 * x.numel()
         cfg = {"workload": "spectral.Pwelch 2^30-sample stream, Hann NFFT 4096, 50% overlap",
                "segments_total": sh.nsegs_total, "parallelism": f"segments{world}+allreduce"}
-        kernel = "pwelch_kernel<12>"
+        kernel = "pwelch_half_kernel<12>"
         metric = "Gsamples/s, spectral.Pwelch 2^30 samples NFFT 4096 50% overlap"
     torch.cuda.synchronize()
     for _ in range(args.warmup):
@@ -157,7 +166,7 @@ def main():
 
     # parity spot check of this run's output (untimed)
     check = None
-    if rank == 0 and args.check_rows > 0 and w in ("radix4096", "bluestein3000"):
+    if rank == 0 and args.check_rows > 0 and w in ("radix4096", "bluestein3000", "chirpz3000"):
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import numpy as np
         import oracle
@@ -234,7 +243,7 @@ def cpu_baseline(workload: str, seconds: float):
                 "kind": "port",
                 "sample": f"spectral.Pwelch on a {n}-sample prefix of the stream "
                           f"(NFFT 4096, 50% overlap, {dt:.1f} s), {pool}"}
-    n = {"radix4096": 4096, "bluestein3000": 3000, "fft2_8192": 8192}[workload]
+    n = {"radix4096": 4096, "bluestein3000": 3000, "chirpz3000": 3000, "fft2_8192": 8192}[workload]
     rows = 64 if n != 8192 else 16
     x = oracle.fill_uniform(2 * n * rows, SEED).view(np.complex128).reshape(rows, n)
     done = 0

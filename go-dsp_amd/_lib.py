@@ -57,6 +57,7 @@ SIGNATURES = {
                          ctypes.POINTER(_I64)]),
     "gdsp_window_hann": (_I, [_I64, _P]),
     "gdsp_plan_create": (_I, [_I64, ctypes.POINTER(_P)]),
+    "gdsp_plan_create_chirpz": (_I, [_I64, ctypes.POINTER(_P)]),
     "gdsp_plan_destroy": (_I, [_P]),
     "gdsp_plan_kind": (_I, [_P]),
     "gdsp_fft_batch_device": (_I, [_P, _P, _P, _I64, _I, _P]),

@@ -7,6 +7,7 @@
 #include <math.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <string>
@@ -218,14 +219,16 @@ int copy_d2h(void *dst, const void *src, size_t bytes, hipStream_t s) {
 }  // namespace
 
 enum PlanKind { KIND_TRIVIAL = 0, KIND_LDS = 1, KIND_GLOBAL = 2, KIND_BLUESTEIN = 3,
-                KIND_BLUESTEIN_COMPOSED = 4 };
+                KIND_BLUESTEIN_COMPOSED = 4, KIND_MIXED = 5 };
 
 struct gdsp_plan {
   int device = 0;
   int64_t n = 0;
   int kind = KIND_TRIVIAL;
   int log2n = 0;
-  cd *tw = nullptr;  // power of 2: T_n[k] = exp(-2 pi i k/n), n entries
+  cd *tw = nullptr;  // power of 2: T_n[k] = exp(-2 pi i k/n), n entries;
+                     // mixed radix: the per-pass butterfly-major table
+  gdsp::MixedDesc md{};
   // Bluestein (fft/bluestein.go): M = NextPowerOf2(2n-1), chirp = conj(w),
   // bhat = FFT_M(b)/M
   int64_t m = 0;
@@ -241,6 +244,7 @@ namespace {
 // fetches sub-plans from this cache on the same thread
 std::recursive_mutex g_plan_mu;
 std::map<std::pair<int, int64_t>, gdsp_plan *> g_plans;
+std::map<std::pair<int, int64_t>, gdsp_plan *> g_chirpz_plans;  // forced Bluestein
 
 int exec_plan(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
               hipStream_t s);
@@ -261,18 +265,85 @@ int upload_twiddles(int dev, int64_t n, cd **dst) {
 
 int get_plan_locked(int dev, int64_t n, gdsp_plan **out);
 
-int build_plan(int dev, int64_t n, gdsp_plan *p) {
+// Radices of the mixed-radix kernel for n (fft_mixed.hip), or false when n is
+// a power of 2, too long, or has a prime factor above 13 (-> Bluestein).
+bool mixed_radices(int64_t n, std::vector<int> &rad) {
+  rad.clear();
+  if (n < 2 || n > gdsp::kMixedMax || is_pow2(n)) return false;
+  int64_t m = n;
+  int a = 0;
+  while (m % 2 == 0) {
+    m /= 2;
+    ++a;
+  }
+  std::vector<int> odd;
+  for (int q : {13, 11, 7, 5, 3})
+    while (m % q == 0) {
+      m /= q;
+      odd.push_back(q);
+    }
+  if (m != 1) return false;
+  while (a >= 4) {
+    rad.push_back(16);
+    a -= 4;
+  }
+  if (a) rad.push_back(1 << a);
+  rad.insert(rad.end(), odd.begin(), odd.end());
+  return rad.size() <= 12;
+}
+
+int build_mixed(int dev, int64_t n, const std::vector<int> &rad, gdsp_plan *p) {
+  p->kind = KIND_MIXED;
+  gdsp::MixedDesc &d = p->md;
+  d.n = (int)n;
+  d.npass = (int)rad.size();
+  d.codes = 0;
+  int need = 1;
+  for (size_t q = 0; q < rad.size(); ++q) {
+    d.codes |= (uint64_t)rad[q] << (5 * q);
+    const int jmax = 16 / rad[q], nb = (int)n / rad[q];
+    need = std::max(need, (nb + jmax - 1) / jmax);
+  }
+  int t1 = 1;
+  while (t1 < need) t1 <<= 1;
+  if (t1 > 64) t1 = (need + 63) / 64 * 64;
+  if (t1 > 512) return fail(GDSP_ERR_UNSUPPORTED, "mixed-radix geometry");
+  d.t1 = t1;
+  d.tpw = std::max(1, std::min(256 / t1, gdsp::kMixedMax / (int)n));
+  // per-pass twiddles W_{Ns*R}^{k*r}, k < Ns, r = 1..R-1, butterfly-major
+  std::vector<cd> h;
+  int64_t ns = rad[0];
+  for (size_t q = 1; q < rad.size(); ++q) {
+    const int R = rad[q];
+    for (int64_t k = 0; k < ns; ++k)
+      for (int r = 1; r < R; ++r) {
+        const long double ang = -2.0L * 3.141592653589793238462643383279502884L *
+                                (long double)(k * r) / (long double)(ns * R);
+        h.push_back({(double)cosl(ang), (double)sinl(ang)});
+      }
+    ns *= R;
+  }
+  if (h.empty()) h.push_back({1.0, 0.0});
+  HIPCHK(hipMalloc((void **)&p->tw, h.size() * sizeof(cd)));
+  STCHK(copy_h2d(p->tw, h.data(), h.size() * sizeof(cd), thread_stream(dev)));
+  HIPCHK(hipStreamSynchronize(thread_stream(dev)));
+  return GDSP_OK;
+}
+
+int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   p->device = dev;
   p->n = n;
   if (n <= 1) {
     p->kind = KIND_TRIVIAL;
     return GDSP_OK;
   }
-  if (is_pow2(n)) {
+  if (is_pow2(n) && !chirpz) {
     p->log2n = ilog2(n);
     p->kind = p->log2n <= gdsp::kMaxLdsLog2 ? KIND_LDS : KIND_GLOBAL;
     return upload_twiddles(dev, n, &p->tw);
   }
+  std::vector<int> rad;
+  if (!chirpz && mixed_radices(n, rad)) return build_mixed(dev, n, rad, p);
   // Bluestein factors, bluestein.go:32-61: w_k = (cos, sin)(Pi/n * k*k),
   // k = 0 exactly 1 (angle not reduced, as the reference computes it).
   p->m = next_pow2_ref(2 * n - 1);
@@ -312,29 +383,34 @@ int build_plan(int dev, int64_t n, gdsp_plan *p) {
   return st;
 }
 
-int get_plan_locked(int dev, int64_t n, gdsp_plan **out) {
+int get_plan_locked(int dev, int64_t n, gdsp_plan **out, bool chirpz = false) {
+  auto &cache = chirpz ? g_chirpz_plans : g_plans;
   auto key = std::make_pair(dev, n);
-  auto it = g_plans.find(key);
-  if (it != g_plans.end()) {
+  auto it = cache.find(key);
+  if (it != cache.end()) {
     *out = it->second;
     return GDSP_OK;
   }
   gdsp_plan *p = new gdsp_plan();
-  int st = build_plan(dev, n, p);
+  int st = build_plan(dev, n, p, chirpz);
   if (st != GDSP_OK) {
     delete p;  // device tables of a failed plan are leaked deliberately (rare)
     return st;
   }
-  g_plans[key] = p;
+  cache[key] = p;
   *out = p;
   return GDSP_OK;
 }
 
-int get_plan(int64_t n, gdsp_plan **out) {
+int get_plan_locked(int dev, int64_t n, gdsp_plan **out) {
+  return get_plan_locked(dev, n, out, false);
+}
+
+int get_plan(int64_t n, gdsp_plan **out, bool chirpz = false) {
   int dev = 0;
   STCHK(current_device(&dev));
   std::lock_guard<std::recursive_mutex> lk(g_plan_mu);
-  return get_plan_locked(dev, n, out);
+  return get_plan_locked(dev, n, out, chirpz);
 }
 
 // Large power of 2: radix-16 Stockham passes through HBM, last pass into out.
@@ -453,6 +529,9 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
       }
       return GDSP_OK;
     }
+    case KIND_MIXED:
+      HIPCHK(gdsp::launch_fft_mixed(p->md, inv, load, in, out, batch, p->tw, scale, s));
+      return GDSP_OK;
     case KIND_LDS:
       HIPCHK(gdsp::launch_fft_lds(p->log2n, inv, load, lds_split_default(), in, out, batch, p->tw,
                                   scale, s));
@@ -819,6 +898,11 @@ int gdsp_window_hann(int64_t L, double *out) {
 int gdsp_plan_create(int64_t n, gdsp_plan **plan) {
   if (n < 0 || !plan) return fail(GDSP_ERR_INVALID, "bad argument");
   return get_plan(n, plan);
+}
+
+int gdsp_plan_create_chirpz(int64_t n, gdsp_plan **plan) {
+  if (n < 2 || !plan) return fail(GDSP_ERR_INVALID, "bad argument");
+  return get_plan(n, plan, true);
 }
 
 int gdsp_plan_destroy(gdsp_plan *) { return GDSP_OK; }

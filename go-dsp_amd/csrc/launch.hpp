@@ -16,6 +16,15 @@ constexpr int kMaxLdsLog2 = 14;
 
 hipError_t launch_fft_lds(int log2n, bool inv, int load, bool split, const void *in, cd *out,
                           int64_t batch, const cd *tw, double scale, hipStream_t s);
+// Mixed-radix one-kernel transform (fft_mixed.hip): n = prod of the radices
+// in `codes` (5 bits per pass, radices 2,3,4,5,7,8,11,13,16), n <= kMixedMax.
+struct MixedDesc {
+  uint64_t codes;
+  int n, npass, t1, tpw;
+};
+constexpr int kMixedMax = 4096;
+hipError_t launch_fft_mixed(const MixedDesc &d, bool inv, int load, const void *in, cd *out,
+                            int64_t batch, const cd *tw, double scale, hipStream_t s);
 hipError_t launch_bluestein(int log2m, bool inv, const cd *in, cd *out, int64_t n,
                             int64_t batch, const cd *twm, const cd *chirp, const cd *bhat,
                             double scale, hipStream_t s);

@@ -29,35 +29,43 @@ def _ptr(t) -> ctypes.c_void_p:
 class Plan:
     """Cached device plan for transform length n on the current device
     (gdsp_plan_create). kind: 0 trivial, 1 LDS Stockham, 2 multi-pass
-    Stockham, 3 fused Bluestein, 4 composed Bluestein."""
+    Stockham, 3 fused Bluestein, 4 composed Bluestein, 5 mixed radix.
+    chirpz=True forces the reference's Bluestein algorithm
+    (gdsp_plan_create_chirpz) for a non-trivial length."""
 
-    def __init__(self, n: int):
+    def __init__(self, n: int, chirpz: bool = False):
         self.n = int(n)
+        self.chirpz = bool(chirpz)
         self.handle = ctypes.c_void_p()
-        check(lib().gdsp_plan_create(self.n, ctypes.byref(self.handle)), "plan_create")
+        if self.chirpz:
+            check(lib().gdsp_plan_create_chirpz(self.n, ctypes.byref(self.handle)),
+                  "plan_create_chirpz")
+        else:
+            check(lib().gdsp_plan_create(self.n, ctypes.byref(self.handle)), "plan_create")
         self.kind = int(lib().gdsp_plan_kind(self.handle))
 
 
 _plans: dict = {}
 
 
-def plan(n: int) -> Plan:
+def plan(n: int, chirpz: bool = False) -> Plan:
     torch = _torch()
-    key = (torch.cuda.current_device(), int(n))
+    key = (torch.cuda.current_device(), int(n), bool(chirpz))
     if key not in _plans:
-        _plans[key] = Plan(n)
+        _plans[key] = Plan(n, chirpz)
     return _plans[key]
 
 
-def fft_batch(x, out=None, inverse: bool = False, stream=None):
-    """Batched FFT/IFFT of the rows of a (batch, n) complex128 CUDA tensor."""
+def fft_batch(x, out=None, inverse: bool = False, stream=None, chirpz: bool = False):
+    """Batched FFT/IFFT of the rows of a (batch, n) complex128 CUDA tensor
+    (chirpz=True: through the forced-Bluestein plan)."""
     torch = _torch()
     assert x.is_cuda and x.dtype == torch.complex128 and x.dim() == 2 and x.is_contiguous()
     if out is None:
         out = torch.empty_like(x)
     assert out.shape == x.shape and out.dtype == x.dtype and out.is_contiguous()
     with torch.cuda.device(x.device):
-        p = plan(x.shape[1])
+        p = plan(x.shape[1], chirpz)
         check(lib().gdsp_fft_batch_device(p.handle, _ptr(x), _ptr(out), x.shape[0], int(inverse),
                                           _stream_ptr(stream, x.device)), "fft_batch_device")
     return out

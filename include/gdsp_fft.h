@@ -58,8 +58,10 @@ int gdsp_device_count(void);
 /* ---- fft package: host pointers, synchronous ----------------------------- */
 
 /* fft.FFT — fft/fft.go:72-87. n <= 1 copies; power of 2 → Stockham radix-16
- * kernels (reference: radix2FFT, fft/radix2.go:80-154); otherwise Bluestein
- * (fft/bluestein.go:68-94). x, out: n complex128. */
+ * kernels (reference: radix2FFT, fft/radix2.go:80-154); other n whose prime
+ * factors are all <= 13 (n <= 4096) → a mixed-radix Stockham kernel computing
+ * the same DFT directly; otherwise Bluestein (fft/bluestein.go:68-94).
+ * x, out: n complex128. */
 int gdsp_fft(const double *x, double *out, int64_t n);
 
 /* fft.IFFT — fft/fft.go:35-52. n == 0 → GDSP_ERR_EMPTY (reference panics). */
@@ -141,9 +143,15 @@ typedef struct gdsp_plan gdsp_plan;
  * plans and exists for API symmetry. */
 int gdsp_plan_create(int64_t n, gdsp_plan **plan);
 int gdsp_plan_destroy(gdsp_plan *plan);
+/* The same transform as fft.FFT for non-power-of-2 n, always computed with
+ * Bluestein's chirp-z (fft/bluestein.go:68-94) — the reference's algorithm —
+ * even where the default plan uses the mixed-radix kernel. n >= 2. Cached
+ * separately from gdsp_plan_create's plans. */
+int gdsp_plan_create_chirpz(int64_t n, gdsp_plan **plan);
 /* Which algorithm a plan runs: 0 trivial (n<=1), 1 one-kernel LDS Stockham,
  * 2 multi-pass global Stockham (large power of 2), 3 fused Bluestein,
- * 4 composed Bluestein (M > 16384). */
+ * 4 composed Bluestein (M > 16384), 5 one-kernel mixed radix (non-power-of-2
+ * n <= 4096 whose prime factors are all <= 13). */
 int gdsp_plan_kind(const gdsp_plan *plan);
 
 /* Batched C2C on device buffers: d_in/d_out hold batch*n complex128 (may

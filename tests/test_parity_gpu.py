@@ -252,8 +252,58 @@ def test_plan_kinds(gdsp):
     assert D.plan(1).kind == 0
     assert D.plan(4096).kind == 1
     assert D.plan(1 << 16).kind == 2
-    assert D.plan(3000).kind == 3
-    assert D.plan(10000).kind == 4
+    assert D.plan(3000).kind == 5  # 2^3 3 5^3: mixed radix
+    assert D.plan(4097).kind == 3  # 17 * 241: fused Bluestein
+    assert D.plan(10000).kind == 4  # > 4096, M = 32768: composed Bluestein
+    assert D.plan(3000, chirpz=True).kind == 3
+    assert D.plan(10000, chirpz=True).kind == 4
+    assert D.plan(4096, chirpz=True).kind == 3  # forced chirp-z on a power of 2
+
+
+# every prime in the mixed-radix set, products of them, the largest lengths it
+# takes, and neighbours that fall back to Bluestein (17, 19*...)
+MIXED = [3, 5, 6, 7, 10, 11, 12, 13, 14, 18, 20, 21, 22, 24, 25, 26, 27, 39, 48, 49, 60, 77,
+         81, 96, 100, 121, 125, 143, 169, 243, 343, 360, 625, 720, 729, 1000, 1001, 1331, 1536,
+         2048 + 1024, 2187, 2197, 2401, 2500, 3000, 3125, 3375, 3840, 4000, 4095, 4050, 19 * 5,
+         17 * 3]
+
+
+@pytest.mark.parametrize("n", MIXED)
+def test_mixed_radix_vs_oracle(gdsp, oracle, n):
+    rng = np.random.default_rng(1000 + n)
+    batch = 5
+    x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
+    assert row_nrel(gdsp.fft.FFTBatch(x), oracle.fft_rows(x)) < TOL
+    assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL
+    xr = rng.uniform(-1, 1, (batch, n))
+    assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
+
+
+@pytest.mark.parametrize("n", [3, 5, 100, 3000, 4097, 10000])
+def test_chirpz_plan_vs_oracle(gdsp, oracle, n):
+    # the reference's own algorithm (Bluestein) on the device API, against the
+    # oracle and against the default plan for the same length
+    import torch
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    rng = np.random.default_rng(2000 + n)
+    x = rng.uniform(-1, 1, (7, n)) + 1j * rng.uniform(-1, 1, (7, n))
+    xt = torch.from_numpy(x).cuda()
+    yc = D.fft_batch(xt, chirpz=True).cpu().numpy()
+    yd = D.fft_batch(xt).cpu().numpy()
+    ref = oracle.fft_rows(x)
+    assert row_nrel(yc, ref) < TOL and row_nrel(yd, ref) < TOL
+    yci = D.fft_batch(xt, inverse=True, chirpz=True).cpu().numpy()
+    assert row_nrel(yci, oracle.ifft_rows(x)) < TOL
+
+
+def test_mixed_radix_large_batch(gdsp, oracle):
+    # grid wider than one launch's tail handling: odd batch, transforms per
+    # workgroup > 1 (n = 12: 4 per group of 16 threads)
+    for n, batch in [(12, 1001), (3000, 333), (100, 4099)]:
+        x = oracle.fill_uniform(2 * n * batch, 0x5EED, n).view(np.complex128).reshape(batch, n)
+        y = gdsp.fft.FFTBatch(x)
+        assert row_nrel(y, oracle.fft_rows(x)) < TOL, n
+        assert row_nrel(gdsp.fft.FFTBatch(y, inverse=True), x) < TOL, n
 
 
 def test_TestFFTN(gdsp, refvec):

@@ -12,8 +12,9 @@ import statistics
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"radix4096": "fft_lds_kernel<12", "bluestein3000": "bluestein_kernel<13",
-           "pwelch": "pwelch_kernel<12", "fft2_8192": "fft_lds_kernel<13"}
+KERNELS = {"radix4096": "fft_lds_kernel<12", "bluestein3000": "fft_mixed_kernel",
+           "chirpz3000": "bluestein_kernel<13",
+           "pwelch": "pwelch_half_kernel<12", "fft2_8192": "fft_lds_kernel<13"}
 
 
 def values(w, counter):
