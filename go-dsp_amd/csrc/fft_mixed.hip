@@ -25,7 +25,7 @@
 namespace gdsp {
 
 template <int R>
-struct OddTab;  // cos / sin(2 pi q / R), q < R
+struct OddTab;  // cos / sin(2 pi q / R), q < R (primes and the composite radices)
 template <>
 struct OddTab<3> {
   static constexpr double c[3] = {1, -0.5, -0.5};
@@ -110,6 +110,42 @@ struct OddTab<13> {
                                    -0.46472317204376856};
 };
 
+template <>
+struct OddTab<6> {
+  static constexpr double c[6] = {1, 0.5, -0.5, -1, -0.5, 0.5};
+  static constexpr double s[6] = {0, 0.8660254037844386, 0.8660254037844386, -3.8247850373932361e-40, -0.8660254037844386, -0.8660254037844386};
+};
+template <>
+struct OddTab<9> {
+  static constexpr double c[9] = {1, 0.76604444311897801, 0.17364817766693036, -0.5, -0.93969262078590843, -0.93969262078590843, -0.5, 0.17364817766693036, 0.76604444311897801};
+  static constexpr double s[9] = {0, 0.64278760968653936, 0.98480775301220802, 0.8660254037844386, 0.34202014332566871, -0.34202014332566871, -0.8660254037844386, -0.98480775301220802, -0.64278760968653936};
+};
+template <>
+struct OddTab<10> {
+  static constexpr double c[10] = {1, 0.80901699437494745, 0.30901699437494745, -0.30901699437494745, -0.80901699437494745, -1, -0.80901699437494745, -0.30901699437494745, 0.30901699437494745, 0.80901699437494745};
+  static constexpr double s[10] = {0, 0.58778525229247314, 0.95105651629515353, 0.95105651629515353, 0.58778525229247314, -3.8247850373932361e-40, -0.58778525229247314, -0.95105651629515353, -0.95105651629515353, -0.58778525229247314};
+};
+template <>
+struct OddTab<12> {
+  static constexpr double c[12] = {1, 0.8660254037844386, 0.5, -8.0778275495162712e-41, -0.5, -0.8660254037844386, -1, -0.8660254037844386, -0.5, -8.0778275495162712e-41, 0.5, 0.8660254037844386};
+  static constexpr double s[12] = {0, 0.5, 0.8660254037844386, 1, 0.8660254037844386, 0.5, -3.8247850373932361e-40, -0.5, -0.8660254037844386, -1, -0.8660254037844386, -0.5};
+};
+template <>
+struct OddTab<15> {
+  static constexpr double c[15] = {1, 0.91354545764260087, 0.66913060635885824, 0.30901699437494745, -0.10452846326765347, -0.5, -0.80901699437494745, -0.97814760073380569, -0.97814760073380569, -0.80901699437494745, -0.5, -0.10452846326765347, 0.30901699437494745, 0.66913060635885824, 0.91354545764260087};
+  static constexpr double s[15] = {0, 0.40673664307580021, 0.74314482547739424, 0.95105651629515353, 0.99452189536827329, 0.8660254037844386, 0.58778525229247314, 0.20791169081775934, -0.20791169081775934, -0.58778525229247314, -0.8660254037844386, -0.99452189536827329, -0.95105651629515353, -0.74314482547739424, -0.40673664307580021};
+};
+template <>
+struct OddTab<20> {
+  static constexpr double c[20] = {1, 0.95105651629515353, 0.80901699437494745, 0.58778525229247314, 0.30901699437494745, -8.0778275495162712e-41, -0.30901699437494745, -0.58778525229247314, -0.80901699437494745, -0.95105651629515353, -1, -0.95105651629515353, -0.80901699437494745, -0.58778525229247314, -0.30901699437494745, -8.0778275495162712e-41, 0.30901699437494745, 0.58778525229247314, 0.80901699437494745, 0.95105651629515353};
+  static constexpr double s[20] = {0, 0.30901699437494745, 0.58778525229247314, 0.80901699437494745, 0.95105651629515353, 1, 0.95105651629515353, 0.80901699437494745, 0.58778525229247314, 0.30901699437494745, -3.8247850373932361e-40, -0.30901699437494745, -0.58778525229247314, -0.80901699437494745, -0.95105651629515353, -1, -0.95105651629515353, -0.80901699437494745, -0.58778525229247314, -0.30901699437494745};
+};
+template <>
+struct OddTab<25> {
+  static constexpr double c[25] = {1, 0.96858316112863108, 0.87630668004386358, 0.72896862742141155, 0.53582679497899666, 0.30901699437494745, 0.062790519529313374, -0.18738131458572463, -0.42577929156507266, -0.63742398974868975, -0.80901699437494745, -0.92977648588825146, -0.99211470131447788, -0.99211470131447788, -0.92977648588825146, -0.80901699437494745, -0.63742398974868975, -0.42577929156507266, -0.18738131458572463, 0.062790519529313374, 0.30901699437494745, 0.53582679497899666, 0.72896862742141155, 0.87630668004386358, 0.96858316112863108};
+  static constexpr double s[25] = {0, 0.24868988716485479, 0.48175367410171527, 0.68454710592868873, 0.84432792550201508, 0.95105651629515353, 0.99802672842827156, 0.98228725072868872, 0.90482705246601958, 0.77051324277578925, 0.58778525229247314, 0.36812455268467797, 0.12533323356430426, -0.12533323356430426, -0.36812455268467797, -0.58778525229247314, -0.77051324277578925, -0.90482705246601958, -0.98228725072868872, -0.99802672842827156, -0.95105651629515353, -0.84432792550201508, -0.68454710592868873, -0.48175367410171527, -0.24868988716485479};
+};
+
 // Forward DFT of odd prime size R: with a_m = v_m + v_{R-m}, b_m = v_m - v_{R-m},
 // X_k = v_0 + sum_m cos(2 pi km/R) a_m - i sum_m sin(2 pi km/R) b_m and
 // X_{R-k} the same with +i (k, m = 1 .. (R-1)/2).
@@ -143,11 +179,85 @@ __device__ __forceinline__ void dft_odd(cd (&v)[R]) {
 }
 
 template <int R>
+__device__ __forceinline__ void dft_any(cd (&v)[R]);
+
+// Composite R = R1*R2 (n = R2*n1 + n2, k = k1 + R1*k2): R2 DFTs of size R1,
+// twiddles W_R^(n2*k1) as constants, then R1 DFTs of size R2.
+template <int R1, int R2>
+__device__ __forceinline__ void dft_split_gen(cd (&a)[R1 * R2]) {
+  constexpr int R = R1 * R2;
+  cd y[R2][R1];
+#pragma unroll
+  for (int n2 = 0; n2 < R2; ++n2) {
+    cd tmp[R1];
+#pragma unroll
+    for (int n1 = 0; n1 < R1; ++n1) tmp[n1] = a[R2 * n1 + n2];
+    dft_any<R1>(tmp);
+#pragma unroll
+    for (int k1 = 0; k1 < R1; ++k1) {
+      const int q = (n2 * k1) % R;
+      if (q == 0) {
+        y[n2][k1] = tmp[k1];
+      } else {  // x * (c - i s)
+        const double c = OddTab<R>::c[q], sn = OddTab<R>::s[q];
+        y[n2][k1] = {tmp[k1].x * c + tmp[k1].y * sn, tmp[k1].y * c - tmp[k1].x * sn};
+      }
+    }
+  }
+#pragma unroll
+  for (int k1 = 0; k1 < R1; ++k1) {
+    cd tmp[R2];
+#pragma unroll
+    for (int n2 = 0; n2 < R2; ++n2) tmp[n2] = y[n2][k1];
+    dft_any<R2>(tmp);
+#pragma unroll
+    for (int k2 = 0; k2 < R2; ++k2) a[k1 + R1 * k2] = tmp[k2];
+  }
+}
+
+template <int R>
 __device__ __forceinline__ void dft_any(cd (&v)[R]) {
   if constexpr ((R & (R - 1)) == 0) {
     Dft<R>::run(v);
-  } else {
+  } else if constexpr (R == 3 || R == 5 || R == 7 || R == 11 || R == 13) {
     dft_odd<R>(v);
+  } else if constexpr (R == 6 || R == 10) {
+    dft_split_gen<2, R / 2>(v);
+  } else if constexpr (R == 12 || R == 20) {
+    dft_split_gen<4, R / 4>(v);
+  } else if constexpr (R == 9 || R == 15) {
+    dft_split_gen<3, R / 3>(v);
+  } else {
+    static_assert(R == 25, "radix without a DFT");
+    dft_split_gen<5, 5>(v);
+  }
+}
+
+// LDS slot of element i: XOR-swizzled inside aligned groups of 8 slots, so
+// the stride-R ds_write_b128 of a first pass (8 lanes = 8 distinct bank
+// quads) and the unit-stride reads are both conflict-free. Transforms are
+// padded to a multiple of 8 slots.
+__device__ __forceinline__ int lsw(int i) { return i ^ ((i >> 3) & 7); }
+
+// v[r] *= W^r for r = 1..R-1 from the one table entry W (= W_{Ns*R}^k): two
+// interleaved power chains (odd powers step by W^2 from W, even ones by W^2
+// from W^2), depth about R/2.
+template <int R>
+__device__ __forceinline__ void twiddle_chain(cd (&v)[R], cd w) {
+  if constexpr (R > 1) {
+    const cd w2 = cmul(w, w);
+    cd wo = w, we = w2;
+    v[1] = cmul(v[1], wo);
+#pragma unroll
+    for (int r = 2; r < R; ++r) {
+      if (r & 1) {
+        wo = cmul(wo, w2);
+        v[r] = cmul(v[r], wo);
+      } else {
+        if (r > 2) we = cmul(we, w2);
+        v[r] = cmul(v[r], we);
+      }
+    }
   }
 }
 
@@ -176,7 +286,7 @@ __device__ __attribute__((noinline)) void mixed_pass(int n, int ns, int t1, int 
       for (int r = 0; r < R; ++r) {
         cd x;
         if constexpr (!FROM_HBM) {
-          x = lds[j + r * nb];
+          x = lds[lsw(j + r * nb)];
         } else if constexpr (LOAD == LOAD_REAL) {
           x = {reinterpret_cast<const double *>(gin)[j + r * nb], 0.0};
         } else {
@@ -196,9 +306,7 @@ __device__ __attribute__((noinline)) void mixed_pass(int n, int ns, int t1, int 
       int k = 0;
       if constexpr (!FROM_HBM) {
         k = j % ns;
-        const cd *w = tw + k * (R - 1);
-#pragma unroll
-        for (int r = 1; r < R; ++r) v[jj][r] = cmul(v[jj][r], w[r - 1]);
+        twiddle_chain<R>(v[jj], tw[k]);
       }
       dft_any<R>(v[jj]);
       const int o = (j - k) * R + k;
@@ -209,7 +317,7 @@ __device__ __attribute__((noinline)) void mixed_pass(int n, int ns, int t1, int 
           if constexpr (INV) y = {y.x * scale, -y.y * scale};
           gout[o + r * ns] = y;
         } else {
-          lds[o + r * ns] = v[jj][r];
+          lds[lsw(o + r * ns)] = v[jj][r];
         }
       }
     }
@@ -257,7 +365,7 @@ __global__ __launch_bounds__(512) void fft_mixed_kernel(const void *__restrict__
                         ? (const void *)(reinterpret_cast<const double *>(in) + row * n)
                         : (const void *)(reinterpret_cast<const cd *>(in) + row * n);
   cd *gout = out + row * n;
-  cd *lds = lds_mixed + (sub < d.tpw ? sub : 0) * n;
+  cd *lds = lds_mixed + (sub < d.tpw ? sub : 0) * ((n + 7) & ~7);
   const int np = d.npass;
   int R = (int)(d.codes & 31);
   if (np == 1) {
@@ -275,132 +383,220 @@ __global__ __launch_bounds__(512) void fft_mixed_kernel(const void *__restrict__
     else
       mixed_dispatch<INV, LOAD, MP_LAST>(R, n, ns, d.t1, tl, valid, gin, gout, lds, tw + twoff,
                                          scale);
-    twoff += ns * (R - 1);
+    twoff += ns;
     ns *= R;
   }
 }
 
 // ---------------------------------------------------------------------------
 // Compile-time specialisations for frequent lengths (BASELINE config 3 is
-// n = 3000): the same passes with n, Ns, the thread count and the twiddle
-// offsets known to the compiler, every pass inlined into one kernel.
-template <int R, bool INV, int LOAD, int MODE, int N, int NS, int T1>
-__device__ __forceinline__ void fixed_pass(int tl, bool valid, const void *__restrict__ gin,
-                                           cd *__restrict__ gout, cd *lds,
-                                           const cd *__restrict__ tw, double scale) {
-  constexpr bool FROM_HBM = MODE == MP_FIRST || MODE == MP_SINGLE;
-  constexpr bool TO_HBM = MODE == MP_LAST || MODE == MP_SINGLE;
-  constexpr int NB = N / R;
-  constexpr int J = (NB + T1 - 1) / T1;
+// n = 3000): n, Ns, the thread count and the twiddle offsets are known to the
+// compiler and every pass is inlined. Each pass is load -> twiddle + DFT ->
+// store; between passes the data crosses LDS either as complex128 (one
+// exchange, two barriers) or, with SPLIT, as real then imaginary halves
+// through an n-double buffer (half the LDS, so more workgroups per CU, for
+// four barriers).
+template <int R, int N, int NS, int T1>
+struct FPass {
+  static constexpr int NB = N / R;
+  static constexpr int J = (NB + T1 - 1) / T1;
+  static constexpr bool FULL = NB % T1 == 0;
   cd v[J][R];
+
+  __device__ __forceinline__ static bool act(int j, bool valid) {
+    return valid && (FULL || j < NB);
+  }
+  template <bool INV, int LOAD>
+  __device__ __forceinline__ void load_hbm(int tl, bool valid, const void *__restrict__ gin) {
 #pragma unroll
-  for (int jj = 0; jj < J; ++jj) {
-    const int j = tl + jj * T1;
-    if (valid && (NB % T1 == 0 || j < NB)) {
+    for (int jj = 0; jj < J; ++jj) {
+      const int j = tl + jj * T1;
+      if (act(j, valid)) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        cd x;
-        if constexpr (!FROM_HBM) {
-          x = lds[j + r * NB];
-        } else if constexpr (LOAD == LOAD_REAL) {
-          x = {reinterpret_cast<const double *>(gin)[j + r * NB], 0.0};
-        } else {
-          x = reinterpret_cast<const cd *>(gin)[j + r * NB];
-          if constexpr (INV) x.y = -x.y;
+        for (int r = 0; r < R; ++r) {
+          if constexpr (LOAD == LOAD_REAL) {
+            v[jj][r] = {reinterpret_cast<const double *>(gin)[j + r * NB], 0.0};
+          } else {
+            v[jj][r] = reinterpret_cast<const cd *>(gin)[j + r * NB];
+            if constexpr (INV) v[jj][r].y = -v[jj][r].y;
+          }
         }
-        v[jj][r] = x;
       }
     }
   }
-  if constexpr (MODE == MP_MID) __syncthreads();
+  // PART 0: real halves, 1: imaginary halves (double buffer), 2: complex
+  template <int PART, bool SWZ>
+  __device__ __forceinline__ void load_lds(int tl, bool valid, void *lds) {
 #pragma unroll
-  for (int jj = 0; jj < J; ++jj) {
-    const int j = tl + jj * T1;
-    if (valid && (NB % T1 == 0 || j < NB)) {
-      const int k = j % NS;
-      if constexpr (!FROM_HBM) {
-        const cd *w = tw + k * (R - 1);
+    for (int jj = 0; jj < J; ++jj) {
+      const int j = tl + jj * T1;
+      if (act(j, valid)) {
 #pragma unroll
-        for (int r = 1; r < R; ++r) v[jj][r] = cmul(v[jj][r], w[r - 1]);
+        for (int r = 0; r < R; ++r) {
+          const int i = SWZ ? lsw(j + r * NB) : j + r * NB;
+          if constexpr (PART == 2) {
+            v[jj][r] = reinterpret_cast<const cd *>(lds)[i];
+          } else if constexpr (PART == 0) {
+            v[jj][r].x = reinterpret_cast<const double *>(lds)[i];
+          } else {
+            v[jj][r].y = reinterpret_cast<const double *>(lds)[i];
+          }
+        }
       }
-      dft_any<R>(v[jj]);
-      const int o = (j - k) * R + k;
+    }
+  }
+  __device__ __forceinline__ void compute(int tl, bool valid, const cd *__restrict__ tw) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        if constexpr (TO_HBM) {
+    for (int jj = 0; jj < J; ++jj) {
+      const int j = tl + jj * T1;
+      if (act(j, valid)) {
+        if constexpr (NS > 1) twiddle_chain<R>(v[jj], tw[j % NS]);
+        dft_any<R>(v[jj]);
+      }
+    }
+  }
+  template <int PART, bool SWZ>
+  __device__ __forceinline__ void store_lds(int tl, bool valid, void *lds) const {
+#pragma unroll
+    for (int jj = 0; jj < J; ++jj) {
+      const int j = tl + jj * T1;
+      if (act(j, valid)) {
+        const int k = j % NS, o = (j - k) * R + k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int i = SWZ ? lsw(o + r * NS) : o + r * NS;
+          if constexpr (PART == 2) {
+            reinterpret_cast<cd *>(lds)[i] = v[jj][r];
+          } else if constexpr (PART == 0) {
+            reinterpret_cast<double *>(lds)[i] = v[jj][r].x;
+          } else {
+            reinterpret_cast<double *>(lds)[i] = v[jj][r].y;
+          }
+        }
+      }
+    }
+  }
+  template <bool INV>
+  __device__ __forceinline__ void store_hbm(int tl, bool valid, cd *__restrict__ gout,
+                                            double scale) const {
+#pragma unroll
+    for (int jj = 0; jj < J; ++jj) {
+      const int j = tl + jj * T1;
+      if (act(j, valid)) {
+        const int k = j % NS, o = (j - k) * R + k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
           cd y = v[jj][r];
           if constexpr (INV) y = {y.x * scale, -y.y * scale};
           gout[o + r * NS] = y;
-        } else {
-          lds[o + r * NS] = v[jj][r];
         }
       }
     }
   }
-}
+};
 
-template <bool INV, int LOAD, int N, int T1, int NS, int TWOFF, int P, int NP, int R,
+// exchange prev -> pass (R, NS) through LDS, compute it, then continue
+template <bool INV, bool SPLIT, bool SWZ, int N, int T1, int NS, int TWOFF, class Prev, int R,
           int... REST>
-__device__ __forceinline__ void fixed_passes(int tl, bool valid, const void *gin, cd *gout,
-                                             cd *lds, const cd *tw, double scale) {
-  constexpr int MODE = NP == 1 ? MP_SINGLE : P == 0 ? MP_FIRST : P == NP - 1 ? MP_LAST : MP_MID;
-  if constexpr (P > 0) __syncthreads();
-  fixed_pass<R, INV, LOAD, MODE, N, NS, T1>(tl, valid, gin, gout, lds, tw + TWOFF, scale);
-  if constexpr (sizeof...(REST) > 0)
-    fixed_passes<INV, LOAD, N, T1, NS * R, (P == 0 ? 0 : TWOFF + NS * (R - 1)), P + 1, NP,
-                 REST...>(tl, valid, gin, gout, lds, tw, scale);
+__device__ __forceinline__ void fixed_chain(const Prev &prev, int tl, bool valid, cd *gout,
+                                            void *lds, const cd *tw, double scale) {
+  FPass<R, N, NS, T1> cur;
+  if constexpr (SPLIT) {
+    prev.template store_lds<0, SWZ>(tl, valid, lds);
+    __syncthreads();
+    cur.template load_lds<0, SWZ>(tl, valid, lds);
+    __syncthreads();
+    prev.template store_lds<1, SWZ>(tl, valid, lds);
+    __syncthreads();
+    cur.template load_lds<1, SWZ>(tl, valid, lds);
+  } else {
+    prev.template store_lds<2, SWZ>(tl, valid, lds);
+    __syncthreads();
+    cur.template load_lds<2, SWZ>(tl, valid, lds);
+  }
+  cur.compute(tl, valid, tw + TWOFF);
+  if constexpr (sizeof...(REST) == 0) {
+    cur.template store_hbm<INV>(tl, valid, gout, scale);
+  } else {
+    __syncthreads();  // every read of this exchange lands before the next one's writes
+    fixed_chain<INV, SPLIT, SWZ, N, T1, NS * R, TWOFF + NS, FPass<R, N, NS, T1>, REST...>(
+        cur, tl, valid, gout, lds, tw, scale);
+  }
 }
 
-template <int... RS>
+template <int R0, int... RS>
 struct FixedGeo {
-  static constexpr int N = (RS * ...);
-  static constexpr int NP = sizeof...(RS);
+  static constexpr int N = R0 * (RS * ... * 1);
   static constexpr int need() {
     int m = 1;
-    for (int r : {RS...}) {
-      const int nb = N / r, jm = 16 / r, q = (nb + jm - 1) / jm;
+    for (int r : {R0, RS...}) {
+      const int nb = N / r, jm = r > 16 ? 1 : 16 / r, q = (nb + jm - 1) / jm;
       m = q > m ? q : m;
     }
     return m;
   }
-  static constexpr int T1 = (need() + 63) / 64 * 64;
+  static constexpr int T1 = need();
 };
 
-template <bool INV, int LOAD, int... RS>
-__global__ __launch_bounds__(FixedGeo<RS...>::T1) void fft_mixed_fixed_kernel(
+template <bool INV, int LOAD, bool SPLIT, bool SWZ, int R0, int... RS>
+__global__ __launch_bounds__((FixedGeo<R0, RS...>::T1)) void fft_mixed_fixed_kernel(
     const void *__restrict__ in, cd *__restrict__ out, int64_t batch, const cd *__restrict__ tw,
     double scale) {
-  using G = FixedGeo<RS...>;
-  __shared__ cd lds[G::N];
+  using G = FixedGeo<R0, RS...>;
+  constexpr int SLOTS = (G::N + 7) & ~7;
+  __shared__ double lds[SPLIT ? SLOTS : 2 * SLOTS];
   const int tl = threadIdx.x;
   const int64_t row = xcd_remap(blockIdx.x, gridDim.x);
   const bool valid = row < batch;
   const void *gin = LOAD == LOAD_REAL
                         ? (const void *)(reinterpret_cast<const double *>(in) + row * G::N)
                         : (const void *)(reinterpret_cast<const cd *>(in) + row * G::N);
-  fixed_passes<INV, LOAD, G::N, G::T1, 1, 0, 0, G::NP, RS...>(tl, valid, gin, out + row * G::N,
-                                                              lds, tw, scale);
+  FPass<R0, G::N, 1, G::T1> p0;
+  p0.template load_hbm<INV, LOAD>(tl, valid, gin);
+  p0.compute(tl, valid, tw);
+  if constexpr (sizeof...(RS) == 0)
+    p0.template store_hbm<INV>(tl, valid, out + row * G::N, scale);
+  else
+    fixed_chain<INV, SPLIT, SWZ, G::N, G::T1, R0, 0, FPass<R0, G::N, 1, G::T1>, RS...>(
+        p0, tl, valid, out + row * G::N, lds, tw, scale);
 }
 
-template <int... RS>
+template <bool SPLIT, bool SWZ, int... RS>
 static bool launch_fixed(const MixedDesc &d, bool inv, int load, const void *in, cd *out,
                          int64_t batch, const cd *tw, double scale, hipStream_t s) {
   using G = FixedGeo<RS...>;
   uint64_t codes = 0;
   int q = 0;
   for (int r : {RS...}) codes |= (uint64_t)r << (5 * q++);
-  if (d.n != G::N || d.codes != codes || G::N * sizeof(cd) > 65536) return false;
+  if (d.n != G::N || d.codes != codes) return false;
   const dim3 grid((unsigned)batch), block(G::T1);
   if (inv)
-    hipLaunchKernelGGL((fft_mixed_fixed_kernel<true, LOAD_COMPLEX, RS...>), grid, block, 0, s,
-                       in, out, batch, tw, scale);
+    hipLaunchKernelGGL((fft_mixed_fixed_kernel<true, LOAD_COMPLEX, SPLIT, SWZ, RS...>), grid,
+                       block, 0, s, in, out, batch, tw, scale);
   else if (load == LOAD_REAL)
-    hipLaunchKernelGGL((fft_mixed_fixed_kernel<false, LOAD_REAL, RS...>), grid, block, 0, s, in,
-                       out, batch, tw, scale);
+    hipLaunchKernelGGL((fft_mixed_fixed_kernel<false, LOAD_REAL, SPLIT, SWZ, RS...>), grid,
+                       block, 0, s, in, out, batch, tw, scale);
   else
-    hipLaunchKernelGGL((fft_mixed_fixed_kernel<false, LOAD_COMPLEX, RS...>), grid, block, 0, s,
-                       in, out, batch, tw, scale);
+    hipLaunchKernelGGL((fft_mixed_fixed_kernel<false, LOAD_COMPLEX, SPLIT, SWZ, RS...>), grid,
+                       block, 0, s, in, out, batch, tw, scale);
   return true;
+}
+
+// Radix lists of the compiled specialisations (launch_fft_mixed picks the
+// kernel by matching n and the list). GDSP_MIXED_GENERIC=1 disables them.
+bool mixed_fixed_radices(int n, int *rad, int *npass) {
+  if (getenv("GDSP_MIXED_GENERIC")) return false;
+  // n = 3000: measured 1.10 ms per 65536 transforms for 25*15*8 against
+  // 1.14-1.18 ms for the other orders of these radices, and 1.82 ms for the
+  // generic 8*5*5*5*3 kernel; the split (re/im) exchange measured 3-4 % slower
+  if (n == 3000) {
+    rad[0] = 25;
+    rad[1] = 15;
+    rad[2] = 8;
+    *npass = 3;
+    return true;
+  }
+  return false;
 }
 
 hipError_t launch_fft_mixed(const MixedDesc &d, bool inv, int load, const void *in, cd *out,
@@ -409,10 +605,11 @@ hipError_t launch_fft_mixed(const MixedDesc &d, bool inv, int load, const void *
   if (d.t1 <= 0 || d.tpw <= 0 || d.t1 * d.tpw > 512) return hipErrorInvalidValue;
   const int64_t nblk = (batch + d.tpw - 1) / d.tpw;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-  if (batch <= 0x7fffffff && !getenv("GDSP_MIXED_GENERIC") &&
-      launch_fixed<8, 5, 5, 5, 3>(d, inv, load, in, out, batch, tw, scale, s))
+  // odd first radix: its stride-25 LDS writes are conflict-free unswizzled
+  if (batch <= 0x7fffffff &&
+      launch_fixed<false, false, 25, 15, 8>(d, inv, load, in, out, batch, tw, scale, s))
     return hipGetLastError();
-  const size_t lds = (size_t)d.tpw * (size_t)d.n * sizeof(cd);
+  const size_t lds = (size_t)d.tpw * (size_t)((d.n + 7) & ~7) * sizeof(cd);
   const dim3 grid((unsigned)nblk), block((unsigned)(d.t1 * d.tpw));
   if (inv) {
     hipLaunchKernelGGL((fft_mixed_kernel<true, LOAD_COMPLEX>), grid, block, lds, s, in, out,

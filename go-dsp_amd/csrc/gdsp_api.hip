@@ -283,6 +283,11 @@ bool mixed_radices(int64_t n, std::vector<int> &rad) {
       odd.push_back(q);
     }
   if (m != 1) return false;
+  int fr[16], fnp = 0;
+  if (gdsp::mixed_fixed_radices((int)n, fr, &fnp)) {
+    rad.assign(fr, fr + fnp);
+    return true;
+  }
   while (a >= 4) {
     rad.push_back(16);
     a -= 4;
@@ -301,7 +306,7 @@ int build_mixed(int dev, int64_t n, const std::vector<int> &rad, gdsp_plan *p) {
   int need = 1;
   for (size_t q = 0; q < rad.size(); ++q) {
     d.codes |= (uint64_t)rad[q] << (5 * q);
-    const int jmax = 16 / rad[q], nb = (int)n / rad[q];
+    const int jmax = rad[q] > 16 ? 1 : 16 / rad[q], nb = (int)n / rad[q];
     need = std::max(need, (nb + jmax - 1) / jmax);
   }
   int t1 = 1;
@@ -310,17 +315,17 @@ int build_mixed(int dev, int64_t n, const std::vector<int> &rad, gdsp_plan *p) {
   if (t1 > 512) return fail(GDSP_ERR_UNSUPPORTED, "mixed-radix geometry");
   d.t1 = t1;
   d.tpw = std::max(1, std::min(256 / t1, gdsp::kMixedMax / (int)n));
-  // per-pass twiddles W_{Ns*R}^{k*r}, k < Ns, r = 1..R-1, butterfly-major
+  // per-pass twiddle bases W_{Ns*R}^k, k < Ns (the kernels raise them to
+  // the powers r = 1..R-1 in registers)
   std::vector<cd> h;
   int64_t ns = rad[0];
   for (size_t q = 1; q < rad.size(); ++q) {
     const int R = rad[q];
-    for (int64_t k = 0; k < ns; ++k)
-      for (int r = 1; r < R; ++r) {
-        const long double ang = -2.0L * 3.141592653589793238462643383279502884L *
-                                (long double)(k * r) / (long double)(ns * R);
-        h.push_back({(double)cosl(ang), (double)sinl(ang)});
-      }
+    for (int64_t k = 0; k < ns; ++k) {
+      const long double ang = -2.0L * 3.141592653589793238462643383279502884L * (long double)k /
+                              (long double)(ns * R);
+      h.push_back({(double)cosl(ang), (double)sinl(ang)});
+    }
     ns *= R;
   }
   if (h.empty()) h.push_back({1.0, 0.0});

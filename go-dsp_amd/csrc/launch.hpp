@@ -23,6 +23,8 @@ struct MixedDesc {
   int n, npass, t1, tpw;
 };
 constexpr int kMixedMax = 4096;
+// radix list of a compiled specialisation for n (false: use the generic list)
+bool mixed_fixed_radices(int n, int *rad, int *npass);
 hipError_t launch_fft_mixed(const MixedDesc &d, bool inv, int load, const void *in, cd *out,
                             int64_t batch, const cd *tw, double scale, hipStream_t s);
 hipError_t launch_bluestein(int log2m, bool inv, const cd *in, cd *out, int64_t n,

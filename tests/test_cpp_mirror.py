@@ -82,3 +82,31 @@ print("ok")
     env = dict(os.environ, GDSP_NO_TORCH_PRELOAD="1", REPO=REPO)
     r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_mixed_generic_kernel_for_specialised_lengths():
+    """GDSP_MIXED_GENERIC=1 routes lengths that have a compiled
+    specialisation (n = 3000) through the generic mixed-radix kernel: both
+    kernels must agree with the oracle (the bench times the specialisation)."""
+    code = r'''
+import importlib, os, sys
+sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
+import numpy as np, oracle
+g = importlib.import_module("go-dsp_amd")
+D = importlib.import_module("go-dsp_amd.device")
+import torch
+assert D.plan(3000).kind == 5
+rng = np.random.default_rng(3)
+for n in (3000, 1000, 12):
+    x = rng.standard_normal((9, n)) + 1j * rng.standard_normal((9, n))
+    for inv in (False, True):
+        y = g.fft.FFTBatch(x, inverse=inv)
+        ref = oracle.ifft_rows(x) if inv else oracle.fft_rows(x)
+        err = max(np.linalg.norm(a - b) / np.linalg.norm(b) for a, b in zip(y, ref))
+        assert err < 1e-9, (n, inv, err)
+print("ok")
+'''
+    env = dict(os.environ, GDSP_MIXED_GENERIC="1", REPO=REPO)
+    r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
