@@ -101,7 +101,7 @@ def main():
                "n": n, "batch_per_gpu": batch, "parallelism": f"shard{world}",
                "algorithm": algo}
         kernel = {1: "fft_lds_kernel<12>", 3: "bluestein_kernel<13>",
-                  5: "fft_mixed_kernel"}.get(kind, str(kind))
+                  5: "fft_mixed_fixed_kernel<25,15,8>"}.get(kind, str(kind))
         metric = "Gsamples/s + % HBM roofline, batched N=4096 complex128 FFT at 1/2/4/8 GPUs"
     elif w == "fft2_8192":
         rows = cols = 8192

@@ -16,13 +16,17 @@
 #include "fft_device.hpp"
 #include "launch.hpp"
 
+#include <stdlib.h>
+
 namespace gdsp {
 
 // ----------------------------------------------------------------------------
 // One-kernel transform: each workgroup owns TPW whole transforms in registers
 // (16 complex128 per thread) and LDS (exchange between radix-16 passes).
+// N >= 8192: 512+ threads per transform, so <= 128 VGPRs is what lets two
+// workgroups share a CU (measured 1.27 -> 1.21 ms on the FFT2 8192^2 step).
 template <int LOG2N, bool INV, int LOAD, bool SPLIT>
-__global__ __launch_bounds__(Geo<LOG2N>::WG) void fft_lds_kernel(
+__global__ __launch_bounds__(Geo<LOG2N>::WG, (LOG2N >= 13 ? 4 : 1)) void fft_lds_kernel(
     const void *__restrict__ in, cd *__restrict__ out, int64_t batch,
     const cd *__restrict__ tw, double scale) {
   using G = Geo<LOG2N>;
@@ -224,11 +228,14 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_kernel(
 // the window stays in registers.
 // WMODE: where the window lives — 0 registers, 1 re-read from global (L1/L2)
 // every iteration, 2 an LDS table shared by the workgroup.
-template <int LOG2F, int WMODE = 2, int MINW = 1>
-__global__ __launch_bounds__(Geo<LOG2F>::WG, MINW) void pwelch_half_kernel(
+// Measured at F = 4096 (2^30 samples): E = 16 with the LDS window 3.19 ms;
+// E = 8 (LOG2E = 3: 104 VGPRs, twice the waves, one more exchange) 3.67 ms;
+// E = 16 forced to 168 / 128 VGPRs (MINW 3 / 4) spills: 4.85 / 6.07 ms.
+template <int LOG2F, int WMODE = 2, int MINW = 1, int LOG2E = 4>
+__global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_kernel(
     const double *__restrict__ x, int64_t seg_begin, int64_t seg_end, int64_t pairs_per_worker,
     const double *__restrict__ win, const cd *__restrict__ tw, double *__restrict__ partial) {
-  using G = Geo<LOG2F>;
+  using G = Geo<LOG2F, LOG2E>;
   constexpr int E = G::E, H = E / 2;
   constexpr int64_t STRIDE = G::N / 2;
   __shared__ double lds[G::LDS_DOUBLES + (WMODE == 2 ? G::N : 0)];
@@ -291,7 +298,7 @@ __global__ __launch_bounds__(Geo<LOG2F>::WG, MINW) void pwelch_half_kernel(
     }
 #pragma unroll
     for (int k = 0; k < H; ++k) carry[k] = c2[k];
-    fft_regs<LOG2F, true, true>(v, opaque_int(t), tw, lre, lre, it == 0);
+    fft_regs<LOG2F, true, true, LOG2E>(v, opaque_int(t), tw, lre, lre, it == 0);
     if (active) {
 #pragma unroll
       for (int k = 0; k < E; ++k) acc[k] += v[k].x * v[k].x + v[k].y * v[k].y;
@@ -644,13 +651,14 @@ static hipError_t launch_pw_t(const double *x, int64_t nfft, int64_t stride, int
   return hipGetLastError();
 }
 
-template <int LOG2F, int WMODE = 2, int MINW = 1>
+template <int LOG2F, int WMODE = 2, int MINW = 1, int LOG2E = 4>
 static hipError_t launch_pwh_t(const double *x, int64_t seg_begin, int64_t seg_end, int64_t ppw,
                                int64_t nworkers, const double *win, const cd *tw, double *partial,
                                hipStream_t s) {
-  using G = Geo<LOG2F>;
+  using G = Geo<LOG2F, LOG2E>;
+  if (G::TPW != Geo<LOG2F>::TPW) return hipErrorInvalidValue;  // workers per block
   const int64_t nblk = (nworkers + G::TPW - 1) / G::TPW;
-  hipLaunchKernelGGL((pwelch_half_kernel<LOG2F, WMODE, MINW>), dim3((unsigned)nblk), dim3(G::WG), 0, s,
+  hipLaunchKernelGGL((pwelch_half_kernel<LOG2F, WMODE, MINW, LOG2E>), dim3((unsigned)nblk), dim3(G::WG), 0, s,
                      x, seg_begin, seg_end, ppw, win, tw, partial);
   return hipGetLastError();
 }
@@ -662,7 +670,8 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
 #define GDSP_PWH(L) \
   case L: return launch_pwh_t<L>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
     GDSP_PWH(5) GDSP_PWH(6) GDSP_PWH(7) GDSP_PWH(8) GDSP_PWH(9) GDSP_PWH(10) GDSP_PWH(11)
-    GDSP_PWH(12) GDSP_PWH(13)
+    GDSP_PWH(12)
+    GDSP_PWH(13)
 #undef GDSP_PWH
     // F = 16384: the exchange buffer alone takes 136 KiB, so the window is
     // re-read from L1/L2 instead of living in LDS

@@ -12,21 +12,28 @@ import statistics
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"radix4096": "fft_lds_kernel<12", "bluestein3000": "fft_mixed_kernel",
+KERNELS = {"radix4096": "fft_lds_kernel<12", "bluestein3000": "fft_mixed_fixed_kernel",
            "chirpz3000": "bluestein_kernel<13",
-           "pwelch": "pwelch_half_kernel<12", "fft2_8192": "fft_lds_kernel<13"}
+           "pwelch": "pwelch_half_kernel<12",
+           # one FFT2 step = row pass + the two column-tile launches: summed
+           "fft2_8192": ["fft_lds_kernel<13", "colfft_tile_kernel<7", "colfft_tile_kernel<6"]}
 
 
-def values(w, counter):
+def values(w, counter, kernel):
     path = os.path.join(REPO, "gpurun_out", f"pmc_{w}_{counter}", "run_counter_collection.csv")
-    rows = [r for r in csv.DictReader(open(path)) if KERNELS[w] in r["Kernel_Name"]]
+    rows = [r for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
     return [float(r["Counter_Value"]) for r in rows], path
 
 
 def main(w, tag):
-    fetch, pf = values(w, "FETCH_SIZE")
-    write, pw = values(w, "WRITE_SIZE")
-    f_kib, w_kib = statistics.median(fetch), statistics.median(write)
+    ks = KERNELS[w] if isinstance(KERNELS[w], list) else [KERNELS[w]]
+    f_kib = w_kib = 0.0
+    fetch = write = []
+    for k in ks:
+        fetch, pf = values(w, "FETCH_SIZE", k)
+        write, pw = values(w, "WRITE_SIZE", k)
+        f_kib += statistics.median(fetch)
+        w_kib += statistics.median(write)
     out = {
         "workload": w, "kernel": KERNELS[w], "launches": [len(fetch), len(write)],
         "fetch_size_kib": f_kib, "write_size_kib": w_kib,
