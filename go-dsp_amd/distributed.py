@@ -71,6 +71,23 @@ def gpu_accumulate(x_local, shard: PwelchShard, win_seg, acc, stream=None):
     return acc
 
 
+_win_dev: dict = {}
+
+
+def _device_window(wf, flen: int, dev, torch):
+    """wf(flen) as a float64 tensor on dev, uploaded once per (window, length,
+    device): the window functions are pure, and a per-call pageable upload
+    is a synchronous host copy inside every Pwelch step."""
+    key = (wf, int(flen), str(dev))
+    t = _win_dev.get(key)
+    if t is None:
+        if len(_win_dev) >= 32:  # e.g. a fresh lambda per call: keep it bounded
+            _win_dev.clear()
+        t = torch.as_tensor(np.ascontiguousarray(wf(flen)), dtype=torch.float64, device=dev)
+        _win_dev[key] = t
+    return t
+
+
 def pwelch(x_local, Fs: float, o: spectral.PwelchOptions, shard: PwelchShard, group=None,
            accumulate: Optional[Callable] = None, stream=None):
     """Sharded spectral.Pwelch. x_local: this rank's samples
@@ -88,8 +105,7 @@ def pwelch(x_local, Fs: float, o: spectral.PwelchOptions, shard: PwelchShard, gr
     # on the same stream as the library's kernels
     ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
     with ctx:
-        win_seg = torch.as_tensor(np.ascontiguousarray(wf(flen)), dtype=torch.float64,
-                                  device=dev)
+        win_seg = _device_window(wf, flen, dev, torch)
         acc = torch.zeros(flen, dtype=torch.float64, device=dev)
         if shard.seg_hi > shard.seg_lo:
             (accumulate or gpu_accumulate)(x_local, shard, win_seg, acc, stream)
