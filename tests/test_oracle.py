@@ -42,6 +42,21 @@ def test_fft2_reference_vectors(oracle, refvec):
         assert all(close_c(a, b) for a, b in zip(yi, x))
 
 
+def test_fftn_reference_vectors(oracle, refvec):
+    # fft/fft_test.go:225-239 (TestFFTN): FFTN(in) ~ out, IFFTN(out) ~ in
+    assert refvec["fftnTests"]
+    for case in refvec["fftnTests"]:
+        x = np.asarray(case["in"], np.float64).astype(np.complex128)
+        out = cpx(case["out"])
+        assert close_c(oracle.fftn(x, case["dim"]), out), case["dim"]
+        assert close_c(oracle.fftn(out, case["dim"], inverse=True), x), case["dim"]
+    # and against numpy's N-D transform on a seeded ragged shape
+    rng = np.random.default_rng(5)
+    z = rng.standard_normal((3, 5, 7)) + 1j * rng.standard_normal((3, 5, 7))
+    ref = np.fft.fftn(z).ravel()
+    assert np.linalg.norm(oracle.fftn(z, [3, 5, 7]) - ref) / np.linalg.norm(ref) < 1e-12
+
+
 def test_reverse_bits(oracle, refvec):
     # fft/fft_test.go:241-249
     for c in refvec["reverseBitsTests"]:
