@@ -64,6 +64,8 @@ SIGNATURES = {
     "gdsp_fft2_device": (_I, [_P, _P, _I64, _I64, _I, _P, _P]),
     "gdsp_pwelch_accumulate_device": (_I, [_P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P]),
     "gdsp_pwelch_finalize": (_I, [_P, _I64, _I64, _I64, _I64, _P, _D, _I, _P, _P]),
+    "gdsp_wav_read_floats": (_I, [_P, _I64, _I, _I, _P, _I]),
+    "gdsp_wav_read_floats_device": (_I, [_P, _I64, _I, _I, _P, _I, _P]),
     "gdsp_fill_uniform_device": (_I, [_P, _I64, _U64, _U64, _P]),
 }
 

@@ -26,7 +26,7 @@ namespace gdsp {
 // N >= 8192: 512+ threads per transform, so <= 128 VGPRs is what lets two
 // workgroups share a CU (measured 1.27 -> 1.21 ms on the FFT2 8192^2 step).
 template <int LOG2N, bool INV, int LOAD, bool SPLIT>
-__global__ __launch_bounds__(Geo<LOG2N>::WG, (LOG2N >= 13 ? 4 : 1)) void fft_lds_kernel(
+__global__ __launch_bounds__(Geo<LOG2N>::WG, (LOG2N >= 13 && SPLIT ? 4 : 1)) void fft_lds_kernel(
     const void *__restrict__ in, cd *__restrict__ out, int64_t batch,
     const cd *__restrict__ tw, double scale) {
   using G = Geo<LOG2N>;

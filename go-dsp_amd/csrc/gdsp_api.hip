@@ -1055,6 +1055,52 @@ int gdsp_pwelch(const double *x, int64_t n, double fs, int64_t nfft, int64_t pad
   return GDSP_OK;
 }
 
+static bool wav_format_ok(int audio_format, int bits) {
+  return (audio_format == 1 && (bits == 8 || bits == 16)) || audio_format == 3;
+}
+
+static int64_t wav_sample_bytes(int audio_format, int bits) {
+  return audio_format == 3 ? 4 : bits / 8;
+}
+
+int gdsp_wav_read_floats_device(const void *d_in, int64_t count, int audio_format,
+                                int bits_per_sample, void *d_out, int out_f64, void *stream) {
+  if (count < 0 || (count && (!d_in || !d_out))) return fail(GDSP_ERR_INVALID, "bad argument");
+  if (!wav_format_ok(audio_format, bits_per_sample))
+    return fail(GDSP_ERR_UNSUPPORTED, audio_format == 1 ? "wav: unknown bits per sample"
+                                                        : "wav: unknown audio format");
+  if (count == 0) return GDSP_OK;
+  int dev = 0;
+  STCHK(current_device(&dev));
+  HIPCHK(gdsp::launch_wav_decode(d_in, count, audio_format, bits_per_sample, d_out, out_f64 != 0,
+                                 (hipStream_t)stream));
+  return GDSP_OK;
+}
+
+int gdsp_wav_read_floats(const void *in, int64_t count, int audio_format, int bits_per_sample,
+                         void *out, int out_f64) {
+  if (count < 0 || (count && (!in || !out))) return fail(GDSP_ERR_INVALID, "bad argument");
+  if (!wav_format_ok(audio_format, bits_per_sample))
+    return fail(GDSP_ERR_UNSUPPORTED, audio_format == 1 ? "wav: unknown bits per sample"
+                                                        : "wav: unknown audio format");
+  if (count == 0) return GDSP_OK;
+  int dev = 0;
+  STCHK(current_device(&dev));
+  hipStream_t s = thread_stream(dev);
+  if (!s) return fail(GDSP_ERR_HIP, "stream creation failed");
+  const size_t in_bytes = (size_t)count * (size_t)wav_sample_bytes(audio_format, bits_per_sample);
+  const size_t out_bytes = (size_t)count * (out_f64 ? 8 : 4);
+  DevBuf din, dout;
+  STCHK(din.alloc(in_bytes, s, SLOT_IN));
+  STCHK(dout.alloc(out_bytes, s, SLOT_OUT));
+  STCHK(copy_h2d(din.p, in, in_bytes, s));
+  HIPCHK(gdsp::launch_wav_decode(din.p, count, audio_format, bits_per_sample, dout.p,
+                                 out_f64 != 0, s));
+  STCHK(copy_d2h(out, dout.p, out_bytes, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return GDSP_OK;
+}
+
 int gdsp_fill_uniform_device(double *d_out, int64_t count, uint64_t seed, uint64_t offset,
                              void *stream) {
   if (count < 0 || (!d_out && count)) return fail(GDSP_ERR_INVALID, "bad argument");

@@ -68,6 +68,9 @@ hipError_t launch_chirp_postmul(const cd *a, cd *out, int64_t n, int64_t m, int6
                                 const cd *chirp, bool inv, double scale, hipStream_t s);
 hipError_t launch_pointwise_mul(const cd *a, const cd *b, cd *out, int64_t count, hipStream_t s);
 hipError_t launch_scale(cd *a, int64_t count, double sc, hipStream_t s);
+// wav.ReadFloats conversion (wav.hip): audio_format 1 (bits 8 / 16) or 3
+hipError_t launch_wav_decode(const void *in, int64_t count, int audio_format, int bits,
+                             void *out, bool f64, hipStream_t s);
 hipError_t launch_fill_uniform(double *out, int64_t count, uint64_t seed, uint64_t offset,
                                hipStream_t s);
 

@@ -134,6 +134,19 @@ int gdsp_pwelch(const double *x, int64_t n, double fs, int64_t nfft, int64_t pad
  * shim for the default window (L float64 written to out). */
 int gdsp_window_hann(int64_t L, double *out);
 
+/* ---- wav package (the wav -> Pwelch feeder) -------------------------------- */
+
+/* wav.(*Wav).ReadFloats — wav/wav.go:135-161 — on the GPU: converts `count`
+ * little-endian samples of a WAV data chunk (what ReadSamples reads,
+ * wav.go:110-131) with the reference's float32 formulas. audio_format 1 with
+ * bits_per_sample 8 or 16 (PCM) or 3 (IEEE float32); anything else →
+ * GDSP_ERR_UNSUPPORTED ("wav: unknown bits per sample" / "unknown audio
+ * format" in the reference). out_f64 = 0 writes float32 (the reference's
+ * []float32), 1 writes float64 (the float32 values widened: a Pwelch input).
+ * Host-pointer form: in/out on the host, synchronous. */
+int gdsp_wav_read_floats(const void *in, int64_t count, int audio_format, int bits_per_sample,
+                         void *out, int out_f64);
+
 /* ---- device-pointer API (stream-ordered; multi-GPU building blocks) ---------- */
 
 typedef struct gdsp_plan gdsp_plan;
@@ -186,6 +199,12 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
 int gdsp_pwelch_finalize(const double *acc, int64_t flen, int64_t nsegs, int64_t nfft,
                          int64_t pad, const double *win_nfft, double fs, int scale_off,
                          double *pxx, double *freqs);
+
+/* gdsp_wav_read_floats on device buffers (d_in: the raw data-chunk bytes at
+ * any alignment; d_out: count float32 or float64), stream-ordered: decode a
+ * WAV stream straight into the HBM-resident Pwelch input. */
+int gdsp_wav_read_floats_device(const void *d_in, int64_t count, int audio_format,
+                                int bits_per_sample, void *d_out, int out_f64, void *stream);
 
 /* Device synthetic input: d_out[i] = uniform[-1,1) from splitmix64(seed,
  * offset + i), i < count (float64). Identical to the host generator the tests

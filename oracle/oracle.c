@@ -731,3 +731,40 @@ void or_fill_uniform(double *out, int64_t count, uint64_t seed, uint64_t offset)
     out[i] = (double)(z >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0;
   }
 }
+
+/* wav/wav.go:135-161 (ReadFloats) over the bytes ReadSamples (:110-131) reads
+ * with binary.LittleEndian. Go evaluates float32(v) - math.MinInt16 and the
+ * division in float32 (the untyped constants convert to float32). */
+int or_wav_floats(const void *in, int64_t count, int audio_format, int bits_per_sample,
+                  float *out) {
+  const unsigned char *b = (const unsigned char *)in;
+  if (audio_format == 1) {
+    if (bits_per_sample == 8) {
+      for (int64_t i = 0; i < count; i++) {
+        volatile float v = (float)b[i];
+        out[i] = v / 255.0f;
+      }
+      return 0;
+    }
+    if (bits_per_sample == 16) {
+      for (int64_t i = 0; i < count; i++) {
+        const int16_t s = (int16_t)((uint16_t)b[2 * i] | ((uint16_t)b[2 * i + 1] << 8));
+        volatile float num = (float)s - (-32768.0f);
+        out[i] = num / 65535.0f;
+      }
+      return 0;
+    }
+    return -1;
+  }
+  if (audio_format == 3) {
+    for (int64_t i = 0; i < count; i++) {
+      uint32_t u = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) |
+                   ((uint32_t)b[4 * i + 2] << 16) | ((uint32_t)b[4 * i + 3] << 24);
+      float f;
+      memcpy(&f, &u, 4);
+      out[i] = f;
+    }
+    return 0;
+  }
+  return -1;
+}

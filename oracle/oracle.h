@@ -97,6 +97,14 @@ int or_pwelch_threaded(const double *x, int64_t n, double fs, int64_t nfft, int6
  * (splitmix64; see DESIGN.md §Synthetic data): uniform [-1, 1). */
 void or_fill_uniform(double *out, int64_t count, uint64_t seed, uint64_t offset);
 
+/* wav.(*Wav).ReadFloats's conversion, wav/wav.go:135-161, of `count`
+ * little-endian samples in `in` (ReadSamples, wav.go:110-131): PCM 8-bit
+ * v/MaxUint8, PCM 16-bit (v - MinInt16)/(MaxInt16 - MinInt16), both in
+ * float32 arithmetic; IEEE float32 copied. Returns -1 for a format the
+ * reference rejects ("unknown bits per sample" / "unknown audio format"). */
+int or_wav_floats(const void *in, int64_t count, int audio_format, int bits_per_sample,
+                  float *out);
+
 #ifdef __cplusplus
 }
 #endif

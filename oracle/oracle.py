@@ -66,6 +66,8 @@ def lib():
         L.or_is_pow2.restype = ctypes.c_int
         L.or_fill_uniform.argtypes = [P, I64, ctypes.c_uint64, ctypes.c_uint64]
         L.or_fill_uniform.restype = None
+        L.or_wav_floats.argtypes = [P, I64, ctypes.c_int, ctypes.c_int, P]
+        L.or_wav_floats.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -247,4 +249,15 @@ def fill_uniform(count: int, seed: int, offset: int = 0) -> np.ndarray:
     """Synthetic inputs identical to the device generator."""
     out = np.empty(count, np.float64)
     lib().or_fill_uniform(_p(out), count, seed, offset)
+    return out
+
+
+def wav_floats(raw: bytes, count: int, audio_format: int, bits_per_sample: int) -> np.ndarray:
+    """wav.ReadFloats's conversion (wav/wav.go:135-161) of `count` samples
+    of little-endian bytes; float32 like the reference."""
+    buf = np.frombuffer(bytes(raw), dtype=np.uint8)
+    out = np.empty(count, np.float32)
+    st = lib().or_wav_floats(_p(buf), count, audio_format, bits_per_sample, _p(out))
+    if st != 0:
+        raise ValueError("wav: unknown format")
     return out

@@ -14,6 +14,10 @@ reference's test tables from /root/reference as data.
      spectral/pwelch_test.go:31-46   pwelchTests
      spectral/spectral_test.go:31-56 segmentTests
      window/window_test.go:34-59     windowTests
+     wav/wav_test.go:62-95           wavTests      (header fields per file)
+   and wav/small.wav (copied) + the first 64 KiB of wav/float.wav's data
+   chunk (header intact) into tests/golden/wav/ — the data files the
+   reference's wav test reads.
 2. golden_fft.npz / golden_pwelch.npz — full-precision vectors (seeded inputs,
    outputs of the C restatement in oracle/, cross-checked here against numpy's
    pocketfft and scipy.signal.welch before they are written).
@@ -94,7 +98,37 @@ def reference_vectors() -> dict:
         {"L": e[0], "hamming": e[1], "hann": e[2], "bartlett": e[3], "flattop": e[4],
          "blackman": e[5]}
         for e in _literal_to_json(_block("window/window_test.go", "var windowTests = []windowTest{"))]
+    out["wavTests"] = wav_tests()
     return out
+
+
+def wav_tests() -> dict:
+    src = open(os.path.join(REF, "wav/wav_test.go")).read()
+    res = {}
+    for name in ("small.wav", "float.wav"):
+        blk = _block("wav/wav_test.go", f'"{name}": {{')
+        fields = {}
+        for key, expr in re.findall(r"(\w+):\s*([0-9][0-9 /]*)[,\n]", blk):
+            if not re.fullmatch(r"[0-9 /]+", expr):
+                continue
+            parts = [int(v) for v in expr.split("/")]
+            v = parts[0]
+            for d in parts[1:]:
+                v //= d
+            fields[key] = v
+        res[name] = fields
+    assert "checkHeader" in src  # the file also holds header tests (not data)
+    return res
+
+
+def wav_fixtures() -> None:
+    import shutil
+    dst = os.path.join(HERE, "wav")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(REF, "wav/small.wav"), os.path.join(dst, "small.wav"))
+    b = open(os.path.join(REF, "wav/float.wav"), "rb").read()
+    assert b[36:40] == b"data"  # RIFF(12) + fmt chunk(8 + 16) + data header(8) = 44
+    open(os.path.join(dst, "float_head.wav"), "wb").write(b[:44 + 65536])
 
 
 def _nrel(a, b) -> float:
@@ -164,6 +198,7 @@ def main():
     with open(os.path.join(HERE, "reference_vectors.json"), "w") as f:
         json.dump(vec, f, indent=1)
     full_precision()
+    wav_fixtures()
     print("wrote", os.listdir(HERE))
 
 
