@@ -8,6 +8,8 @@
 #pragma once
 
 #include <cmath>
+#include <cstdio>
+#include <istream>
 #include <complex>
 #include <functional>
 #include <stdexcept>
@@ -356,4 +358,111 @@ inline std::pair<std::vector<double>, std::vector<double>> Pwelch(const std::vec
 }
 
 }  // namespace spectral
+
+namespace wav {  // wav/wav.go
+
+// An error value the reference returns (err.Error() as the message).
+struct WavError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+constexpr int wavFormatPCM = 1, wavFormatIEEEFloat = 3;
+
+// wav.Header — wav.go:37-45
+struct Header {
+  uint16_t AudioFormat = 0, NumChannels = 0;
+  uint32_t SampleRate = 0, ByteRate = 0;
+  uint16_t BlockAlign = 0, BitsPerSample = 0;
+};
+
+// wav.Wav — wav.go:48-56 (Duration: Go time.Duration, nanoseconds)
+struct Wav : Header {
+  int64_t Samples = 0;
+  int64_t Duration = 0;
+  std::istream *r = nullptr;
+  int64_t remaining = 0;  // io.LimitReader over the data chunk
+
+  int sample_bytes() const {
+    if (AudioFormat == wavFormatPCM) {
+      if (BitsPerSample == 8 || BitsPerSample == 16) return BitsPerSample / 8;
+      throw WavError("wav: unknown bits per sample: " + std::to_string(BitsPerSample));
+    }
+    if (AudioFormat == wavFormatIEEEFloat) return 4;
+    throw WavError("wav: unknown audio format");
+  }
+  // binary.Read of n samples: the raw little-endian bytes
+  std::vector<unsigned char> read_raw(int64_t n) {
+    const int64_t want = n * sample_bytes();
+    const int64_t k = want < remaining ? want : remaining;
+    std::vector<unsigned char> b((size_t)want);
+    r->read(reinterpret_cast<char *>(b.data()), k);
+    const int64_t got = r->gcount();
+    remaining -= got;
+    if (got == 0 && want > 0) throw WavError("EOF");
+    if (got < want) throw WavError("unexpected EOF");
+    return b;
+  }
+  // ReadFloats — wav.go:135-161, converted on the GPU
+  std::vector<float> ReadFloats(int64_t n) {
+    const auto raw = read_raw(n);
+    std::vector<float> out((size_t)n);
+    check(gdsp_wav_read_floats(raw.data(), n, AudioFormat, BitsPerSample, out.data(), 0),
+          "wav.ReadFloats");
+    return out;
+  }
+};
+
+// wav.New — wav.go:59-107
+inline Wav New(std::istream &r) {
+  auto read_full = [&](unsigned char *b, int64_t n) {
+    r.read(reinterpret_cast<char *>(b), n);
+    const int64_t got = r.gcount();
+    if (got == 0 && n > 0) throw WavError("EOF");
+    if (got < n) throw WavError("unexpected EOF");
+  };
+  auto u16 = [](const unsigned char *p) { return (uint16_t)(p[0] | (p[1] << 8)); };
+  auto u32 = [](const unsigned char *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) |
+           ((uint32_t)p[3] << 24);
+  };
+  Wav w;
+  unsigned char h[16];
+  read_full(h, 12);
+  if (std::string((char *)h, 4) != "RIFF") throw WavError("wav: missing RIFF");
+  if (std::string((char *)h + 8, 4) != "WAVE") throw WavError("wav: missing WAVE");
+  bool has_fmt = false;
+  for (;;) {
+    read_full(h, 8);
+    const uint32_t sz = u32(h + 4);
+    const std::string typ((char *)h, 4);
+    if (typ == "fmt ") {
+      if (sz < 16) throw WavError("wav: bad fmt size");
+      std::vector<unsigned char> f(sz);
+      read_full(f.data(), sz);
+      w.AudioFormat = u16(&f[0]);
+      w.NumChannels = u16(&f[2]);
+      w.SampleRate = u32(&f[4]);
+      w.ByteRate = u32(&f[8]);
+      w.BlockAlign = u16(&f[12]);
+      w.BitsPerSample = u16(&f[14]);
+      if (w.AudioFormat != wavFormatPCM && w.AudioFormat != wavFormatIEEEFloat) {
+        char m[64];
+        snprintf(m, sizeof m, "wav: unknown audio format: %02x", w.AudioFormat);
+        throw WavError(m);
+      }
+      has_fmt = true;
+    } else if (typ == "data") {
+      if (!has_fmt) throw WavError("wav: unexpected fmt chunk");
+      w.Samples = (int64_t)sz / (int64_t)w.BitsPerSample * 8;
+      w.Duration = w.Samples * 1000000000LL / (int64_t)w.SampleRate / (int64_t)w.NumChannels;
+      w.r = &r;
+      w.remaining = sz;
+      return w;
+    } else {
+      r.ignore(sz);  // io.CopyN(ioutil.Discard, r, sz)
+    }
+  }
+}
+
+}  // namespace wav
 }  // namespace gdsp

@@ -5,6 +5,7 @@
 // tests/golden/reference_vectors.json, flattened to text by
 // tests/test_cpp_mirror.py (argv[1]). Exit code 0 = all pass.
 #include <cstdio>
+#include <cstring>
 #include <fstream>
 #include <iostream>
 #include <sstream>
@@ -84,6 +85,33 @@ int main(int argc, char **argv) {
       auto m = dsputils::MakeMatrix(x, dims), o = dsputils::MakeMatrix(out, dims);
       EXPECT(fft::FFTN(m).PrettyClose(o), "FFTN");
       EXPECT(fft::IFFTN(o).PrettyClose(m), "IFFTN");
+    } else if (kind == "WAV") {  // TestWav, wav_test.go:62-115 (+ ReadFloats)
+      std::string path;
+      int64_t fmt, ch, rate, brate, align, bits, samples, dur;
+      in >> path >> fmt >> ch >> rate >> brate >> align >> bits >> samples >> dur;
+      std::ifstream f(path, std::ios::binary);
+      auto w = wav::New(f);
+      EXPECT(w.AudioFormat == fmt && w.NumChannels == ch && w.SampleRate == rate &&
+                 w.ByteRate == brate && w.BlockAlign == align && w.BitsPerSample == bits &&
+                 w.Samples == samples && w.Duration == dur,
+             "wav header " << path);
+      const auto fl = w.ReadFloats(1024);
+      std::ifstream g(path, std::ios::binary);
+      g.seekg(44);
+      bool ok = true;
+      for (int i = 0; i < 1024; ++i) {  // wav.go:145-153 in float32 arithmetic
+        float want;
+        if (fmt == 3) {
+          g.read(reinterpret_cast<char *>(&want), 4);
+        } else {
+          int16_t v;
+          g.read(reinterpret_cast<char *>(&v), 2);
+          volatile float num = (float)v - (-32768.0f);
+          want = num / 65535.0f;
+        }
+        ok = ok && std::memcmp(&want, &fl[(size_t)i], 4) == 0;
+      }
+      EXPECT(ok, "wav ReadFloats " << path);
     } else if (kind == "PWELCH") {  // TestPwelch, pwelch_test.go:48-60
       double fs;
       size_t n, lp;

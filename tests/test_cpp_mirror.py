@@ -25,6 +25,12 @@ def _write_vectors(refvec, path):
         lines.append(" ".join(["FFTN", str(len(c["dim"]))] + [str(d) for d in c["dim"]]
                               + [repr(float(v)) for v in c["in"]]
                               + [repr(float(v)) for p in c["out"] for v in p]))
+    files = {"small.wav": "small.wav", "float.wav": "float_head.wav"}
+    for name, h in refvec["wavTests"].items():
+        path = os.path.join(REPO, "tests", "golden", "wav", files[name])
+        lines.append(" ".join(["WAV", path] + [str(h[k]) for k in (
+            "AudioFormat", "NumChannels", "SampleRate", "ByteRate", "BlockAlign",
+            "BitsPerSample", "Samples", "Duration")]))
     for c in refvec["pwelchTests"]:
         if not c["x"]:
             continue
