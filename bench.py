@@ -44,7 +44,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="radix4096",
-                    choices=["radix4096", "bluestein3000", "chirpz3000", "fft2_8192", "pwelch"])
+                    choices=["radix4096", "bluestein3000", "chirpz3000", "fft2_8192", "fft2_dist",
+                             "pwelch"])
     ap.add_argument("--batch", type=int, default=0, help="rows per GPU (0 = config default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU seconds for the cpu_baseline sample (0 disables)")
@@ -118,6 +119,25 @@ def main():
         cfg = {"workload": "fft.FFT2 complex128 8192x8192", "rows": rows, "cols": cols,
                "parallelism": f"replicas{world}"}
         kernel = "fft2 (all launches)"
+        metric = "Gsamples/s, fft.FFT2 8192x8192 complex128"
+    elif w == "fft2_dist":  # one 8192^2 FFT2 with its rows sharded over the ranks (strong)
+        Dd = importlib.import_module("go-dsp_amd.distributed")
+        R = C = 8192
+        lo, hi = Dd.shard_range(R, world, rank)
+        x = torch.empty((hi - lo, C), dtype=torch.complex128, device=dev)
+        D.fill_uniform(x, SEED, offset=lo * C * 2, stream=stream)
+        result = {}
+        group = None
+
+        def step():
+            result["y"] = Dd.fft2_sharded(x, R, group=group, stream=stream)
+
+        samples_per_step = R * C // world
+        alg_bytes = 2 * 2 * 16 * x.numel()
+        cfg = {"workload": "fft.FFT2 complex128 8192x8192, rows sharded over the ranks "
+                           "(row FFTs, RCCL all-to-all, column FFTs, all-to-all back)",
+               "rows": R, "cols": C, "parallelism": f"rows{world}+alltoall"}
+        kernel = "fft2_sharded (all launches and both all-to-alls)"
         metric = "Gsamples/s, fft.FFT2 8192x8192 complex128"
     else:  # pwelch: 2^30 samples total, NFFT 4096, 50 % overlap, Hann (strong scaling)
         Dd = importlib.import_module("go-dsp_amd.distributed")
@@ -200,7 +220,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong" if w == "pwelch" else "weak",
+            "scaling": "strong" if w in ("pwelch", "fft2_dist") else "weak",
             "vs_baseline": None,
             "dtype": "f64 (complex128)",
             "data": "synthetic (splitmix64 uniform[-1,1), generated in HBM)",
@@ -243,6 +263,8 @@ def cpu_baseline(workload: str, seconds: float):
                 "kind": "port",
                 "sample": f"spectral.Pwelch on a {n}-sample prefix of the stream "
                           f"(NFFT 4096, 50% overlap, {dt:.1f} s), {pool}"}
+    if workload == "fft2_dist":
+        workload = "fft2_8192"
     n = {"radix4096": 4096, "bluestein3000": 3000, "chirpz3000": 3000, "fft2_8192": 8192}[workload]
     rows = 64 if n != 8192 else 16
     x = oracle.fill_uniform(2 * n * rows, SEED).view(np.complex128).reshape(rows, n)

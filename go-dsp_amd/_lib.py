@@ -49,6 +49,7 @@ SIGNATURES = {
     "gdsp_fft2_real": (_I, [_P, _P, _I64, _I64, _I]),
     "gdsp_ensure_plan": (_I, [_I64]),
     "gdsp_fftn": (_I, [_P, _P, _P, _I, _I]),
+    "gdsp_fft_axis_device": (_I, [_P, _P, _P, _I, _I, _I, _P]),
     "gdsp_fftn_device": (_I, [_P, _P, _P, _I, _I, _P]),
     "gdsp_set_worker_pool_size": (None, [_I]),
     "gdsp_worker_pool_size": (_I, []),

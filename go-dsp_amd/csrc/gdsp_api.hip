@@ -753,69 +753,141 @@ int gdsp_fft2_device(const void *d_in, void *d_out, int64_t rows, int64_t cols, 
 // kernels batched over `outer` (one pass for L <= 512, the four-step split
 // above); anything else through a batched transpose, the row kernels and a
 // transpose back.
+// One axis of computeFFTN (fft/fft.go:172-185): the 1-D transform of the
+// `outer` x `inner` lines of length L, read from src (cur itself, or the
+// caller's input for the first axis), result in cur; other is scratch.
+static int fft_axis(const cd *src, cd *cur, cd *other, int64_t L, int64_t inner, int64_t outer,
+                    bool inv, hipStream_t s) {
+  gdsp_plan *pl = nullptr;
+  STCHK(get_plan(L, &pl));
+  if (inner == 1) {
+    STCHK(exec_plan(pl, src, cur, outer, inv, gdsp::LOAD_COMPLEX, s));
+    return GDSP_OK;
+  }
+  const int lL = ilog2(L);
+  const double sc = 1.0 / (double)L;
+  if (is_pow2(L) && lL >= gdsp::kColMinLog2 && lL <= 2 * gdsp::kColMaxLog2) {
+    const int l1 = lL <= gdsp::kColMaxLog2 ? lL : lL / 2, l2 = lL - l1;
+    gdsp_plan *p1 = nullptr, *p2 = nullptr;
+    STCHK(get_plan((int64_t)1 << l1, &p1));
+    if (l2) STCHK(get_plan((int64_t)1 << l2, &p2));
+    const int64_t R1 = (int64_t)1 << l1, R2 = (int64_t)1 << l2;
+    for (int64_t o0 = 0; o0 < outer; o0 += 65535) {
+      const int64_t nb = outer - o0 < 65535 ? outer - o0 : 65535;
+      const cd *s0 = src + o0 * L * inner;
+      cd *c0 = cur + o0 * L * inner, *t0 = other + o0 * L * inner;
+      if (!l2) {
+        HIPCHK(gdsp::launch_colfft(lL, inv, 0, inv, s0, c0, inner, 1, 0, 1, 0, 1, pl->tw,
+                                   nullptr, lL, sc, nb, L * inner, s));
+      } else {
+        // A: src -> other, B: other -> cur (the result lands in cur, and
+        // the caller's input is never written)
+        HIPCHK(gdsp::launch_colfft(l1, inv, 1, false, s0, t0, inner, R2, 1, R2, 1, R2, p1->tw,
+                                   pl->tw, lL, 1.0, nb, L * inner, s));
+        HIPCHK(gdsp::launch_colfft(l2, false, 0, inv, t0, c0, inner, R1, R2, 1, 1, R1, p2->tw,
+                                   nullptr, lL, sc, nb, L * inner, s));
+      }
+    }
+    return GDSP_OK;
+  }
+  for (int64_t o0 = 0; o0 < outer; o0 += 65535) {
+    const int64_t nb = outer - o0 < 65535 ? outer - o0 : 65535;
+    HIPCHK(gdsp::launch_transpose(src + o0 * L * inner, other + o0 * L * inner, L, inner, s, nb));
+  }
+  STCHK(exec_plan(pl, other, other, outer * inner, inv, gdsp::LOAD_COMPLEX, s));
+  for (int64_t o0 = 0; o0 < outer; o0 += 65535) {
+    const int64_t nb = outer - o0 < 65535 ? outer - o0 : 65535;
+    HIPCHK(gdsp::launch_transpose(other + o0 * L * inner, cur + o0 * L * inner, inner, L, s, nb));
+  }
+  return GDSP_OK;
+}
+
+// fft.FFTN / IFFTN (fft/fft.go:157-192): the 1-D transform along every line
+// of dimension 0, then 1, ... of a row-major array. Per axis (length L,
+// `inner` elements after it, `outer` before): contiguous lines (inner = 1) go
+// to the batched row kernels; strided power-of-2 lines to the column-tile
+// kernels batched over `outer` (one pass for L <= 512, the four-step split
+// above); anything else through a batched transpose, the row kernels and a
+// transpose back.
+// One axis of computeFFTN (fft/fft.go:172-185): the 1-D transform of the
+// `outer` x `inner` lines of length L. The result lands in cur, or in other
+// when the four-step split ends there (then the two are swapped).
+static int fft_axis(cd *&cur, cd *&other, int64_t L, int64_t inner, int64_t outer, bool inv,
+                    hipStream_t s) {
+  if (L == 1) return GDSP_OK;
+  gdsp_plan *pl = nullptr;
+  STCHK(get_plan(L, &pl));
+  if (inner == 1) {
+    STCHK(exec_plan(pl, cur, cur, outer, inv, gdsp::LOAD_COMPLEX, s));
+    return GDSP_OK;
+  }
+  const int lL = ilog2(L);
+  const double sc = 1.0 / (double)L;
+  if (is_pow2(L) && lL >= gdsp::kColMinLog2 && lL <= 2 * gdsp::kColMaxLog2) {
+    const int l1 = lL <= gdsp::kColMaxLog2 ? lL : lL / 2, l2 = lL - l1;
+    gdsp_plan *p1 = nullptr, *p2 = nullptr;
+    STCHK(get_plan((int64_t)1 << l1, &p1));
+    if (l2) STCHK(get_plan((int64_t)1 << l2, &p2));
+    const int64_t R1 = (int64_t)1 << l1, R2 = (int64_t)1 << l2;
+    for (int64_t o0 = 0; o0 < outer; o0 += 65535) {
+      const int64_t nb = outer - o0 < 65535 ? outer - o0 : 65535;
+      cd *c0 = cur + o0 * L * inner, *t0 = other + o0 * L * inner;
+      if (!l2) {
+        HIPCHK(gdsp::launch_colfft(lL, inv, 0, inv, c0, c0, inner, 1, 0, 1, 0, 1, pl->tw,
+                                   nullptr, lL, sc, nb, L * inner, s));
+      } else {
+        HIPCHK(gdsp::launch_colfft(l1, inv, 1, false, c0, c0, inner, R2, 1, R2, 1, R2, p1->tw,
+                                   pl->tw, lL, 1.0, nb, L * inner, s));
+        HIPCHK(gdsp::launch_colfft(l2, false, 0, inv, c0, t0, inner, R1, R2, 1, 1, R1, p2->tw,
+                                   nullptr, lL, sc, nb, L * inner, s));
+      }
+    }
+    if (l2) std::swap(cur, other);
+    return GDSP_OK;
+  }
+  for (int64_t o0 = 0; o0 < outer; o0 += 65535) {
+    const int64_t nb = outer - o0 < 65535 ? outer - o0 : 65535;
+    HIPCHK(gdsp::launch_transpose(cur + o0 * L * inner, other + o0 * L * inner, L, inner, s, nb));
+  }
+  STCHK(exec_plan(pl, other, other, outer * inner, inv, gdsp::LOAD_COMPLEX, s));
+  for (int64_t o0 = 0; o0 < outer; o0 += 65535) {
+    const int64_t nb = outer - o0 < 65535 ? outer - o0 : 65535;
+    HIPCHK(gdsp::launch_transpose(other + o0 * L * inner, cur + o0 * L * inner, inner, L, s, nb));
+  }
+  return GDSP_OK;
+}
+
+// fft.FFTN / IFFTN (fft/fft.go:157-192): the 1-D transform along every line
+// of dimension 0, then 1, ... of a row-major array. Per axis (length L,
+// `inner` elements after it, `outer` before): contiguous lines (inner = 1) go
+// to the batched row kernels; strided power-of-2 lines to the column-tile
+// kernels batched over `outer` (one pass for L <= 512, the four-step split
+// above); anything else through a batched transpose, the row kernels and a
+// transpose back. axis >= 0 transforms that axis only.
 static int fftn_device(const cd *in, cd *out, const int64_t *dims, int ndims, bool inv,
-                       hipStream_t s) {
+                       hipStream_t s, int axis = -1) {
   if (ndims < 1 || !dims) return fail(GDSP_ERR_INVALID, "no dimensions");
+  if (axis >= ndims) return fail(GDSP_ERR_INVALID, "axis out of range");
   int64_t total = 1;
   for (int i = 0; i < ndims; ++i) {
     if (dims[i] < 1) return fail(GDSP_ERR_INVALID, "invalid dimensions");  // matrix.go:43
     total *= dims[i];
   }
-  if (in != out)
-    HIPCHK(hipMemcpyAsync(out, in, (size_t)total * sizeof(cd), hipMemcpyDeviceToDevice, s));
   DevBuf work;
   STCHK(work.alloc((size_t)total * sizeof(cd), s, SLOT_FFTN));
   cd *cur = out, *other = (cd *)work.p;
+  const cd *src = in;  // the first transformed axis reads the input directly
   int64_t inner = total;
   for (int d = 0; d < ndims; ++d) {
     const int64_t L = dims[d];
     inner /= L;
     const int64_t outer = total / (L * inner);
-    if (L == 1) continue;
-    gdsp_plan *pl = nullptr;
-    STCHK(get_plan(L, &pl));
-    if (inner == 1) {
-      STCHK(exec_plan(pl, cur, cur, outer, inv, gdsp::LOAD_COMPLEX, s));
-      continue;
-    }
-    const int lL = ilog2(L);
-    const double sc = 1.0 / (double)L;
-    if (is_pow2(L) && lL >= gdsp::kColMinLog2 && lL <= 2 * gdsp::kColMaxLog2) {
-      const int l1 = lL <= gdsp::kColMaxLog2 ? lL : lL / 2, l2 = lL - l1;
-      gdsp_plan *p1 = nullptr, *p2 = nullptr;
-      STCHK(get_plan((int64_t)1 << l1, &p1));
-      if (l2) STCHK(get_plan((int64_t)1 << l2, &p2));
-      const int64_t R1 = (int64_t)1 << l1, R2 = (int64_t)1 << l2;
-      for (int64_t o0 = 0; o0 < outer; o0 += 65535) {
-        const int64_t nb = outer - o0 < 65535 ? outer - o0 : 65535;
-        cd *c0 = cur + o0 * L * inner, *t0 = other + o0 * L * inner;
-        if (!l2) {
-          HIPCHK(gdsp::launch_colfft(lL, inv, 0, inv, c0, c0, inner, 1, 0, 1, 0, 1, pl->tw,
-                                     nullptr, lL, sc, nb, L * inner, s));
-        } else {
-          HIPCHK(gdsp::launch_colfft(l1, inv, 1, false, c0, c0, inner, R2, 1, R2, 1, R2, p1->tw,
-                                     pl->tw, lL, 1.0, nb, L * inner, s));
-          HIPCHK(gdsp::launch_colfft(l2, false, 0, inv, c0, t0, inner, R1, R2, 1, 1, R1, p2->tw,
-                                     nullptr, lL, sc, nb, L * inner, s));
-        }
-      }
-      if (l2) std::swap(cur, other);
-      continue;
-    }
-    for (int64_t o0 = 0; o0 < outer; o0 += 65535) {
-      const int64_t nb = outer - o0 < 65535 ? outer - o0 : 65535;
-      HIPCHK(gdsp::launch_transpose(cur + o0 * L * inner, other + o0 * L * inner, L, inner, s,
-                                    nb));
-    }
-    STCHK(exec_plan(pl, other, other, outer * inner, inv, gdsp::LOAD_COMPLEX, s));
-    for (int64_t o0 = 0; o0 < outer; o0 += 65535) {
-      const int64_t nb = outer - o0 < 65535 ? outer - o0 : 65535;
-      HIPCHK(gdsp::launch_transpose(other + o0 * L * inner, cur + o0 * L * inner, inner, L, s,
-                                    nb));
-    }
+    if ((axis >= 0 && d != axis) || L == 1) continue;
+    STCHK(fft_axis(src, cur, other, L, inner, outer, inv, s));
+    src = cur;
   }
-  if (cur != out)
-    HIPCHK(hipMemcpyAsync(out, cur, (size_t)total * sizeof(cd), hipMemcpyDeviceToDevice, s));
+  if (src != out)
+    HIPCHK(hipMemcpyAsync(out, src, (size_t)total * sizeof(cd), hipMemcpyDeviceToDevice, s));
   return GDSP_OK;
 }
 
@@ -850,6 +922,15 @@ int gdsp_fft2(const double *x, double *out, int64_t rows, int64_t cols, int inve
 
 int gdsp_fft2_real(const double *x, double *out, int64_t rows, int64_t cols, int inverse) {
   return fft2_host(x, true, out, rows, cols, inverse);
+}
+
+int gdsp_fft_axis_device(const void *d_in, void *d_out, const int64_t *dims, int ndims,
+                         int axis, int inverse, void *stream) {
+  if (axis < 0) return fail(GDSP_ERR_INVALID, "axis out of range");
+  int dev = 0;
+  STCHK(current_device(&dev));
+  return fftn_device((const cd *)d_in, (cd *)d_out, dims, ndims, inverse != 0,
+                     (hipStream_t)stream, axis);
 }
 
 int gdsp_fftn_device(const void *d_in, void *d_out, const int64_t *dims, int ndims, int inverse,

@@ -84,6 +84,24 @@ def fft2(x, out=None, inverse: bool = False, work=None, stream=None):
     return out
 
 
+def fft_axis(x, axis: int, out=None, inverse: bool = False, stream=None):
+    """The 1-D FFT/IFFT along one axis of a contiguous complex128 CUDA tensor
+    (gdsp_fft_axis_device; axis 0 of a matrix = computeFFT2's column pass)."""
+    torch = _torch()
+    assert x.is_cuda and x.dtype == torch.complex128 and x.is_contiguous()
+    if out is None:
+        out = torch.empty_like(x)
+    assert out.shape == x.shape and out.is_contiguous()
+    if x.numel() == 0:
+        return out
+    dims = (ctypes.c_int64 * x.dim())(*x.shape)
+    with torch.cuda.device(x.device):
+        check(lib().gdsp_fft_axis_device(_ptr(x), _ptr(out), dims, x.dim(), axis % x.dim(),
+                                         int(inverse), _stream_ptr(stream, x.device)),
+              "fft_axis_device")
+    return out
+
+
 def fill_uniform(t, seed: int, offset: int = 0, stream=None):
     """Fill a float64 (or complex128, as interleaved pairs) CUDA tensor with the
     counter-based uniform[-1,1) generator."""

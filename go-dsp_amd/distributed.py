@@ -3,6 +3,10 @@
 
 - Batched FFT (fft.FFT over many rows): rows are independent, so each rank
   transforms a contiguous row shard; there is no data-path collective.
+- FFT2 (fft/fft.go:123-154) of a matrix whose rows are sharded over the
+  ranks: local row FFTs, one all-to-all that gives every rank all rows of its
+  column block, local column FFTs (gdsp_fft_axis_device), and one all-to-all
+  back to the row shards. Two RCCL all-to-alls of (W-1)/W of the shard each.
 - Pwelch (spectral/pwelch.go:74-145): segments [S*r/W, S*(r+1)/W) go to rank
   r, which needs samples [lo*stride, (hi-1)*stride + nfft) — its slice plus an
   (nfft - stride)-sample halo. Each rank accumulates per-bin power sums on its
@@ -116,6 +120,68 @@ def pwelch(x_local, Fs: float, o: spectral.PwelchOptions, shard: PwelchShard, gr
         host = acc.cpu().numpy()
     return spectral.finalize(host, shard.nsegs_total, nfft, pad,
                              np.asarray(wf(nfft), np.float64), Fs, not scaling)
+
+
+def _all_to_all_c128(send, recv, send_counts, recv_counts, group, dist, torch):
+    """all_to_all_single of complex128 pieces (as float64 pairs). gloo (the
+    CPU rehearsal of the N>1 path) exchanges host copies."""
+    sv, rv = torch.view_as_real(send).reshape(-1), torch.view_as_real(recv).reshape(-1)
+    host = sv.is_cuda and dist.get_backend(group) != "nccl"
+    s_, r_ = (sv.cpu(), torch.empty(rv.shape, dtype=rv.dtype)) if host else (sv, rv)
+    dist.all_to_all_single(r_, s_, [2 * c for c in recv_counts], [2 * c for c in send_counts],
+                           group=group)
+    if host:
+        rv.copy_(r_)
+
+
+def fft2_sharded(x_local, rows_total: int, inverse: bool = False, group=None, stream=None,
+                 row_fft: Optional[Callable] = None, col_fft: Optional[Callable] = None):
+    """Multi-GPU fft.FFT2 / IFFT2 (fft/fft.go:109-154). x_local: this rank's
+    rows [shard_range(rows_total, W, r)) of the rows_total x C matrix, a
+    (rows_r, C) complex128 tensor. Returns this rank's rows of the result.
+
+    1. row FFTs of the local rows (independent rows: no exchange);
+    2. all-to-all: the column block [C*q/W, C*(q+1)/W) of the local rows goes
+       to rank q, so each rank holds every row of its column block;
+    3. column FFTs of that rows_total x C_r block;
+    4. all-to-all back to row shards.
+    The reference transforms columns first (fft.go:138-147); the 2-D DFT is
+    the same either way (separable), at roundoff level.
+    row_fft / col_fft (tensor -> tensor, FFT along rows / along axis 0)
+    replace the device kernels — the CPU tests pass oracle-backed ones."""
+    import torch
+    import torch.distributed as dist
+
+    W = dist.get_world_size(group) if dist.is_initialized() else 1
+    r = dist.get_rank(group) if dist.is_initialized() else 0
+    rows_r, C = x_local.shape
+    lo, hi = shard_range(rows_total, W, r)
+    assert rows_r == hi - lo, "x_local is not this rank's row shard"
+    if row_fft is None or col_fft is None:
+        from . import device
+    row_fft = row_fft or (lambda a: device.fft_batch(a, inverse=inverse, stream=stream))
+    col_fft = col_fft or (lambda a: device.fft_axis(a, 0, inverse=inverse, stream=stream))
+    ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+    with ctx:
+        y = row_fft(x_local.contiguous())
+        if W == 1:
+            return col_fft(y)
+        rows = [shard_range(rows_total, W, q) for q in range(W)]
+        cols = [shard_range(C, W, q) for q in range(W)]
+        c_lo, c_hi = cols[r]
+        send = torch.cat([y[:, a:b].reshape(-1) for a, b in cols])
+        blk = torch.empty((rows_total, c_hi - c_lo), dtype=y.dtype, device=y.device)
+        _all_to_all_c128(send, blk, [rows_r * (b - a) for a, b in cols],
+                         [(b - a) * (c_hi - c_lo) for a, b in rows], group, dist, torch)
+        blk = col_fft(blk)
+        back = torch.empty(rows_r * C, dtype=y.dtype, device=y.device)
+        _all_to_all_c128(blk.reshape(-1), back, [(b - a) * (c_hi - c_lo) for a, b in rows],
+                         [rows_r * (b - a) for a, b in cols], group, dist, torch)
+        pieces, off = [], 0
+        for a, b in cols:
+            pieces.append(back[off:off + rows_r * (b - a)].view(rows_r, b - a))
+            off += rows_r * (b - a)
+        return torch.cat(pieces, dim=1)
 
 
 def fft_rows_sharded(x_shard, inverse: bool = False, out=None, stream=None):

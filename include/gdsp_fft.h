@@ -181,6 +181,14 @@ int gdsp_fft2_device(const void *d_in, void *d_out, int64_t rows, int64_t cols,
 int gdsp_fftn_device(const void *d_in, void *d_out, const int64_t *dims, int ndims, int inverse,
                      void *stream);
 
+/* One axis of FFTN: the 1-D FFT/IFFT along dimension `axis` of a device
+ * row-major array (the per-dimension loop of computeFFTN, fft/fft.go:172-185;
+ * axis 0 of a rows x cols matrix is computeFFT2's column pass, :138-147).
+ * The building block of the multi-GPU FFT2 (row FFTs, all-to-all, column
+ * FFTs on a column block). */
+int gdsp_fft_axis_device(const void *d_in, void *d_out, const int64_t *dims, int ndims,
+                         int axis, int inverse, void *stream);
+
 /* Pwelch partial accumulation over segments [seg_begin, seg_end) of a device
  * signal d_x (n float64, sample 0 = sample 0 of segment 0). Adds into
  * d_acc[0..flen) (flen = max(pad, nfft)) the per-bin sums S_k of |Z_k|² over
