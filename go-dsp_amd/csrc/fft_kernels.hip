@@ -230,23 +230,27 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_kernel(
 // every iteration, 2 an LDS table shared by the workgroup.
 // Measured at F = 4096 (2^30 samples): E = 16 with the LDS window 3.19 ms;
 // E = 8 (LOG2E = 3: 104 VGPRs, twice the waves, one more exchange) 3.67 ms;
-// E = 16 forced to 168 / 128 VGPRs (MINW 3 / 4) spills: 4.85 / 6.07 ms.
-template <int LOG2F, int WMODE = 2, int MINW = 1, int LOG2E = 4>
+// E = 16 forced to 168 / 128 VGPRs (MINW 3 / 4) spills: 4.85 / 6.07 ms;
+// window re-read from L1/L2 (WMODE 1) with the split exchange 3.48 ms, with
+// a complex (two-buffer) exchange 3.45 ms.
+template <int LOG2F, int WMODE = 2, int MINW = 1, int LOG2E = 4, bool SPLIT = true>
 __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_kernel(
     const double *__restrict__ x, int64_t seg_begin, int64_t seg_end, int64_t pairs_per_worker,
     const double *__restrict__ win, const cd *__restrict__ tw, double *__restrict__ partial) {
   using G = Geo<LOG2F, LOG2E>;
   constexpr int E = G::E, H = E / 2;
   constexpr int64_t STRIDE = G::N / 2;
-  __shared__ double lds[G::LDS_DOUBLES + (WMODE == 2 ? G::N : 0)];
+  constexpr int XD = (SPLIT ? 1 : 2) * G::LDS_DOUBLES;  // exchange buffer(s)
+  __shared__ double lds[XD + (WMODE == 2 ? G::N : 0)];
   const int lt = threadIdx.x;
   const int slot = lt / G::T;
   const int t = lt & (G::T - 1);
   const int64_t worker = (int64_t)blockIdx.x * G::TPW + slot;
   double *lre = lds + slot * G::STRIDE;
+  double *lim = SPLIT ? lre : lre + G::LDS_DOUBLES;
   const int64_t npairs = (seg_end - seg_begin + 1) / 2;
   double wv[E];
-  double *wl = lds + G::LDS_DOUBLES;
+  double *wl = lds + XD;
   if constexpr (WMODE == 0) {
 #pragma unroll
     for (int k = 0; k < E; ++k) wv[k] = win[t + k * G::T];
@@ -298,7 +302,7 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_ker
     }
 #pragma unroll
     for (int k = 0; k < H; ++k) carry[k] = c2[k];
-    fft_regs<LOG2F, true, true, LOG2E>(v, opaque_int(t), tw, lre, lre, it == 0);
+    fft_regs<LOG2F, SPLIT, true, LOG2E>(v, opaque_int(t), tw, lre, lim, it == 0);
     if (active) {
 #pragma unroll
       for (int k = 0; k < E; ++k) acc[k] += v[k].x * v[k].x + v[k].y * v[k].y;
@@ -651,14 +655,14 @@ static hipError_t launch_pw_t(const double *x, int64_t nfft, int64_t stride, int
   return hipGetLastError();
 }
 
-template <int LOG2F, int WMODE = 2, int MINW = 1, int LOG2E = 4>
+template <int LOG2F, int WMODE = 2, int MINW = 1, int LOG2E = 4, bool SPLIT = true>
 static hipError_t launch_pwh_t(const double *x, int64_t seg_begin, int64_t seg_end, int64_t ppw,
                                int64_t nworkers, const double *win, const cd *tw, double *partial,
                                hipStream_t s) {
   using G = Geo<LOG2F, LOG2E>;
   if (G::TPW != Geo<LOG2F>::TPW) return hipErrorInvalidValue;  // workers per block
   const int64_t nblk = (nworkers + G::TPW - 1) / G::TPW;
-  hipLaunchKernelGGL((pwelch_half_kernel<LOG2F, WMODE, MINW, LOG2E>), dim3((unsigned)nblk), dim3(G::WG), 0, s,
+  hipLaunchKernelGGL((pwelch_half_kernel<LOG2F, WMODE, MINW, LOG2E, SPLIT>), dim3((unsigned)nblk), dim3(G::WG), 0, s,
                      x, seg_begin, seg_end, ppw, win, tw, partial);
   return hipGetLastError();
 }
