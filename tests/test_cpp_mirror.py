@@ -27,8 +27,8 @@ def _write_vectors(refvec, path):
                               + [repr(float(v)) for p in c["out"] for v in p]))
     files = {"small.wav": "small.wav", "float.wav": "float_head.wav"}
     for name, h in refvec["wavTests"].items():
-        path = os.path.join(REPO, "tests", "golden", "wav", files[name])
-        lines.append(" ".join(["WAV", path] + [str(h[k]) for k in (
+        wav_path = os.path.join(REPO, "tests", "golden", "wav", files[name])
+        lines.append(" ".join(["WAV", wav_path] + [str(h[k]) for k in (
             "AudioFormat", "NumChannels", "SampleRate", "ByteRate", "BlockAlign",
             "BitsPerSample", "Samples", "Duration")]))
     for c in refvec["pwelchTests"]:
