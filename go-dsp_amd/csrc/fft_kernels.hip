@@ -418,23 +418,33 @@ __global__ __launch_bounds__(256) void colfft_tile_kernel(
   }
 }
 
-// out[c*rows + r] = in[r*cols + c] through a 32x33 LDS tile (complex128).
+// out[c*rows + r] = in[r*cols + c] through a 32x33 LDS tile (complex128),
+// for `batch` consecutive matrices. Tiles of all matrices form one index
+// space that a bounded grid strides over, so small matrices (the 210 x 210
+// steps of a 44100-point four-step) do not cost a workgroup per tile.
+// Options: conj + scale on the way out; times tw[r*c] (conjugated if
+// tw_conj; the caller guarantees r*c < twn, as rows*cols = twn in the
+// mixed four-step's W_N^(n2*k1) step).
 __global__ __launch_bounds__(256) void transpose_kernel(const cd *__restrict__ in,
                                                         cd *__restrict__ out, int64_t rows,
-                                                        int64_t cols, int conj_scale,
-                                                        double scale) {
+                                                        int64_t cols, int64_t batch,
+                                                        int conj_scale, double scale,
+                                                        const cd *__restrict__ tw, int64_t twn,
+                                                        int tw_conj) {
   __shared__ cd tile[32][33];
-  in += (int64_t)blockIdx.y * rows * cols;
-  out += (int64_t)blockIdx.y * rows * cols;
   const int64_t tiles_c = (cols + 31) / 32;
   const int64_t tiles_r = (rows + 31) / 32;
-  for (int64_t tb = blockIdx.x; tb < tiles_c * tiles_r; tb += gridDim.x) {
+  const int64_t per = tiles_c * tiles_r;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int64_t tg = blockIdx.x; tg < per * batch; tg += gridDim.x) {
+    const int64_t b = tg / per, tb = tg - b * per;
     const int64_t tr = tb / tiles_c, tc = tb - tr * tiles_c;
-    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+    const cd *src = in + b * rows * cols;
+    cd *dst = out + b * rows * cols;
 #pragma unroll
     for (int i = 0; i < 32; i += 8) {
       const int64_t r = tr * 32 + ty + i, c = tc * 32 + tx;
-      if (r < rows && c < cols) tile[ty + i][tx] = in[r * cols + c];
+      if (r < rows && c < cols) tile[ty + i][tx] = src[r * cols + c];
     }
     __syncthreads();
 #pragma unroll
@@ -442,8 +452,13 @@ __global__ __launch_bounds__(256) void transpose_kernel(const cd *__restrict__ i
       const int64_t c = tc * 32 + ty + i, r = tr * 32 + tx;
       if (r < rows && c < cols) {
         cd o = tile[tx][ty + i];
+        if (tw) {
+          cd w = tw[r * c];
+          if (tw_conj) w.y = -w.y;
+          o = cmul(o, w);
+        }
         if (conj_scale) o = {o.x * scale, -o.y * scale};
-        out[c * rows + r] = o;
+        dst[c * rows + r] = o;
       }
     }
     __syncthreads();
@@ -786,12 +801,15 @@ hipError_t launch_colfft(int log2l, bool conj_in, int twiddle, bool conj_scale_o
 }
 
 hipError_t launch_transpose(const cd *in, cd *out, int64_t rows, int64_t cols, hipStream_t s,
-                            int64_t batch, bool conj_scale, double scale) {
+                            int64_t batch, bool conj_scale, double scale, const cd *tw,
+                            int64_t twn, bool tw_conj) {
   if (batch < 1 || batch > 65535) return hipErrorInvalidValue;
-  const int64_t tiles = ((rows + 31) / 32) * ((cols + 31) / 32);
-  const unsigned nb = (unsigned)(tiles < 65536 ? tiles : 65536);
-  hipLaunchKernelGGL(transpose_kernel, dim3(nb, (unsigned)batch), dim3(256), 0, s, in, out, rows,
-                     cols, (int)conj_scale, scale);
+  if (tw && (rows - 1) * (cols - 1) >= twn) return hipErrorInvalidValue;  // r*c < twn
+  const int64_t tiles = ((rows + 31) / 32) * ((cols + 31) / 32) * batch;
+  const int64_t cap = 256 * 32;  // 32 tile-loop workgroups per CU
+  const unsigned nb = (unsigned)(tiles < cap ? tiles : cap);
+  hipLaunchKernelGGL(transpose_kernel, dim3(nb), dim3(256), 0, s, in, out, rows, cols, batch,
+                     (int)conj_scale, scale, tw, twn, (int)tw_conj);
   return hipGetLastError();
 }
 

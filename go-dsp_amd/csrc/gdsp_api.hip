@@ -101,7 +101,7 @@ bool lds_split_default() {
 enum Slot {
   SLOT_IN = 0, SLOT_OUT, SLOT_AUX, SLOT_AUX2, SLOT_GLOBAL, SLOT_GLOBAL_IN, SLOT_REAL,
   SLOT_BLU, SLOT_FFT2, SLOT_PW_PART, SLOT_PW_RED, SLOT_PW_BUF, SLOT_FS0, SLOT_FS1, SLOT_FS2,
-  SLOT_FS3, SLOT_FFTN, SLOT_COUNT
+  SLOT_FS3, SLOT_FFTN, SLOT_MX0, SLOT_MX1, SLOT_COUNT
 };
 
 struct Workspace {
@@ -219,7 +219,7 @@ int copy_d2h(void *dst, const void *src, size_t bytes, hipStream_t s) {
 }  // namespace
 
 enum PlanKind { KIND_TRIVIAL = 0, KIND_LDS = 1, KIND_GLOBAL = 2, KIND_BLUESTEIN = 3,
-                KIND_BLUESTEIN_COMPOSED = 4, KIND_MIXED = 5 };
+                KIND_BLUESTEIN_COMPOSED = 4, KIND_MIXED = 5, KIND_MIXED4 = 6 };
 
 struct gdsp_plan {
   int device = 0;
@@ -229,6 +229,9 @@ struct gdsp_plan {
   cd *tw = nullptr;  // power of 2: T_n[k] = exp(-2 pi i k/n), n entries;
                      // mixed radix: the per-pass butterfly-major table
   gdsp::MixedDesc md{};
+  // mixed four-step (KIND_MIXED4): n = n1 * n2, one-kernel sub-plans, tw = T_n
+  int64_t n1 = 0, n2 = 0;
+  gdsp_plan *p1 = nullptr, *p2 = nullptr;
   // Bluestein (fft/bluestein.go): M = NextPowerOf2(2n-1), chirp = conj(w),
   // bhat = FFT_M(b)/M
   int64_t m = 0;
@@ -335,6 +338,28 @@ int build_mixed(int dev, int64_t n, const std::vector<int> &rad, gdsp_plan *p) {
   return GDSP_OK;
 }
 
+// Lengths one kernel transforms per row: powers of 2 up to the LDS limit, or
+// the mixed-radix set.
+bool one_kernel_len(int64_t m) {
+  if (m < 2) return false;
+  if (is_pow2(m)) return ilog2(m) <= gdsp::kMaxLdsLog2;
+  std::vector<int> rad;
+  return mixed_radices(m, rad);
+}
+
+// n = n1 * n2 with both factors one-kernel lengths, n1 <= n2 as balanced as
+// possible (fewest, shortest transposes); false if none exists.
+bool mixed4_split(int64_t n, int64_t &n1, int64_t &n2) {
+  for (int64_t d = (int64_t)sqrtl((long double)n); d >= 2; --d) {
+    if (n % d == 0 && one_kernel_len(d) && one_kernel_len(n / d)) {
+      n1 = d;
+      n2 = n / d;
+      return true;
+    }
+  }
+  return false;
+}
+
 int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   p->device = dev;
   p->n = n;
@@ -349,6 +374,17 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   }
   std::vector<int> rad;
   if (!chirpz && mixed_radices(n, rad)) return build_mixed(dev, n, rad, p);
+  if (!chirpz && next_pow2_ref(2 * n - 1) > ((int64_t)1 << gdsp::kMaxLdsLog2) &&
+      mixed4_split(n, p->n1, p->n2)) {
+    // smooth n beyond one kernel, where Bluestein would be the composed
+    // multi-pass chain: four-step over one-kernel factors (5 passes; 3-3.5x
+    // faster than composed chirp-z at 10^4..10^6, while the fused chirp-z
+    // kernel still wins for n <= 8192: 3.5 vs 6.3 ms at n = 5000)
+    p->kind = KIND_MIXED4;
+    STCHK(get_plan_locked(dev, p->n1, &p->p1));
+    STCHK(get_plan_locked(dev, p->n2, &p->p2));
+    return upload_twiddles(dev, n, &p->tw);
+  }
   // Bluestein factors, bluestein.go:32-61: w_k = (cos, sin)(Pi/n * k*k),
   // k = 0 exactly 1 (angle not reduced, as the reference computes it).
   p->m = next_pow2_ref(2 * n - 1);
@@ -499,6 +535,46 @@ int exec_fourstep(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bo
   return GDSP_OK;
 }
 
+// Smooth non-power-of-2 n = N1*N2 beyond one kernel (x as N1 rows x N2
+// columns, n = N2*n1 + n2, k = k1 + N1*k2), every step a one-kernel pass:
+//   a  transpose x -> B (N2 x N1)                          (w1)
+//   b  DFT_N1 along B's rows                               (in place)
+//   c  transpose -> Y (N1 x N2), times W_N^(n2*k1)         (w2)
+//   d  DFT_N2 along Y's rows                               (in place)
+//   e  transpose -> X (N2 x N1), X[k1 + N1*k2] = Z[k1][k2] (out)
+// Inverse: inverse sub-transforms (1/N1 * 1/N2 = 1/N) and conj(W).
+// The reference runs these lengths through Bluestein (fft/bluestein.go).
+int exec_mixed4(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
+                hipStream_t s) {
+  const int64_t N = p->n, N1 = p->n1, N2 = p->n2;
+  const size_t bytes = (size_t)batch * (size_t)N * sizeof(cd);
+  DevBuf b1, b2;
+  STCHK(b1.alloc(bytes, s, SLOT_MX0));
+  STCHK(b2.alloc(bytes, s, SLOT_MX1));
+  cd *w1 = (cd *)b1.p, *w2 = (cd *)b2.p;
+  const cd *src = (const cd *)in;
+  if (load == gdsp::LOAD_REAL) {
+    HIPCHK(gdsp::launch_real_to_complex((const double *)in, w2, batch * N, s));
+    src = w2;
+  }
+  for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+    const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+    HIPCHK(gdsp::launch_transpose(src + b0 * N, w1 + b0 * N, N1, N2, s, nb));
+  }
+  STCHK(exec_plan(p->p1, w1, w1, batch * N2, inv, gdsp::LOAD_COMPLEX, s));
+  for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+    const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+    HIPCHK(gdsp::launch_transpose(w1 + b0 * N, w2 + b0 * N, N2, N1, s, nb, false, 1.0, p->tw, N,
+                                  inv));
+  }
+  STCHK(exec_plan(p->p2, w2, w2, batch * N1, inv, gdsp::LOAD_COMPLEX, s));
+  for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+    const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+    HIPCHK(gdsp::launch_transpose(w2 + b0 * N, out + b0 * N, N1, N2, s, nb));
+  }
+  return GDSP_OK;
+}
+
 int exec_bluestein_composed(const gdsp_plan *p, const cd *in, cd *out, int64_t batch, bool inv,
                             hipStream_t s) {
   DevBuf a;
@@ -537,6 +613,8 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
     case KIND_MIXED:
       HIPCHK(gdsp::launch_fft_mixed(p->md, inv, load, in, out, batch, p->tw, scale, s));
       return GDSP_OK;
+    case KIND_MIXED4:
+      return exec_mixed4(p, in, out, batch, inv, load, s);
     case KIND_LDS:
       HIPCHK(gdsp::launch_fft_lds(p->log2n, inv, load, lds_split_default(), in, out, batch, p->tw,
                                   scale, s));

@@ -57,9 +57,11 @@ hipError_t launch_colfft(int log2l, bool conj_in, int twiddle, bool conj_scale_o
                          int64_t out_step, int64_t out_stride, const cd *twl, const cd *twr,
                          int log2r, double scale, int64_t batch, int64_t mat_stride,
                          hipStream_t s);
-// batch <= 65535 matrices of rows x cols, consecutive
+// batch <= 65535 matrices of rows x cols, consecutive; optional conj+scale
+// out, and twiddle tw[r*c] (source row r, column c; needs r*c < twn)
 hipError_t launch_transpose(const cd *in, cd *out, int64_t rows, int64_t cols, hipStream_t s,
-                            int64_t batch = 1, bool conj_scale = false, double scale = 1.0);
+                            int64_t batch = 1, bool conj_scale = false, double scale = 1.0,
+                            const cd *tw = nullptr, int64_t twn = 0, bool tw_conj = false);
 hipError_t launch_real_to_complex(const double *in, cd *out, int64_t count, hipStream_t s);
 hipError_t launch_chirp_premul(const cd *in, cd *a, int64_t n, int64_t m, int64_t batch,
                                const cd *chirp, bool conj_in, hipStream_t s);

@@ -59,8 +59,9 @@ int gdsp_device_count(void);
 
 /* fft.FFT — fft/fft.go:72-87. n <= 1 copies; power of 2 → Stockham radix-16
  * kernels (reference: radix2FFT, fft/radix2.go:80-154); other n whose prime
- * factors are all <= 13 (n <= 4096) → a mixed-radix Stockham kernel computing
- * the same DFT directly; otherwise Bluestein (fft/bluestein.go:68-94).
+ * factors are all <= 13 → a mixed-radix Stockham kernel (n <= 4096) or, above
+ * 8192, a four-step over two such factors, computing the same DFT directly;
+ * otherwise Bluestein (fft/bluestein.go:68-94).
  * x, out: n complex128. */
 int gdsp_fft(const double *x, double *out, int64_t n);
 
@@ -164,7 +165,8 @@ int gdsp_plan_create_chirpz(int64_t n, gdsp_plan **plan);
 /* Which algorithm a plan runs: 0 trivial (n<=1), 1 one-kernel LDS Stockham,
  * 2 multi-pass global Stockham (large power of 2), 3 fused Bluestein,
  * 4 composed Bluestein (M > 16384), 5 one-kernel mixed radix (non-power-of-2
- * n <= 4096 whose prime factors are all <= 13). */
+ * n <= 4096 whose prime factors are all <= 13), 6 mixed four-step (such n
+ * above 8192 = n1*n2 with one-kernel factors: transposes + row kernels). */
 int gdsp_plan_kind(const gdsp_plan *plan);
 
 /* Batched C2C on device buffers: d_in/d_out hold batch*n complex128 (may

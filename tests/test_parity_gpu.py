@@ -254,7 +254,9 @@ def test_plan_kinds(gdsp):
     assert D.plan(1 << 16).kind == 2
     assert D.plan(3000).kind == 5  # 2^3 3 5^3: mixed radix
     assert D.plan(4097).kind == 3  # 17 * 241: fused Bluestein
-    assert D.plan(10000).kind == 4  # > 4096, M = 32768: composed Bluestein
+    assert D.plan(10000).kind == 6  # 100 x 100: mixed four-step
+    assert D.plan(5000).kind == 3  # smooth but M = 16384: the fused chirp-z is faster
+    assert D.plan(8209).kind == 4  # prime, M = 32768: composed Bluestein
     assert D.plan(3000, chirpz=True).kind == 3
     assert D.plan(10000, chirpz=True).kind == 4
     assert D.plan(4096, chirpz=True).kind == 3  # forced chirp-z on a power of 2
@@ -294,6 +296,35 @@ def test_chirpz_plan_vs_oracle(gdsp, oracle, n):
     assert row_nrel(yc, ref) < TOL and row_nrel(yd, ref) < TOL
     yci = D.fft_batch(xt, inverse=True, chirpz=True).cpu().numpy()
     assert row_nrel(yci, oracle.ifft_rows(x)) < TOL
+
+
+# smooth lengths beyond one kernel: four-step over one-kernel factors
+# (audio rates 44100 = 210^2, 48000; 2^16 * 3; 10^6) and neighbours that are
+# not smooth (8209 prime, 4100 = 4 * 25 * 41) and stay Bluestein
+MIXED4 = [4100, 5000, 6000, 8190, 10000, 44100, 48000, 3 << 16, 8209, 100000, 1000000]
+
+
+@pytest.mark.parametrize("n", MIXED4)
+def test_mixed_fourstep_vs_oracle(gdsp, oracle, n):
+    rng = np.random.default_rng(3000 + n)
+    batch = 3 if n <= 100000 else 1
+    x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
+    assert row_nrel(gdsp.fft.FFTBatch(x), oracle.fft_rows(x)) < TOL
+    assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL
+    xr = rng.uniform(-1, 1, (batch, n))
+    assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
+
+
+def test_mixed_fourstep_in_place_device(gdsp, oracle):
+    # device API with in == out and a batch that spans transposes' tails
+    import torch
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    n, batch = 44100, 5
+    x = oracle.fill_uniform(2 * n * batch, 0x5EED, 7).view(np.complex128).reshape(batch, n)
+    xt = torch.from_numpy(x).cuda()
+    D.fft_batch(xt, out=xt)
+    assert D.plan(n).kind == 6
+    assert row_nrel(xt.cpu().numpy(), oracle.fft_rows(x)) < TOL
 
 
 def test_mixed_radix_large_batch(gdsp, oracle):
