@@ -824,13 +824,6 @@ int gdsp_fft2_device(const void *d_in, void *d_out, int64_t rows, int64_t cols, 
   return GDSP_OK;
 }
 
-// fft.FFTN / IFFTN (fft/fft.go:157-192): the 1-D transform along every line
-// of dimension 0, then 1, ... of a row-major array. Per axis (length L,
-// `inner` elements after it, `outer` before): contiguous lines (inner = 1) go
-// to the batched row kernels; strided power-of-2 lines to the column-tile
-// kernels batched over `outer` (one pass for L <= 512, the four-step split
-// above); anything else through a batched transpose, the row kernels and a
-// transpose back.
 // One axis of computeFFTN (fft/fft.go:172-185): the 1-D transform of the
 // `outer` x `inner` lines of length L, read from src (cur itself, or the
 // caller's input for the first axis), result in cur; other is scratch.
@@ -871,61 +864,6 @@ static int fft_axis(const cd *src, cd *cur, cd *other, int64_t L, int64_t inner,
   for (int64_t o0 = 0; o0 < outer; o0 += 65535) {
     const int64_t nb = outer - o0 < 65535 ? outer - o0 : 65535;
     HIPCHK(gdsp::launch_transpose(src + o0 * L * inner, other + o0 * L * inner, L, inner, s, nb));
-  }
-  STCHK(exec_plan(pl, other, other, outer * inner, inv, gdsp::LOAD_COMPLEX, s));
-  for (int64_t o0 = 0; o0 < outer; o0 += 65535) {
-    const int64_t nb = outer - o0 < 65535 ? outer - o0 : 65535;
-    HIPCHK(gdsp::launch_transpose(other + o0 * L * inner, cur + o0 * L * inner, inner, L, s, nb));
-  }
-  return GDSP_OK;
-}
-
-// fft.FFTN / IFFTN (fft/fft.go:157-192): the 1-D transform along every line
-// of dimension 0, then 1, ... of a row-major array. Per axis (length L,
-// `inner` elements after it, `outer` before): contiguous lines (inner = 1) go
-// to the batched row kernels; strided power-of-2 lines to the column-tile
-// kernels batched over `outer` (one pass for L <= 512, the four-step split
-// above); anything else through a batched transpose, the row kernels and a
-// transpose back.
-// One axis of computeFFTN (fft/fft.go:172-185): the 1-D transform of the
-// `outer` x `inner` lines of length L. The result lands in cur, or in other
-// when the four-step split ends there (then the two are swapped).
-static int fft_axis(cd *&cur, cd *&other, int64_t L, int64_t inner, int64_t outer, bool inv,
-                    hipStream_t s) {
-  if (L == 1) return GDSP_OK;
-  gdsp_plan *pl = nullptr;
-  STCHK(get_plan(L, &pl));
-  if (inner == 1) {
-    STCHK(exec_plan(pl, cur, cur, outer, inv, gdsp::LOAD_COMPLEX, s));
-    return GDSP_OK;
-  }
-  const int lL = ilog2(L);
-  const double sc = 1.0 / (double)L;
-  if (is_pow2(L) && lL >= gdsp::kColMinLog2 && lL <= 2 * gdsp::kColMaxLog2) {
-    const int l1 = lL <= gdsp::kColMaxLog2 ? lL : lL / 2, l2 = lL - l1;
-    gdsp_plan *p1 = nullptr, *p2 = nullptr;
-    STCHK(get_plan((int64_t)1 << l1, &p1));
-    if (l2) STCHK(get_plan((int64_t)1 << l2, &p2));
-    const int64_t R1 = (int64_t)1 << l1, R2 = (int64_t)1 << l2;
-    for (int64_t o0 = 0; o0 < outer; o0 += 65535) {
-      const int64_t nb = outer - o0 < 65535 ? outer - o0 : 65535;
-      cd *c0 = cur + o0 * L * inner, *t0 = other + o0 * L * inner;
-      if (!l2) {
-        HIPCHK(gdsp::launch_colfft(lL, inv, 0, inv, c0, c0, inner, 1, 0, 1, 0, 1, pl->tw,
-                                   nullptr, lL, sc, nb, L * inner, s));
-      } else {
-        HIPCHK(gdsp::launch_colfft(l1, inv, 1, false, c0, c0, inner, R2, 1, R2, 1, R2, p1->tw,
-                                   pl->tw, lL, 1.0, nb, L * inner, s));
-        HIPCHK(gdsp::launch_colfft(l2, false, 0, inv, c0, t0, inner, R1, R2, 1, 1, R1, p2->tw,
-                                   nullptr, lL, sc, nb, L * inner, s));
-      }
-    }
-    if (l2) std::swap(cur, other);
-    return GDSP_OK;
-  }
-  for (int64_t o0 = 0; o0 < outer; o0 += 65535) {
-    const int64_t nb = outer - o0 < 65535 ? outer - o0 : 65535;
-    HIPCHK(gdsp::launch_transpose(cur + o0 * L * inner, other + o0 * L * inner, L, inner, s, nb));
   }
   STCHK(exec_plan(pl, other, other, outer * inner, inv, gdsp::LOAD_COMPLEX, s));
   for (int64_t o0 = 0; o0 < outer; o0 += 65535) {
