@@ -35,6 +35,13 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (tools/fp64peak.hip measures 67.3 FMA-only)
+# kernels whose FP64 work is taken from the committed SQ counter passes
+# (profiles/r01/sq_counters.json: 64 x (2 FMA + ADD + MUL) F64 instructions)
+SQ_KERNELS = {"radix4096": ["fft_lds_kernel<12"], "bluestein3000": ["fft_mixed_fixed_kernel"],
+              "chirpz3000": ["bluestein_kernel<13"], "pwelch": ["pwelch_half_kernel<12"],
+              "fft2_8192": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"],
+              "fft2_dist": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"]}
 SEED = 0x5EED
 
 
@@ -206,6 +213,8 @@ def main():
         with open(pmc) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
 
+    fp64 = fp64_info(w, avg_launch_s)
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(w, args.cpu_seconds)
@@ -230,12 +239,35 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                          "alg_bytes_per_launch": alg_bytes, "traffic": traffic},
+            "fp64": fp64,
             "cpu_baseline": cpu,
             "parity": check,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def fp64_info(workload: str, launch_s: float):
+    """FP64 work of one launch (from the committed SQ counters, FFT2 summed
+    over its kernels) against the FP64 vector peak — the second roofline of
+    the compute-heavy paths (chirp-z, Pwelch)."""
+    path = os.path.join(REPO, "profiles", "r01", "sq_counters.json")
+    ks = SQ_KERNELS.get("fft2_8192" if workload == "fft2_dist" else workload)
+    if not ks or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        sq = json.load(f).get("fft2_8192" if workload == "fft2_dist" else workload, {})
+    flop = 0.0
+    for k in ks:
+        hit = [v for name, v in sq.items() if k in name]
+        if not hit:
+            return None
+        flop += hit[0]["f64_flop"]
+    tf = flop / launch_s / 1e12
+    return {"flop_per_launch": flop, "achieved_tflops": round(tf, 2),
+            "peak_tflops": FP64_PEAK_TFLOPS, "frac": round(tf / FP64_PEAK_TFLOPS, 4),
+            "source": "profiles/r01/sq_counters.json (SQ_INSTS_VALU_{FMA,ADD,MUL}_F64)"}
 
 
 def cpu_baseline(workload: str, seconds: float):

@@ -64,4 +64,4 @@ def main(tag, workloads):
 
 if __name__ == "__main__":
     main(sys.argv[1] if len(sys.argv) > 1 else "r01",
-         sys.argv[2:] or ["radix4096", "bluestein3000", "pwelch", "fft2_8192"])
+         sys.argv[2:] or ["radix4096", "bluestein3000", "chirpz3000", "pwelch", "fft2_8192"])
