@@ -298,8 +298,13 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
 // register footprint (226 -> 128 VGPRs for M = 8192) and halves occupancy.
 template <class T>
 __device__ __forceinline__ T *opaque_ptr(T *p) {
-  asm volatile("" : "+s"(p));
-  return p;
+  // global-memory pointers only: laundered as an address_space(1) pointer,
+  // so the loads through it stay global_load (a laundered generic pointer
+  // becomes flat_load, which also counts in lgkmcnt and makes every LDS wait
+  // wait for the HBM loads in flight)
+  __attribute__((address_space(1))) T *q = (__attribute__((address_space(1))) T *)p;
+  asm volatile("" : "+s"(q));
+  return (T *)q;
 }
 __device__ __forceinline__ int opaque_int(int v) {
   asm volatile("" : "+v"(v));
@@ -310,14 +315,18 @@ __device__ __forceinline__ int opaque_int(int v) {
 template <int LOG2N, int LOG2E = 4>
 using RegArr = cd[Geo<LOG2N, LOG2E>::E];
 
-template <int LOG2N, bool SPLIT, bool OPAQUE = false, int LOG2E = 4, int ILV = 0, int P = 0>
-__device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t,
-                                         const cd *__restrict__ tw, double *lre, double *lim,
-                                         bool first_exchange = true) {
+// OPAQUE: 0 none; 1 launder the thread index and the twiddle pointer (no
+// address or twiddle value survives from one call to the next); 2 launder
+// only the thread index — enough to keep twiddle loads inside a loop, and it
+// leaves an LDS twiddle pointer's address space visible (ds_read, not flat).
+template <int LOG2N, bool SPLIT, int OPAQUE = 0, int LOG2E = 4, int ILV = 0, int P = 0,
+          class TWP = const cd *>
+__device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw, double *lre,
+                                         double *lim, bool first_exchange = true) {
   using G = Geo<LOG2N, LOG2E>;
   if constexpr (OPAQUE && P == 0 && G::NPASS > 1) {
     t = opaque_int(t);
-    tw = opaque_ptr(tw);
+    if constexpr (OPAQUE == 1) tw = opaque_ptr(tw);
   }
   if constexpr (P < G::NPASS) {
     constexpr int R = G::radix(P);
@@ -330,7 +339,7 @@ __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t,
                                                             first_exchange && P == 1);
     }
     pass_compute<G::N, G::E, G::T, R, NS>(v, t, tw);
-    fft_regs<LOG2N, SPLIT, false, LOG2E, ILV, P + 1>(v, t, tw, lre, lim, first_exchange);
+    fft_regs<LOG2N, SPLIT, 0, LOG2E, ILV, P + 1, TWP>(v, t, tw, lre, lim, first_exchange);
   }
 }
 

@@ -233,7 +233,8 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_kernel(
 // E = 16 forced to 168 / 128 VGPRs (MINW 3 / 4) spills: 4.85 / 6.07 ms;
 // window re-read from L1/L2 (WMODE 1) with the split exchange 3.48 ms, with
 // a complex (two-buffer) exchange 3.45 ms.
-template <int LOG2F, int WMODE = 2, int MINW = 1, int LOG2E = 4, bool SPLIT = true>
+template <int LOG2F, int WMODE = 2, int MINW = 1, int LOG2E = 4, bool SPLIT = true,
+          bool PF = false>
 __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_kernel(
     const double *__restrict__ x, int64_t seg_begin, int64_t seg_end, int64_t pairs_per_worker,
     const double *__restrict__ win, const cd *__restrict__ tw, double *__restrict__ partial) {
@@ -241,7 +242,11 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_ker
   constexpr int E = G::E, H = E / 2;
   constexpr int64_t STRIDE = G::N / 2;
   constexpr int XD = (SPLIT ? 1 : 2) * G::LDS_DOUBLES;  // exchange buffer(s)
-  __shared__ double lds[XD + (WMODE == 2 ? G::N : 0)];
+  // PF: the pass twiddle bases (T_N[0 .. N/R_last)) live in LDS, so the only
+  // global loads in the loop are the samples, and the next pair's samples are
+  // prefetched while this pair's FFT runs (vmcnt then covers only them)
+  constexpr int TWN = PF ? G::N / G::radix(G::NPASS - 1) : 0;
+  __shared__ double lds[XD + (WMODE == 2 ? G::N : 0) + 2 * TWN];
   const int lt = threadIdx.x;
   const int slot = lt / G::T;
   const int t = lt & (G::T - 1);
@@ -256,8 +261,12 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_ker
     for (int k = 0; k < E; ++k) wv[k] = win[t + k * G::T];
   } else if constexpr (WMODE == 2) {
     for (int i = lt; i < G::N; i += G::WG) wl[i] = win[i];
-    __syncthreads();
   }
+  cd *twl = reinterpret_cast<cd *>(lds + XD + (WMODE == 2 ? G::N : 0));
+  if constexpr (PF) {
+    for (int i = lt; i < TWN; i += G::WG) twl[i] = tw[i];
+  }
+  if constexpr (WMODE == 2 || PF) __syncthreads();
   double acc[E];
 #pragma unroll
   for (int k = 0; k < E; ++k) acc[k] = 0.0;
@@ -270,19 +279,36 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_ker
 #pragma unroll
     for (int k = 0; k < H; ++k) carry[k] = (p0 < npairs) ? b[k * G::T] : 0.0;
   }
+  // samples of pair p: a[0..H) = carry, a[H..E) (shared with seg s0+1),
+  // c[0..H) = second half of seg s0+1 (= first half of the next pair)
+  auto load_pair = [&](int64_t p, double (&a2)[H], double (&c2)[H]) {
+    const bool active = p < npairs;
+    const int64_t s0 = seg_begin + 2 * p;
+    const bool has1 = active && (s0 + 1 < seg_end);
+    const double *b = opaque_ptr(x) + s0 * STRIDE + t;
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      a2[k] = active ? b[(H + k) * G::T] : 0.0;
+      c2[k] = has1 ? b[(E + k) * G::T] : 0.0;
+    }
+  };
+  double na2[H], nc2[H];  // PF: the next pair's samples, in flight
+  if constexpr (PF) load_pair(p0, na2, nc2);
   for (int64_t it = 0; it < pairs_per_worker; ++it) {
     const int64_t p = p0 + it;
     const bool active = p < npairs;
     const int64_t s0 = seg_begin + 2 * p;
     const bool has1 = active && (s0 + 1 < seg_end);
-    // samples of this pair: a[0..H) = carry, a[H..E) (shared with seg s0+1),
-    // c[0..H) = second half of seg s0+1 (= first half of the next pair)
-    const double *b = opaque_ptr(x) + s0 * STRIDE + t;
     double a2[H], c2[H];
+    if constexpr (PF) {
 #pragma unroll
-    for (int k = 0; k < H; ++k) {
-      a2[k] = active ? b[(H + k) * G::T] : 0.0;
-      c2[k] = has1 ? b[(E + k) * G::T] : 0.0;
+      for (int k = 0; k < H; ++k) {
+        a2[k] = na2[k];
+        c2[k] = nc2[k];
+      }
+      if (it + 1 < pairs_per_worker) load_pair(p + 1, na2, nc2);
+    } else {
+      load_pair(p, a2, c2);
     }
     if constexpr (WMODE == 1) {
       const double *w = opaque_ptr(win) + t;
@@ -302,7 +328,10 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_ker
     }
 #pragma unroll
     for (int k = 0; k < H; ++k) carry[k] = c2[k];
-    fft_regs<LOG2F, SPLIT, true, LOG2E>(v, opaque_int(t), tw, lre, lim, it == 0);
+    if constexpr (PF)
+      fft_regs<LOG2F, SPLIT, 2, LOG2E>(v, opaque_int(t), (const cd *)twl, lre, lim, it == 0);
+    else
+      fft_regs<LOG2F, SPLIT, 1, LOG2E>(v, opaque_int(t), tw, lre, lim, it == 0);
     if (active) {
 #pragma unroll
       for (int k = 0; k < E; ++k) acc[k] += v[k].x * v[k].x + v[k].y * v[k].y;
@@ -670,14 +699,15 @@ static hipError_t launch_pw_t(const double *x, int64_t nfft, int64_t stride, int
   return hipGetLastError();
 }
 
-template <int LOG2F, int WMODE = 2, int MINW = 1, int LOG2E = 4, bool SPLIT = true>
+template <int LOG2F, int WMODE = 2, int MINW = 1, int LOG2E = 4, bool SPLIT = true,
+          bool PF = false>
 static hipError_t launch_pwh_t(const double *x, int64_t seg_begin, int64_t seg_end, int64_t ppw,
                                int64_t nworkers, const double *win, const cd *tw, double *partial,
                                hipStream_t s) {
   using G = Geo<LOG2F, LOG2E>;
   if (G::TPW != Geo<LOG2F>::TPW) return hipErrorInvalidValue;  // workers per block
   const int64_t nblk = (nworkers + G::TPW - 1) / G::TPW;
-  hipLaunchKernelGGL((pwelch_half_kernel<LOG2F, WMODE, MINW, LOG2E, SPLIT>), dim3((unsigned)nblk), dim3(G::WG), 0, s,
+  hipLaunchKernelGGL((pwelch_half_kernel<LOG2F, WMODE, MINW, LOG2E, SPLIT, PF>), dim3((unsigned)nblk), dim3(G::WG), 0, s,
                      x, seg_begin, seg_end, ppw, win, tw, partial);
   return hipGetLastError();
 }
@@ -689,7 +719,11 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
 #define GDSP_PWH(L) \
   case L: return launch_pwh_t<L>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
     GDSP_PWH(5) GDSP_PWH(6) GDSP_PWH(7) GDSP_PWH(8) GDSP_PWH(9) GDSP_PWH(10) GDSP_PWH(11)
-    GDSP_PWH(12)
+    // F = 4096 (the BASELINE configuration): twiddle bases in LDS and the
+    // next pair prefetched (3.16 -> 3.11 ms; 244 VGPRs, still 2 waves/SIMD)
+    case 12:
+      return launch_pwh_t<12, 2, 1, 4, true, true>(x, seg_begin, seg_end, ppw, nworkers, win, tw,
+                                                   partial, s);
     GDSP_PWH(13)
 #undef GDSP_PWH
     // F = 16384: the exchange buffer alone takes 136 KiB, so the window is
