@@ -299,15 +299,19 @@ __device__ __attribute__((noinline)) void mixed_pass(int n, int ns, int t1, int 
   }
   // a middle pass overwrites the buffer it read: every read lands first
   if constexpr (MODE == MP_MID) __syncthreads();
+  // k = j % ns for j = tl + jj*t1, stepped instead of divided per butterfly
+  // (one division per pass; dk is uniform)
+  int k = FROM_HBM ? 0 : tl % ns;
+  const int dk = FROM_HBM ? 0 : t1 % ns;
 #pragma unroll
   for (int jj = 0; jj < J; ++jj) {
     const int j = tl + jj * t1;
+    if (jj > 0 && !FROM_HBM) {
+      k += dk;
+      if (k >= ns) k -= ns;
+    }
     if (valid && j < nb) {
-      int k = 0;
-      if constexpr (!FROM_HBM) {
-        k = j % ns;
-        twiddle_chain<R>(v[jj], tw[k]);
-      }
+      if constexpr (!FROM_HBM) twiddle_chain<R>(v[jj], tw[k]);
       dft_any<R>(v[jj]);
       const int o = (j - k) * R + k;
 #pragma unroll
