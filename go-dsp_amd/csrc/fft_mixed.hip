@@ -22,6 +22,8 @@
 
 #include <stdlib.h>
 
+#include <tuple>
+
 namespace gdsp {
 
 template <int R>
@@ -540,21 +542,31 @@ struct FixedGeo {
     return m;
   }
   static constexpr int T1 = need();
+  static constexpr int SLOTS = (N + 7) & ~7;
+  // transforms per workgroup: about 256 threads, within 64 KiB of LDS
+  static constexpr int tpw() {
+    int t = 256 / T1 > 1 ? 256 / T1 : 1;
+    while (t > 1 && t * SLOTS * 16 > 65536) --t;
+    return t;
+  }
+  static constexpr int TPW = tpw();
+  static constexpr int WG = TPW * T1;
 };
 
 template <bool INV, int LOAD, bool SPLIT, bool SWZ, int R0, int... RS>
-__global__ __launch_bounds__((FixedGeo<R0, RS...>::T1)) void fft_mixed_fixed_kernel(
+__global__ __launch_bounds__((FixedGeo<R0, RS...>::WG)) void fft_mixed_fixed_kernel(
     const void *__restrict__ in, cd *__restrict__ out, int64_t batch, const cd *__restrict__ tw,
     double scale) {
   using G = FixedGeo<R0, RS...>;
-  constexpr int SLOTS = (G::N + 7) & ~7;
-  __shared__ double lds[SPLIT ? SLOTS : 2 * SLOTS];
-  const int tl = threadIdx.x;
-  const int64_t row = xcd_remap(blockIdx.x, gridDim.x);
+  __shared__ double lds[G::TPW * (SPLIT ? G::SLOTS : 2 * G::SLOTS)];
+  const int sub = G::TPW == 1 ? 0 : (int)threadIdx.x / G::T1;
+  const int tl = (int)threadIdx.x - sub * G::T1;
+  const int64_t row = xcd_remap(blockIdx.x, gridDim.x) * G::TPW + sub;
   const bool valid = row < batch;
   const void *gin = LOAD == LOAD_REAL
                         ? (const void *)(reinterpret_cast<const double *>(in) + row * G::N)
                         : (const void *)(reinterpret_cast<const cd *>(in) + row * G::N);
+  double *ld = lds + sub * (SPLIT ? G::SLOTS : 2 * G::SLOTS);
   FPass<R0, G::N, 1, G::T1> p0;
   p0.template load_hbm<INV, LOAD>(tl, valid, gin);
   p0.compute(tl, valid, tw);
@@ -562,18 +574,22 @@ __global__ __launch_bounds__((FixedGeo<R0, RS...>::T1)) void fft_mixed_fixed_ker
     p0.template store_hbm<INV>(tl, valid, out + row * G::N, scale);
   else
     fixed_chain<INV, SPLIT, SWZ, G::N, G::T1, R0, 0, FPass<R0, G::N, 1, G::T1>, RS...>(
-        p0, tl, valid, out + row * G::N, lds, tw, scale);
+        p0, tl, valid, out + row * G::N, ld, tw, scale);
 }
 
-template <bool SPLIT, bool SWZ, int... RS>
+template <bool SPLIT, int... RS>
 static bool launch_fixed(const MixedDesc &d, bool inv, int load, const void *in, cd *out,
                          int64_t batch, const cd *tw, double scale, hipStream_t s) {
   using G = FixedGeo<RS...>;
+  // an odd first radix writes stride-R slots that are conflict-free as they
+  // are; an even one goes through the swizzle
+  constexpr int R0 = [] { constexpr int r[] = {RS...}; return r[0]; }();
+  constexpr bool SWZ = R0 % 2 == 0;
   uint64_t codes = 0;
   int q = 0;
   for (int r : {RS...}) codes |= (uint64_t)r << (5 * q++);
   if (d.n != G::N || d.codes != codes) return false;
-  const dim3 grid((unsigned)batch), block(G::T1);
+  const dim3 grid((unsigned)((batch + G::TPW - 1) / G::TPW)), block(G::WG);
   if (inv)
     hipLaunchKernelGGL((fft_mixed_fixed_kernel<true, LOAD_COMPLEX, SPLIT, SWZ, RS...>), grid,
                        block, 0, s, in, out, batch, tw, scale);
@@ -586,21 +602,53 @@ static bool launch_fixed(const MixedDesc &d, bool inv, int load, const void *in,
   return true;
 }
 
-// Radix lists of the compiled specialisations (launch_fft_mixed picks the
-// kernel by matching n and the list). GDSP_MIXED_GENERIC=1 disables them.
+// The compiled specialisations: radix lists of frequent lengths, each pass a
+// radix <= 25 so a length takes 3 passes (2 LDS exchanges).
+template <int... RS>
+struct Spec {};
+using Specs = std::tuple<Spec<25, 15, 8>,    // 3000 (BASELINE config 3)
+                         Spec<10, 10, 10>,   // 1000
+                         Spec<25, 5, 16>,    // 2000
+                         Spec<15, 10, 10>,   // 1500
+                         Spec<25, 6, 16>,    // 2400
+                         Spec<25, 3, 16>,    // 1200
+                         Spec<15, 8, 8>,     // 960
+                         Spec<15, 16, 8>,    // 1920
+                         Spec<15, 8, 4>,     // 480
+                         Spec<12, 16, 8>,    // 1536
+                         Spec<12, 16, 16>>;  // 3072
+
+template <int... RS>
+static bool spec_radices(Spec<RS...>, int n, int *rad, int *npass) {
+  if (n != (RS * ...)) return false;
+  int q = 0;
+  for (int r : {RS...}) rad[q++] = r;
+  *npass = q;
+  return true;
+}
+template <class... S>
+static bool find_spec(std::tuple<S...>, int n, int *rad, int *npass) {
+  return (spec_radices(S{}, n, rad, npass) || ...);
+}
+template <int... RS>
+static bool spec_launch(Spec<RS...>, const MixedDesc &d, bool inv, int load, const void *in,
+                        cd *out, int64_t batch, const cd *tw, double scale, hipStream_t s) {
+  return launch_fixed<false, RS...>(d, inv, load, in, out, batch, tw, scale, s);
+}
+template <class... S>
+static bool launch_spec(std::tuple<S...>, const MixedDesc &d, bool inv, int load, const void *in,
+                        cd *out, int64_t batch, const cd *tw, double scale, hipStream_t s) {
+  return (spec_launch(S{}, d, inv, load, in, out, batch, tw, scale, s) || ...);
+}
+
+// Radix list of the compiled specialisation for n, if there is one
+// (launch_fft_mixed picks the kernel by n and list). GDSP_MIXED_GENERIC=1
+// disables them. n = 3000: 1.10 ms per 65536 transforms for 25*15*8 against
+// 1.14-1.18 ms for the other orders of these radices and 1.82 ms for the
+// generic 8*5*5*5*3 kernel; a split (re/im) exchange measured 3-4 % slower.
 bool mixed_fixed_radices(int n, int *rad, int *npass) {
   if (getenv("GDSP_MIXED_GENERIC")) return false;
-  // n = 3000: measured 1.10 ms per 65536 transforms for 25*15*8 against
-  // 1.14-1.18 ms for the other orders of these radices, and 1.82 ms for the
-  // generic 8*5*5*5*3 kernel; the split (re/im) exchange measured 3-4 % slower
-  if (n == 3000) {
-    rad[0] = 25;
-    rad[1] = 15;
-    rad[2] = 8;
-    *npass = 3;
-    return true;
-  }
-  return false;
+  return find_spec(Specs{}, n, rad, npass);
 }
 
 hipError_t launch_fft_mixed(const MixedDesc &d, bool inv, int load, const void *in, cd *out,
@@ -609,10 +657,8 @@ hipError_t launch_fft_mixed(const MixedDesc &d, bool inv, int load, const void *
   if (d.t1 <= 0 || d.tpw <= 0 || d.t1 * d.tpw > 512) return hipErrorInvalidValue;
   const int64_t nblk = (batch + d.tpw - 1) / d.tpw;
   if (nblk > 0x7fffffff) return hipErrorInvalidValue;
-  // odd first radix: its stride-25 LDS writes are conflict-free unswizzled
-  if (batch <= 0x7fffffff &&
-      launch_fixed<false, false, 25, 15, 8>(d, inv, load, in, out, batch, tw, scale, s))
-    return hipGetLastError();
+  if (batch > (int64_t)0x7fffffff) return hipErrorInvalidValue;
+  if (launch_spec(Specs{}, d, inv, load, in, out, batch, tw, scale, s)) return hipGetLastError();
   const size_t lds = (size_t)d.tpw * (size_t)((d.n + 7) & ~7) * sizeof(cd);
   const dim3 grid((unsigned)nblk), block((unsigned)(d.t1 * d.tpw));
   if (inv) {

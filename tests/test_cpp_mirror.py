@@ -104,7 +104,7 @@ D = importlib.import_module("go-dsp_amd.device")
 import torch
 assert D.plan(3000).kind == 5
 rng = np.random.default_rng(3)
-for n in (3000, 1000, 12):
+for n in (3000, 1000, 2000, 1500, 2400, 1200, 960, 1920, 480, 1536, 3072, 12):
     x = rng.standard_normal((9, n)) + 1j * rng.standard_normal((9, n))
     for inv in (False, True):
         y = g.fft.FFTBatch(x, inverse=inv)

@@ -267,7 +267,9 @@ def test_plan_kinds(gdsp):
 MIXED = [3, 5, 6, 7, 10, 11, 12, 13, 14, 18, 20, 21, 22, 24, 25, 26, 27, 39, 48, 49, 60, 77,
          81, 96, 100, 121, 125, 143, 169, 243, 343, 360, 625, 720, 729, 1000, 1001, 1331, 1536,
          2048 + 1024, 2187, 2197, 2401, 2500, 3000, 3125, 3375, 3840, 4000, 4095, 4050, 19 * 5,
-         17 * 3]
+         17 * 3,
+         # the compiled specialisations (fft_mixed.hip Specs)
+         480, 960, 1200, 1500, 1920, 2000, 2400]
 
 
 @pytest.mark.parametrize("n", MIXED)
