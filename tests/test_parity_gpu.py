@@ -388,3 +388,36 @@ def test_fft2_sharded_one_rank(gdsp, oracle):
         for inv in (False, True):
             y = Dd.fft2_sharded(torch.from_numpy(x).cuda(), R, inverse=inv).cpu().numpy()
             assert nrel(y, oracle.fft2(x, inverse=inv)) < TOL, (R, C, inv)
+
+
+def test_concurrent_host_calls(gdsp, oracle):
+    # the reference's FFT is safe to call from many goroutines (RWMutex-guarded
+    # caches): host-pointer calls from 8 threads at once, each
+    # with its own lengths (plan builds race on first use), all correct
+    import threading
+    sizes = [4096, 3000, 1000, 8192, 100, 5000, 44100, 17]
+    errs, fails = {}, []
+
+    def work(i):
+        try:
+            n = sizes[i]
+            rng = np.random.default_rng(50 + i)
+            for _ in range(6):
+                x = rng.standard_normal((2, n)) + 1j * rng.standard_normal((2, n))
+                y = gdsp.fft.FFTBatch(x)
+                z = gdsp.fft.FFTBatch(y, inverse=True)
+                e = max(row_nrel(y, oracle.fft_rows(x)), row_nrel(z, x))
+                errs[i] = max(errs.get(i, 0.0), e)
+            p, _ = gdsp.spectral.Pwelch(rng.standard_normal(3000), 1.0,
+                                        gdsp.spectral.PwelchOptions(NFFT=256))
+            assert np.all(np.isfinite(p))
+        except Exception as ex:  # surfaced below
+            fails.append((i, repr(ex)))
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(len(sizes))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not fails, fails
+    assert max(errs.values()) < TOL, errs
