@@ -371,29 +371,41 @@ __global__ void reduce_partials_l2(const double *__restrict__ chunk_sums, int64_
 
 // Materialised Pwelch path (any segment length): windowed, zero-padded real
 // segments as complex rows.
+// Materialised Pwelch: row r of buf = windowed segments seg0 + 2r (real part)
+// and seg0 + 2r + 1 (imaginary part, zero past seg_end), zero-padded to flen
+// — the same packed pairs as the fused kernels.
 __global__ void segments_to_complex_kernel(const double *__restrict__ x, int64_t nfft,
                                            int64_t flen, int64_t stride, int64_t seg0,
-                                           int64_t nseg, const double *__restrict__ win,
+                                           int64_t seg_end, int64_t nrows,
+                                           const double *__restrict__ win,
                                            cd *__restrict__ buf) {
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= nseg * flen) return;
-  const int64_t s = tid / flen;
-  const int64_t i = tid - s * flen;
-  const double a = i < nfft ? x[(seg0 + s) * stride + i] * win[i] : 0.0;
-  buf[tid] = {a, 0.0};
+  if (tid >= nrows * flen) return;
+  const int64_t r = tid / flen;
+  const int64_t i = tid - r * flen;
+  const int64_t s = seg0 + 2 * r;
+  double a = 0.0, b = 0.0;
+  if (i < nfft) {
+    a = x[s * stride + i] * win[i];
+    if (s + 1 < seg_end) b = x[(s + 1) * stride + i] * win[i];
+  }
+  buf[tid] = {a, b};
 }
 
-// acc[k] += sum_s |buf[s][k]|^2
-__global__ void power_accumulate_kernel(const cd *__restrict__ buf, int64_t nseg, int64_t flen,
-                                        double *__restrict__ acc) {
+// partial[c][k] = sum over rows [c*rpp, (c+1)*rpp) of |buf[row][k]|^2
+// (grid: bins x parts; reduced in fixed order by reduce_partials)
+__global__ void power_partials_kernel(const cd *__restrict__ buf, int64_t nrows, int64_t flen,
+                                      int64_t rpp, double *__restrict__ partial) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t c = blockIdx.y;
   if (k >= flen) return;
+  const int64_t r0 = c * rpp, r1 = r0 + rpp < nrows ? r0 + rpp : nrows;
   double s = 0.0;
-  for (int64_t r = 0; r < nseg; ++r) {
+  for (int64_t r = r0; r < r1; ++r) {
     const cd z = buf[r * flen + k];
     s += z.x * z.x + z.y * z.y;
   }
-  acc[k] += s;
+  partial[c * flen + k] = s;
 }
 
 // ----------------------------------------------------------------------------
@@ -772,17 +784,19 @@ int64_t reduce_scratch_doubles(int64_t nworkers, int64_t F) {
 }
 
 hipError_t launch_segments_to_complex(const double *x, int64_t nfft, int64_t flen, int64_t stride,
-                                      int64_t seg0, int64_t nseg, const double *win, cd *buf,
-                                      hipStream_t s) {
-  hipLaunchKernelGGL(segments_to_complex_kernel, dim3(blocks_for(nseg * flen, 256)), dim3(256), 0,
-                     s, x, nfft, flen, stride, seg0, nseg, win, buf);
+                                      int64_t seg0, int64_t seg_end, int64_t nrows,
+                                      const double *win, cd *buf, hipStream_t s) {
+  hipLaunchKernelGGL(segments_to_complex_kernel, dim3(blocks_for(nrows * flen, 256)), dim3(256),
+                     0, s, x, nfft, flen, stride, seg0, seg_end, nrows, win, buf);
   return hipGetLastError();
 }
 
-hipError_t launch_power_accumulate(const cd *buf, int64_t nseg, int64_t flen, double *acc,
-                                   hipStream_t s) {
-  hipLaunchKernelGGL(power_accumulate_kernel, dim3(blocks_for(flen, 256)), dim3(256), 0, s, buf,
-                     nseg, flen, acc);
+hipError_t launch_power_partials(const cd *buf, int64_t nrows, int64_t flen, int64_t rpp,
+                                 double *partial, hipStream_t s) {
+  const int64_t parts = (nrows + rpp - 1) / rpp;
+  if (parts > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(power_partials_kernel, dim3(blocks_for(flen, 256), (unsigned)parts),
+                     dim3(256), 0, s, buf, nrows, flen, rpp, partial);
   return hipGetLastError();
 }
 

@@ -1057,18 +1057,29 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
                                         (double *)red.p, s));
     return GDSP_OK;
   }
-  // materialised path: windowed segments as complex rows, batched FFT, |X|^2
-  int64_t chunk = ((int64_t)1 << 24) / flen;
-  if (chunk < 1) chunk = 1;
-  if (chunk > nseg) chunk = nseg;
-  DevBuf buf;
-  STCHK(buf.alloc((size_t)chunk * (size_t)flen * sizeof(cd), s, SLOT_PW_BUF));
-  for (int64_t s0 = seg_begin; s0 < seg_end; s0 += chunk) {
-    const int64_t ns = (seg_end - s0) < chunk ? (seg_end - s0) : chunk;
-    HIPCHK(gdsp::launch_segments_to_complex(d_x, nfft, flen, stride, s0, ns, d_win_seg,
-                                            (cd *)buf.p, s));
-    STCHK(exec_plan(p, buf.p, (cd *)buf.p, ns, false, gdsp::LOAD_COMPLEX, s));
-    HIPCHK(gdsp::launch_power_accumulate((const cd *)buf.p, ns, flen, d_acc, s));
+  // materialised path (lengths without a fused kernel): packed segment pairs
+  // as complex rows, the batched FFT of the plan, per-bin partial power sums,
+  // deterministic reduction into acc
+  const int64_t nrows_all = (nseg + 1) / 2;
+  int64_t rows = ((int64_t)1 << 25) / flen;  // 512 MiB of rows per chunk
+  constexpr int64_t kRpp = 64;
+  if (rows < 1) rows = 1;
+  if (rows > 65535 * kRpp) rows = 65535 * kRpp;  // partial-sum grid limit
+  if (rows > nrows_all) rows = nrows_all;
+  const int64_t parts = (rows + kRpp - 1) / kRpp;
+  DevBuf buf, part, red;
+  STCHK(buf.alloc((size_t)rows * (size_t)flen * sizeof(cd), s, SLOT_PW_BUF));
+  STCHK(part.alloc((size_t)parts * (size_t)flen * sizeof(double), s, SLOT_PW_PART));
+  STCHK(red.alloc((size_t)gdsp::reduce_scratch_doubles(parts, flen) * sizeof(double), s,
+                  SLOT_PW_RED));
+  for (int64_t r0 = 0; r0 < nrows_all; r0 += rows) {
+    const int64_t nr = (nrows_all - r0) < rows ? (nrows_all - r0) : rows;
+    HIPCHK(gdsp::launch_segments_to_complex(d_x, nfft, flen, stride, seg_begin + 2 * r0, seg_end,
+                                            nr, d_win_seg, (cd *)buf.p, s));
+    STCHK(exec_plan(p, buf.p, (cd *)buf.p, nr, false, gdsp::LOAD_COMPLEX, s));
+    HIPCHK(gdsp::launch_power_partials((const cd *)buf.p, nr, flen, kRpp, (double *)part.p, s));
+    HIPCHK(gdsp::launch_reduce_partials((const double *)part.p, (nr + kRpp - 1) / kRpp, flen,
+                                        d_acc, (double *)red.p, s));
   }
   return GDSP_OK;
 }

@@ -44,11 +44,13 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
 hipError_t launch_reduce_partials(const double *partial, int64_t nworkers, int64_t F, double *acc,
                                   double *scratch, hipStream_t s);
 int64_t reduce_scratch_doubles(int64_t nworkers, int64_t F);
+// materialised Pwelch: packed segment pairs (nrows rows of flen), then
+// per-bin partial power sums over parts of rpp rows (<= 65535 parts)
 hipError_t launch_segments_to_complex(const double *x, int64_t nfft, int64_t flen, int64_t stride,
-                                      int64_t seg0, int64_t nseg, const double *win, cd *buf,
-                                      hipStream_t s);
-hipError_t launch_power_accumulate(const cd *buf, int64_t nseg, int64_t flen, double *acc,
-                                   hipStream_t s);
+                                      int64_t seg0, int64_t seg_end, int64_t nrows,
+                                      const double *win, cd *buf, hipStream_t s);
+hipError_t launch_power_partials(const cd *buf, int64_t nrows, int64_t flen, int64_t rpp,
+                                 double *partial, hipStream_t s);
 // FFT2 column pass on row-segment tiles; 4 <= log2l <= 9 (see fft_kernels.hip)
 constexpr int kColMinLog2 = 4, kColMaxLog2 = 9;
 // twiddle: 0 none, 1 W_R^(group*j), 2 W_R^(col*j)
