@@ -277,7 +277,7 @@ __device__ __attribute__((noinline)) void mixed_pass(int n, int ns, int t1, int 
                                                      const cd *__restrict__ tw, double scale) {
   constexpr bool FROM_HBM = MODE == MP_FIRST || MODE == MP_SINGLE;
   constexpr bool TO_HBM = MODE == MP_LAST || MODE == MP_SINGLE;
-  constexpr int J = 16 / R;
+  constexpr int J = R > 16 ? 1 : 16 / R;
   const int nb = n / R;
   cd v[J][R];
 #pragma unroll
@@ -330,6 +330,10 @@ __device__ __attribute__((noinline)) void mixed_pass(int n, int ns, int t1, int 
   }
 }
 
+// the radices of the generic lists (the runtime-radix kernels; compiled
+// specialisations with composite radices have their own kernels)
+#define GDSP_FOR_RADICES(X) X(2) X(3) X(4) X(5) X(7) X(8) X(11) X(13) X(16)
+
 template <bool INV, int LOAD, int MODE>
 __device__ __forceinline__ void mixed_dispatch(int R, int n, int ns, int t1, int tl, bool valid,
                                                const void *gin, cd *gout, cd *lds, const cd *tw,
@@ -339,15 +343,7 @@ __device__ __forceinline__ void mixed_dispatch(int R, int n, int ns, int t1, int
   case RR:                                                                                  \
     mixed_pass<RR, INV, LOAD, MODE>(n, ns, t1, tl, valid, gin, gout, lds, tw, scale);       \
     break;
-    GDSP_MIXED_CASE(2)
-    GDSP_MIXED_CASE(3)
-    GDSP_MIXED_CASE(4)
-    GDSP_MIXED_CASE(5)
-    GDSP_MIXED_CASE(7)
-    GDSP_MIXED_CASE(8)
-    GDSP_MIXED_CASE(11)
-    GDSP_MIXED_CASE(13)
-    GDSP_MIXED_CASE(16)
+    GDSP_FOR_RADICES(GDSP_MIXED_CASE)
 #undef GDSP_MIXED_CASE
     default:
       break;
@@ -392,6 +388,154 @@ __global__ __launch_bounds__(512) void fft_mixed_kernel(const void *__restrict__
     twoff += ns;
     ns *= R;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Fused Pwelch over a mixed-radix segment length (spectral/pwelch.go:104-122
+// for NFFT / Pad that are not powers of 2): the same packed segment pairs
+// z = w*x_s + i*w*x_{s+1} and per-bin |Z_k|^2 sums as the power-of-2 kernels
+// (finalize folds k and F-k), on the runtime-radix passes above. One
+// transform per workgroup, persistent over a contiguous range of pairs; the
+// per-bin sums live in LDS, each bin written by the one thread whose last
+// pass produces it, so they need no synchronisation.
+template <int R>
+__device__ __attribute__((noinline)) void pw_first_pass(int flen, int nfft, int t1, int tl,
+                                                        bool active, bool has1,
+                                                        const double *__restrict__ x0,
+                                                        const double *__restrict__ x1,
+                                                        const double *__restrict__ win,
+                                                        cd *lds) {
+  constexpr int J = R > 16 ? 1 : 16 / R;
+  const int nb = flen / R;
+  cd v[J][R];
+#pragma unroll
+  for (int jj = 0; jj < J; ++jj) {
+    const int j = tl + jj * t1;
+    if (j < nb) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int i = j + r * nb;
+        double a = 0.0, b = 0.0;
+        if (active && i < nfft) {
+          const double w = win[i];
+          a = w * x0[i];
+          if (has1) b = w * x1[i];
+        }
+        v[jj][r] = {a, b};
+      }
+      dft_any<R>(v[jj]);
+#pragma unroll
+      for (int r = 0; r < R; ++r) lds[lsw(j * R + r)] = v[jj][r];
+    }
+  }
+}
+
+template <int R>
+__device__ __attribute__((noinline)) void pw_last_pass(int flen, int t1, int tl, bool active,
+                                                       cd *lds, const cd *__restrict__ tw,
+                                                       double *lacc) {
+  constexpr int J = R > 16 ? 1 : 16 / R;
+  const int nb = flen / R;  // = Ns of the last pass: butterfly j writes bins j + r*nb
+  cd v[J][R];
+#pragma unroll
+  for (int jj = 0; jj < J; ++jj) {
+    const int j = tl + jj * t1;
+    if (j < nb) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[jj][r] = lds[lsw(j + r * nb)];
+    }
+  }
+#pragma unroll
+  for (int jj = 0; jj < J; ++jj) {
+    const int j = tl + jj * t1;
+    if (j < nb) {
+      twiddle_chain<R>(v[jj], tw[j]);
+      dft_any<R>(v[jj]);
+      if (active) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          lacc[j + r * nb] += v[jj][r].x * v[jj][r].x + v[jj][r].y * v[jj][r].y;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(512) void pwelch_mixed_kernel(
+    const double *__restrict__ x, int64_t nfft, int64_t stride, int64_t seg_begin,
+    int64_t seg_end, int64_t pairs_per_worker, MixedDesc d, const double *__restrict__ win,
+    const cd *__restrict__ tw, double *__restrict__ partial) {
+  extern __shared__ double pw_lds[];
+  const int flen = d.n, slots = (flen + 7) & ~7;
+  cd *lds = reinterpret_cast<cd *>(pw_lds);
+  double *lacc = pw_lds + 2 * slots;
+  const int tl = threadIdx.x, t1 = d.t1;
+  for (int i = tl; i < flen; i += t1) lacc[i] = 0.0;
+  const int64_t worker = blockIdx.x;
+  const int64_t p0 = worker * pairs_per_worker;
+  const int64_t npairs = (seg_end - seg_begin + 1) / 2;
+  const int np = d.npass;
+  for (int64_t it = 0; it < pairs_per_worker; ++it) {
+    const int64_t p = p0 + it;
+    const bool active = p < npairs;
+    const int64_t s0 = seg_begin + 2 * (active ? p : 0);
+    const bool has1 = active && s0 + 1 < seg_end;
+    const double *x0 = x + s0 * stride, *x1 = x0 + stride;
+    __syncthreads();  // the previous pair's last-pass reads are done
+    int R = (int)(d.codes & 31);
+    switch (R) {
+#define GDSP_PW_FIRST(RR)                                                                 \
+  case RR:                                                                                \
+    pw_first_pass<RR>(flen, (int)nfft, t1, tl, active, has1, x0, x1, win, lds);           \
+    break;
+      GDSP_FOR_RADICES(GDSP_PW_FIRST)
+#undef GDSP_PW_FIRST
+      default:
+        break;
+    }
+    int ns = R, twoff = 0;
+    for (int q = 1; q < np; ++q) {
+      R = (int)((d.codes >> (5 * q)) & 31);
+      __syncthreads();
+      if (q < np - 1) {
+        mixed_dispatch<false, LOAD_COMPLEX, MP_MID>(R, flen, ns, t1, tl, true, nullptr, nullptr,
+                                                    lds, tw + twoff, 1.0);
+      } else {
+        switch (R) {
+#define GDSP_PW_LAST(RR)                                                                   \
+  case RR:                                                                                 \
+    pw_last_pass<RR>(flen, t1, tl, active, lds, tw + twoff, lacc);                         \
+    break;
+          GDSP_FOR_RADICES(GDSP_PW_LAST)
+#undef GDSP_PW_LAST
+          default:
+            break;
+        }
+      }
+      twoff += ns;
+      ns *= R;
+    }
+  }
+  __syncthreads();
+  if (p0 < npairs)
+    for (int i = tl; i < flen; i += t1) partial[worker * flen + i] = lacc[i];
+}
+
+hipError_t launch_pwelch_mixed(const MixedDesc &d, const double *x, int64_t nfft, int64_t stride,
+                               int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,
+                               const double *win, const cd *tw, double *partial, hipStream_t s) {
+  if (d.npass < 2 || d.t1 <= 0 || d.t1 > 512 || nworkers > 0x7fffffff)
+    return hipErrorInvalidValue;
+  const size_t lds = (2 * (size_t)((d.n + 7) & ~7) + (size_t)d.n) * sizeof(double);
+  static bool attr = false;
+  if (!attr) {  // up to 4096 points: 96 KiB of dynamic LDS
+    hipError_t e = hipFuncSetAttribute((const void *)pwelch_mixed_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(pwelch_mixed_kernel, dim3((unsigned)nworkers), dim3(d.t1), lds, s, x, nfft,
+                     stride, seg_begin, seg_end, ppw, d, win, tw, partial);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

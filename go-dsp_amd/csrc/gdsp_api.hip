@@ -229,6 +229,8 @@ struct gdsp_plan {
   cd *tw = nullptr;  // power of 2: T_n[k] = exp(-2 pi i k/n), n entries;
                      // mixed radix: the per-pass butterfly-major table
   gdsp::MixedDesc md{};
+  gdsp::MixedDesc md_gen{};  // generic radix list (runtime-radix kernels)
+  cd *tw_gen = nullptr;
   // mixed four-step (KIND_MIXED4): n = n1 * n2, one-kernel sub-plans, tw = T_n
   int64_t n1 = 0, n2 = 0;
   gdsp_plan *p1 = nullptr, *p2 = nullptr;
@@ -270,7 +272,7 @@ int get_plan_locked(int dev, int64_t n, gdsp_plan **out);
 
 // Radices of the mixed-radix kernel for n (fft_mixed.hip), or false when n is
 // a power of 2, too long, or has a prime factor above 13 (-> Bluestein).
-bool mixed_radices(int64_t n, std::vector<int> &rad) {
+bool mixed_radices(int64_t n, std::vector<int> &rad, bool specs = true) {
   rad.clear();
   if (n < 2 || n > gdsp::kMixedMax || is_pow2(n)) return false;
   int64_t m = n;
@@ -287,7 +289,7 @@ bool mixed_radices(int64_t n, std::vector<int> &rad) {
     }
   if (m != 1) return false;
   int fr[16], fnp = 0;
-  if (gdsp::mixed_fixed_radices((int)n, fr, &fnp)) {
+  if (specs && gdsp::mixed_fixed_radices((int)n, fr, &fnp)) {
     rad.assign(fr, fr + fnp);
     return true;
   }
@@ -300,9 +302,10 @@ bool mixed_radices(int64_t n, std::vector<int> &rad) {
   return rad.size() <= 12;
 }
 
-int build_mixed(int dev, int64_t n, const std::vector<int> &rad, gdsp_plan *p) {
-  p->kind = KIND_MIXED;
-  gdsp::MixedDesc &d = p->md;
+// Descriptor + per-pass twiddle bases W_{Ns*R}^k (k < Ns; the kernels
+// raise them to the powers r = 1..R-1 in registers) of one radix list.
+int make_mixed_desc(int dev, int64_t n, const std::vector<int> &rad, gdsp::MixedDesc &d,
+                    cd **tw) {
   d.n = (int)n;
   d.npass = (int)rad.size();
   d.codes = 0;
@@ -318,8 +321,6 @@ int build_mixed(int dev, int64_t n, const std::vector<int> &rad, gdsp_plan *p) {
   if (t1 > 512) return fail(GDSP_ERR_UNSUPPORTED, "mixed-radix geometry");
   d.t1 = t1;
   d.tpw = std::max(1, std::min(256 / t1, gdsp::kMixedMax / (int)n));
-  // per-pass twiddle bases W_{Ns*R}^k, k < Ns (the kernels raise them to
-  // the powers r = 1..R-1 in registers)
   std::vector<cd> h;
   int64_t ns = rad[0];
   for (size_t q = 1; q < rad.size(); ++q) {
@@ -332,10 +333,25 @@ int build_mixed(int dev, int64_t n, const std::vector<int> &rad, gdsp_plan *p) {
     ns *= R;
   }
   if (h.empty()) h.push_back({1.0, 0.0});
-  HIPCHK(hipMalloc((void **)&p->tw, h.size() * sizeof(cd)));
-  STCHK(copy_h2d(p->tw, h.data(), h.size() * sizeof(cd), thread_stream(dev)));
+  HIPCHK(hipMalloc((void **)tw, h.size() * sizeof(cd)));
+  STCHK(copy_h2d(*tw, h.data(), h.size() * sizeof(cd), thread_stream(dev)));
   HIPCHK(hipStreamSynchronize(thread_stream(dev)));
   return GDSP_OK;
+}
+
+int build_mixed(int dev, int64_t n, const std::vector<int> &rad, gdsp_plan *p) {
+  p->kind = KIND_MIXED;
+  STCHK(make_mixed_desc(dev, n, rad, p->md, &p->tw));
+  // the runtime-radix kernels (fused Pwelch) take the generic list: radices
+  // <= 16, no composites (a compiled specialisation's list may hold them)
+  std::vector<int> gen;
+  mixed_radices(n, gen, false);
+  if (gen == rad) {
+    p->md_gen = p->md;
+    p->tw_gen = p->tw;
+    return GDSP_OK;
+  }
+  return make_mixed_desc(dev, n, gen, p->md_gen, &p->tw_gen);
 }
 
 // Lengths one kernel transforms per row: powers of 2 up to the LDS limit, or
@@ -1053,6 +1069,23 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
       HIPCHK(gdsp::launch_pwelch(p->log2n, d_x, nfft, stride, seg_begin, seg_end, ppw, nworkers,
                                  d_win_seg, p->tw, (double *)part.p, s));
     }
+    HIPCHK(gdsp::launch_reduce_partials((const double *)part.p, nworkers, flen, d_acc,
+                                        (double *)red.p, s));
+    return GDSP_OK;
+  }
+  if (p->kind == KIND_MIXED && p->md_gen.npass >= 2) {
+    // fused mixed-radix path (smooth NFFT / Pad up to 4096)
+    const int64_t npairs = (nseg + 1) / 2;
+    int64_t target = 2048;
+    if (target > npairs) target = npairs;
+    const int64_t ppw = (npairs + target - 1) / target;
+    const int64_t nworkers = (npairs + ppw - 1) / ppw;
+    DevBuf part, red;
+    STCHK(part.alloc((size_t)nworkers * (size_t)flen * sizeof(double), s, SLOT_PW_PART));
+    STCHK(red.alloc((size_t)gdsp::reduce_scratch_doubles(nworkers, flen) * sizeof(double), s,
+                    SLOT_PW_RED));
+    HIPCHK(gdsp::launch_pwelch_mixed(p->md_gen, d_x, nfft, stride, seg_begin, seg_end, ppw,
+                                     nworkers, d_win_seg, p->tw_gen, (double *)part.p, s));
     HIPCHK(gdsp::launch_reduce_partials((const double *)part.p, nworkers, flen, d_acc,
                                         (double *)red.p, s));
     return GDSP_OK;

@@ -23,6 +23,11 @@ struct MixedDesc {
   int n, npass, t1, tpw;
 };
 constexpr int kMixedMax = 4096;
+// fused Pwelch over a mixed-radix segment length d.n = max(pad, nfft) with
+// d.npass >= 2 (fft_mixed.hip); same partial layout as launch_pwelch
+hipError_t launch_pwelch_mixed(const MixedDesc &d, const double *x, int64_t nfft, int64_t stride,
+                               int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,
+                               const double *win, const cd *tw, double *partial, hipStream_t s);
 // radix list of a compiled specialisation for n (false: use the generic list)
 bool mixed_fixed_radices(int n, int *rad, int *npass);
 hipError_t launch_fft_mixed(const MixedDesc &d, bool inv, int load, const void *in, cd *out,

@@ -205,6 +205,16 @@ WINDOWS = {"hann": "Hann", "hamming": "Hamming", "rectangular": "Rectangular",
     (20000, 32, 16, 16, "hann"),
     (100000, 8192, 4096, 2048, "hamming"),
     (8191, 8192, 4096, 0, "hann"),     # shorter than NFFT: one zero-padded segment
+    # smooth non-power-of-2 lengths: the fused mixed-radix Pwelch kernel
+    (30000, 1000, 500, 0, "hann"),
+    (20001, 3000, 1500, 0, "hann"),
+    (12345, 960, 0, 1200, "hamming"),  # Pad > NFFT, both smooth
+    (9999, 1500, 700, 0, "blackman"),
+    (50000, 4095, 2000, 0, "hann"),    # 13*7*5*3*3: five passes
+    (3001, 12, 5, 0, "bartlett"),      # two tiny passes
+    # materialised path: a single-radix length, and a Bluestein length
+    (5000, 7, 3, 0, "hann"),
+    (100000, 5000, 2500, 0, "flattop"),
 ])
 def test_pwelch_vs_oracle(gdsp, oracle, n, nfft, nov, pad, win):
     rng = np.random.default_rng(n + nfft)
