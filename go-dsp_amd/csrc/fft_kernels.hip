@@ -447,12 +447,25 @@ __global__ __launch_bounds__(256) void colfft_tile_kernel(
   fft_regs<LOG2L, true, false, 4, CW>(v, t, twl, lds + c, lds + c);
   if (col < C) {
     cd *dst = out + q * out_step * C + col;
+    // W_R^(m*j), m = q (mode 1) or col (mode 2), for j = t + k*T: the base
+    // W^(m*t) and the step W^(m*T) from the table, the rest by recurrence
+    // (two table reads per thread instead of E scattered ones: for N = 2^20
+    // the table is 16 MiB and the scattered reads missed L2)
+    const int64_t mask = ((int64_t)1 << log2r) - 1;
+    const int64_t m = TWIDDLE == 1 ? q : col;
+    cd w = {1.0, 0.0}, wstep = {1.0, 0.0};
+    if constexpr (TWIDDLE != 0) {
+      w = twr[(m * t) & mask];
+      wstep = twr[(m * G::T) & mask];
+    }
 #pragma unroll
     for (int k = 0; k < G::E; ++k) {
       const int64_t j = t + k * G::T;
       cd o = v[k];
-      if constexpr (TWIDDLE == 1) o = cmul(o, twr[(q * j) & (((int64_t)1 << log2r) - 1)]);
-      if constexpr (TWIDDLE == 2) o = cmul(o, twr[(col * j) & (((int64_t)1 << log2r) - 1)]);
+      if constexpr (TWIDDLE != 0) {
+        o = cmul(o, w);
+        if (k + 1 < G::E) w = cmul(w, wstep);
+      }
       if constexpr (CONJ_SCALE_OUT) o = {o.x * scale, -o.y * scale};
       dst[j * out_stride * C] = o;
     }
@@ -477,6 +490,8 @@ __global__ __launch_bounds__(256) void transpose_kernel(const cd *__restrict__ i
   const int64_t tiles_r = (rows + 31) / 32;
   const int64_t per = tiles_c * tiles_r;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  // (a register-prefetch variant, next tile's loads issued before this
+  // tile's stores, measured 853 -> 1385 us on 2048 16x4096 matrices)
   for (int64_t tg = blockIdx.x; tg < per * batch; tg += gridDim.x) {
     const int64_t b = tg / per, tb = tg - b * per;
     const int64_t tr = tb / tiles_c, tc = tb - tr * tiles_c;
