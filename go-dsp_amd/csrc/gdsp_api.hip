@@ -150,6 +150,7 @@ struct Staging {
   char *buf = nullptr;
   size_t half = 0;
   hipEvent_t ev[2] = {nullptr, nullptr};
+  bool pending[2] = {false, false};  // a queued copy may still read / write the half
   ~Staging() {
     if (buf) (void)hipHostFree(buf);
     for (auto &e : ev)
@@ -173,26 +174,31 @@ int staging_get(Staging **out) {
   return GDSP_OK;
 }
 
+// Host -> device through the staging halves. A half is refilled only after
+// the copy that last used it has completed (its event); the copies themselves
+// stay queued, and the stream orders them before the kernels and the
+// device -> host copies that follow on the same stream.
 int copy_h2d(void *dst, const void *src, size_t bytes, hipStream_t s) {
   Staging *st = nullptr;
   STCHK(staging_get(&st));
-  bool used[2] = {false, false};
   int h = 0;
   for (size_t off = 0; off < bytes; off += st->half, h ^= 1) {
     const size_t c = bytes - off < st->half ? bytes - off : st->half;
     char *stg = st->buf + (size_t)h * st->half;
-    if (used[h]) HIPCHK(hipEventSynchronize(st->ev[h]));
+    if (st->pending[h]) {
+      HIPCHK(hipEventSynchronize(st->ev[h]));
+      st->pending[h] = false;
+    }
     memcpy(stg, (const char *)src + off, c);
     HIPCHK(hipMemcpyAsync((char *)dst + off, stg, c, hipMemcpyHostToDevice, s));
     HIPCHK(hipEventRecord(st->ev[h], s));
-    used[h] = true;
+    st->pending[h] = true;
   }
-  // the staging halves stay referenced by queued copies until they complete
-  for (int i = 0; i < 2; ++i)
-    if (used[i]) HIPCHK(hipEventSynchronize(st->ev[i]));
   return GDSP_OK;
 }
 
+// Device -> host, double-buffered; returns once every chunk has landed in
+// dst, so everything queued on s before it has completed too.
 int copy_d2h(void *dst, const void *src, size_t bytes, hipStream_t s) {
   Staging *st = nullptr;
   STCHK(staging_get(&st));
@@ -203,16 +209,49 @@ int copy_d2h(void *dst, const void *src, size_t bytes, hipStream_t s) {
     HIPCHK(hipMemcpyAsync(st->buf + (i & 1) * st->half, (const char *)src + off, c,
                           hipMemcpyDeviceToHost, s));
     HIPCHK(hipEventRecord(st->ev[i & 1], s));
+    st->pending[i & 1] = true;
     return GDSP_OK;
   };
   if (nchunk) STCHK(issue(0));
   for (size_t i = 0; i < nchunk; ++i) {
     if (i + 1 < nchunk) STCHK(issue(i + 1));
     HIPCHK(hipEventSynchronize(st->ev[i & 1]));
+    st->pending[i & 1] = false;
     const size_t off = i * st->half;
     const size_t c = bytes - off < st->half ? bytes - off : st->half;
     memcpy((char *)dst + off, st->buf + (i & 1) * st->half, c);
   }
+  return GDSP_OK;
+}
+
+// Mapped pinned host memory per (thread, device) for small host calls
+// (input at 0, output at kZeroCopyOut): the kernels access it over the
+// fabric, which for a few hundred KiB costs less than two copy launches.
+constexpr size_t kZeroCopyOut = (size_t)512 << 10;
+constexpr size_t kZeroCopyMax = (size_t)512 << 10;  // in + out bytes of one call
+struct ZeroCopy {
+  char *host = nullptr;
+  void *dev = nullptr;
+  ~ZeroCopy() {
+    if (host) (void)hipHostFree(host);
+  }
+};
+
+int zero_copy_get(ZeroCopy **out) {
+  thread_local std::map<int, ZeroCopy> per_dev;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(GDSP_ERR_NO_DEVICE, "hipGetDevice failed");
+  ZeroCopy &z = per_dev[dev];
+  if (!z.host) {
+    HIPCHK(hipHostMalloc((void **)&z.host, 2 * kZeroCopyOut, hipHostMallocMapped));
+    hipError_t e = hipHostGetDevicePointer(&z.dev, z.host, 0);
+    if (e != hipSuccess) {
+      (void)hipHostFree(z.host);
+      z.host = nullptr;
+      return fail(GDSP_ERR_HIP, std::string("hipHostGetDevicePointer: ") + hipGetErrorString(e));
+    }
+  }
+  *out = &z;
   return GDSP_OK;
 }
 
@@ -265,6 +304,8 @@ int upload_twiddles(int dev, int64_t n, cd **dst) {
   }
   HIPCHK(hipMalloc((void **)dst, (size_t)n * sizeof(cd)));
   STCHK(copy_h2d(*dst, h.data(), (size_t)n * sizeof(cd), thread_stream(dev)));
+  // plans are shared by every stream and thread: the table must be complete
+  HIPCHK(hipStreamSynchronize(thread_stream(dev)));
   return GDSP_OK;
 }
 
@@ -675,13 +716,24 @@ int host_batch(const void *x, size_t in_elem_bytes, double *out, int64_t n, int6
   if (!s) return fail(GDSP_ERR_HIP, "stream creation failed");
   const size_t in_bytes = (size_t)batch * (size_t)n * in_elem_bytes;
   const size_t out_bytes = (size_t)batch * (size_t)n * sizeof(cd);
+  if (in_bytes + out_bytes <= kZeroCopyMax) {
+    // small calls: the kernels read and write mapped pinned host memory
+    // directly — one launch and one synchronisation instead of two copies
+    ZeroCopy *zc = nullptr;
+    STCHK(zero_copy_get(&zc));
+    memcpy(zc->host, x, in_bytes);
+    char *dbase = (char *)zc->dev;
+    STCHK(exec_plan(p, dbase, (cd *)(dbase + kZeroCopyOut), batch, inv, load, s));
+    HIPCHK(hipStreamSynchronize(s));
+    memcpy(out, zc->host + kZeroCopyOut, out_bytes);
+    return GDSP_OK;
+  }
   DevBuf din, dout;
   STCHK(din.alloc(in_bytes, s, SLOT_IN));
   STCHK(dout.alloc(out_bytes, s, SLOT_OUT));
   STCHK(copy_h2d(din.p, x, in_bytes, s));
   STCHK(exec_plan(p, din.p, (cd *)dout.p, batch, inv, load, s));
-  STCHK(copy_d2h(out, dout.p, out_bytes, s));
-  HIPCHK(hipStreamSynchronize(s));
+  STCHK(copy_d2h(out, dout.p, out_bytes, s));  // returns after the stream drained
   return GDSP_OK;
 }
 
@@ -1237,8 +1289,7 @@ int gdsp_wav_read_floats(const void *in, int64_t count, int audio_format, int bi
   STCHK(copy_h2d(din.p, in, in_bytes, s));
   HIPCHK(gdsp::launch_wav_decode(din.p, count, audio_format, bits_per_sample, dout.p,
                                  out_f64 != 0, s));
-  STCHK(copy_d2h(out, dout.p, out_bytes, s));
-  HIPCHK(hipStreamSynchronize(s));
+  STCHK(copy_d2h(out, dout.p, out_bytes, s));  // returns after the stream drained
   return GDSP_OK;
 }
 
