@@ -57,6 +57,28 @@ def ZeroPad2(x) -> np.ndarray:
     return ZeroPad(x, NextPowerOf2(len(x)))
 
 
+def Segment(x, segs: int, noverlap: float):
+    """dsputils.Segment — dsputils/dsputils.go:89-120: segs equal-length
+    views into x with a fractional overlap noverlap (0 <= noverlap <= 1);
+    the longest length that fits wins, trailing entries are dropped. Panics
+    "too many segments" when none fits. Host index arithmetic (not on the
+    GPU path); the results are numpy views, as the reference's are slices."""
+    x = np.asarray(x)
+    lx = len(x)
+    length = lx
+    step = 0
+    while length > 0:
+        overlap = int(float(length) * noverlap)  # Go int() truncates toward zero
+        tot = segs * (length - overlap) + overlap
+        if tot <= lx:
+            step = length - overlap
+            break
+        length -= 1
+    if length == 0:
+        raise _panic("too many segments")
+    return [x[n * step:n * step + length] for n in range(segs)]
+
+
 def Float64Equal(a: float, b: float) -> bool:
     """compare.go:94-96: |a-b| <= 1e-8 or |1-a/b| <= 1e-8."""
     if abs(a - b) <= closeFactor:

@@ -91,6 +91,26 @@ inline bool PrettyClose2(const std::vector<std::vector<complex>> &a,
   return true;
 }
 
+// dsputils.Segment — dsputils/dsputils.go:89-120: segs equal-length copies
+// of x with a fractional overlap (the reference returns slices; a C++ caller
+// gets the values). Throws Panic("too many segments") when none fits.
+inline std::vector<std::vector<complex>> Segment(const std::vector<complex> &x, int segs,
+                                                 double noverlap) {
+  const int lx = (int)x.size();
+  int length = lx, step = 0;
+  for (; length > 0; --length) {
+    const int overlap = (int)((double)length * noverlap);
+    if (segs * (length - overlap) + overlap <= lx) {
+      step = length - overlap;
+      break;
+    }
+  }
+  if (length == 0) throw Panic(GDSP_ERR_INVALID, "too many segments");
+  std::vector<std::vector<complex>> r((size_t)segs);
+  for (int n = 0; n < segs; ++n) r[(size_t)n].assign(x.begin() + n * step, x.begin() + n * step + length);
+  return r;
+}
+
 // dsputils.Matrix — dsputils/matrix.go:21-216 (row-major N-D complex128).
 struct Matrix {
   std::vector<complex> list;

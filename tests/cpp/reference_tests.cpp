@@ -166,6 +166,16 @@ int main(int argc, char **argv) {
   EXPECT(panics([] { fft::FFT2({{1, 2}, {3}}); }), "FFT2 ragged panics");
   EXPECT(fft::FFT({}).empty(), "FFT empty returns empty");
   EXPECT(spectral::Pwelch({}, 1, nullptr).first.empty(), "Pwelch empty returns empty");
+  // TestSegment, dsputils/dsputils_test.go:41-58
+  {
+    std::vector<complex> x;
+    for (int n = 0; n < 16; ++n) x.push_back(complex(n, 0));
+    auto v = dsputils::Segment(x, 3, 0.5);
+    std::vector<std::vector<complex>> want = {{x.begin(), x.begin() + 8},
+                                              {x.begin() + 4, x.begin() + 12},
+                                              {x.begin() + 8, x.begin() + 16}};
+    EXPECT(dsputils::PrettyClose2(v, want), "dsputils.Segment");
+  }
   // TestMakeMatrix, dsputils/matrix_test.go:23-47
   {
     std::vector<complex> v;

@@ -15,6 +15,7 @@ reference's test tables from /root/reference as data.
      spectral/spectral_test.go:31-56 segmentTests
      window/window_test.go:34-59     windowTests
      wav/wav_test.go:62-95           wavTests      (header fields per file)
+     dsputils/dsputils_test.go:29-39 dsputilsSegmentTests
    and wav/small.wav (copied) + the first 64 KiB of wav/float.wav's data
    chunk (header intact) into tests/golden/wav/ — the data files the
    reference's wav test reads.
@@ -99,6 +100,10 @@ def reference_vectors() -> dict:
          "blackman": e[5]}
         for e in _literal_to_json(_block("window/window_test.go", "var windowTests = []windowTest{"))]
     out["wavTests"] = wav_tests()
+    out["dsputilsSegmentTests"] = [
+        {"segs": e[0], "noverlap": e[1], "slices": e[2]}
+        for e in _literal_to_json(
+            _block("dsputils/dsputils_test.go", "var segmentTests = []segmentTest{"))]
     return out
 
 

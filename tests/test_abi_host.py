@@ -134,3 +134,21 @@ def test_matrix_reference_table(gdsp):
     with pytest.raises(gdsp.Panic):
         m.Dim([-1, -1, 0])
     assert [list(r) for r in U.MakeMatrix2([[1, 2], [3, 4]]).To2D()] == [[1, 2], [3, 4]]
+
+
+def test_dsputils_segment_reference_table(gdsp, refvec):
+    # dsputils/dsputils_test.go:41-58 (TestSegment)
+    U = gdsp.dsputils
+    x = np.arange(16, dtype=np.float64).astype(np.complex128)
+    for c in refvec["dsputilsSegmentTests"]:
+        v = U.Segment(x, c["segs"], c["noverlap"])
+        want = [x[a:b] for a, b in c["slices"]]
+        assert U.PrettyClose2(v, want)
+    # longest length that fits, trailing entries dropped; and the panic
+    v = U.Segment(np.arange(10), 4, 0.0)
+    assert [list(s) for s in v] == [[0, 1], [2, 3], [4, 5], [6, 7]]
+    v = U.Segment(np.arange(10), 2, 0.25)
+    assert [len(s) for s in v] == [5, 5]  # 2*(6-1)+1 = 11 > 10, so length 5, overlap 1
+    assert list(v[1]) == [4, 5, 6, 7, 8]
+    with pytest.raises(gdsp.Panic, match="too many segments"):
+        U.Segment(np.arange(3), 4, 0.0)
