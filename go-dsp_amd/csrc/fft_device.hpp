@@ -26,6 +26,21 @@ __device__ __forceinline__ cd cmul(cd a, cd b) {
 }
 __device__ __forceinline__ cd conjg(cd a) { return {a.x, -a.y}; }
 
+// Streaming HBM access for data each launch touches exactly once (transform
+// inputs and outputs, Pwelch samples): nontemporal (nt) global_load /
+// global_store_dwordx4. Measured on the N = 4096 x 65536 batch: 1.437 ->
+// 1.355 ms (5.98 -> 6.34 TB/s); loads alone gain nothing, stores alone half.
+// Tables that every workgroup re-reads (twiddles, windows, chirps) keep the
+// default policy.
+__device__ __forceinline__ cd ld_nt(const cd *p) {
+  return {__builtin_nontemporal_load(&p->x), __builtin_nontemporal_load(&p->y)};
+}
+__device__ __forceinline__ double ld_nt(const double *p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void st_nt(cd *p, cd v) {
+  __builtin_nontemporal_store(v.x, &p->x);
+  __builtin_nontemporal_store(v.y, &p->y);
+}
+
 // cos/sin(pi/8) and sqrt(2)/2 to double precision
 #define GDSP_C8 0.92387953251128675613
 #define GDSP_S8 0.38268343236508977173

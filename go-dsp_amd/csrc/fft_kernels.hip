@@ -47,13 +47,13 @@ __global__ __launch_bounds__(Geo<LOG2N>::WG, (LOG2N >= 13 && SPLIT ? 4 : 1)) voi
     const cd *src = reinterpret_cast<const cd *>(in) + gl * G::N;
 #pragma unroll
     for (int k = 0; k < G::E; ++k) {
-      v[k] = src[t + k * G::T];
+      v[k] = ld_nt(&src[t + k * G::T]);
       if constexpr (INV) v[k].y = -v[k].y;
     }
   } else {
     const double *src = reinterpret_cast<const double *>(in) + gl * G::N;
 #pragma unroll
-    for (int k = 0; k < G::E; ++k) v[k] = {src[t + k * G::T], 0.0};
+    for (int k = 0; k < G::E; ++k) v[k] = {ld_nt(&src[t + k * G::T]), 0.0};
   }
   fft_regs<LOG2N, SPLIT>(v, t, tw, lre, lim);
   if (valid) {
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(Geo<LOG2N>::WG, (LOG2N >= 13 && SPLIT ? 4 : 1)) voi
     for (int k = 0; k < G::E; ++k) {
       cd o = v[k];
       if constexpr (INV) o = {o.x * scale, -o.y * scale};
-      dst[t + k * G::T] = o;
+      st_nt(&dst[t + k * G::T], o);
     }
   }
 }
@@ -94,7 +94,7 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
     const int idx = t + k * G::T;
     v[k] = {0.0, 0.0};
     if (valid && idx < n) {
-      cd x = src[idx];
+      cd x = ld_nt(&src[idx]);
       if constexpr (INV) x.y = -x.y;
       v[k] = cmul(x, chirp[idx]);
     }
@@ -113,7 +113,7 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
       if (idx < n) {
         cd y = cmul(conjg(v[k]), chirp[idx]);
         if constexpr (INV) y = {y.x * scale, -y.y * scale};
-        dst[idx] = y;
+        st_nt(&dst[idx], y);
       }
     }
   }
@@ -137,10 +137,10 @@ __global__ __launch_bounds__(256) void stockham_global_pass(
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     if constexpr (LOAD == LOAD_COMPLEX) {
-      u[r] = reinterpret_cast<const cd *>(in)[g * N + j + r * nr];
+      u[r] = ld_nt(reinterpret_cast<const cd *>(in) + g * N + j + r * nr);
       if constexpr (CONJ_IN) u[r].y = -u[r].y;
     } else {
-      u[r] = {reinterpret_cast<const double *>(in)[g * N + j + r * nr], 0.0};
+      u[r] = {ld_nt(reinterpret_cast<const double *>(in) + g * N + j + r * nr), 0.0};
     }
   }
   if (NS > 1) {
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void stockham_global_pass(
   for (int r = 0; r < R; ++r) {
     cd o = u[r];
     if constexpr (CONJ_SCALE_OUT) o = {o.x * scale, -o.y * scale};
-    out[base + r * NS] = o;
+    st_nt(&out[base + r * NS], o);
   }
 }
 
@@ -441,7 +441,7 @@ __global__ __launch_bounds__(256) void colfft_tile_kernel(
   cd v[G::E];
 #pragma unroll
   for (int k = 0; k < G::E; ++k) {
-    v[k] = src[(int64_t)(t + k * G::T) * in_stride * C];
+    v[k] = ld_nt(&src[(int64_t)(t + k * G::T) * in_stride * C]);
     if constexpr (CONJ_IN) v[k].y = -v[k].y;
   }
   fft_regs<LOG2L, true, false, 4, CW>(v, t, twl, lds + c, lds + c);
@@ -467,7 +467,7 @@ __global__ __launch_bounds__(256) void colfft_tile_kernel(
         if (k + 1 < G::E) w = cmul(w, wstep);
       }
       if constexpr (CONJ_SCALE_OUT) o = {o.x * scale, -o.y * scale};
-      dst[j * out_stride * C] = o;
+      st_nt(&dst[j * out_stride * C], o);
     }
   }
 }
@@ -500,7 +500,7 @@ __global__ __launch_bounds__(256) void transpose_kernel(const cd *__restrict__ i
 #pragma unroll
     for (int i = 0; i < 32; i += 8) {
       const int64_t r = tr * 32 + ty + i, c = tc * 32 + tx;
-      if (r < rows && c < cols) tile[ty + i][tx] = src[r * cols + c];
+      if (r < rows && c < cols) tile[ty + i][tx] = ld_nt(&src[r * cols + c]);
     }
     __syncthreads();
 #pragma unroll
@@ -514,7 +514,7 @@ __global__ __launch_bounds__(256) void transpose_kernel(const cd *__restrict__ i
           o = cmul(o, w);
         }
         if (conj_scale) o = {o.x * scale, -o.y * scale};
-        dst[c * rows + r] = o;
+        st_nt(&dst[c * rows + r], o);
       }
     }
     __syncthreads();
