@@ -785,6 +785,183 @@ static bool launch_spec(std::tuple<S...>, const MixedDesc &d, bool inv, int load
   return (spec_launch(S{}, d, inv, load, in, out, batch, tw, scale, s) || ...);
 }
 
+// ---------------------------------------------------------------------------
+// Fused Welch accumulation on a compiled specialisation (spectral/pwelch.go:
+// 104-122 for smooth NFFT / Pad = one of the Specs lengths): the same packed
+// segment pairs as pwelch_kernel (z = w*x_s0 + i*w*x_s1, the k / F-k fold in
+// finalise), but every pass inlined with compile-time radices instead of the
+// runtime-radix pass functions of pwelch_mixed_kernel. Each workgroup slot is
+// one persistent worker; the power sums of the bins a thread's last-pass
+// butterflies produce stay in its registers across the worker's pairs.
+
+// fixed_chain with the last pass handed to a sink instead of stored
+template <bool SPLIT, bool SWZ, int N, int T1, int NS, int TWOFF, class Prev, class F, int R,
+          int... REST>
+__device__ __forceinline__ void fixed_chain_to(const Prev &prev, int tl, bool valid, void *lds,
+                                               const cd *tw, F &sink) {
+  FPass<R, N, NS, T1> cur;
+  if constexpr (SPLIT) {
+    prev.template store_lds<0, SWZ>(tl, valid, lds);
+    __syncthreads();
+    cur.template load_lds<0, SWZ>(tl, valid, lds);
+    __syncthreads();
+    prev.template store_lds<1, SWZ>(tl, valid, lds);
+    __syncthreads();
+    cur.template load_lds<1, SWZ>(tl, valid, lds);
+  } else {
+    prev.template store_lds<2, SWZ>(tl, valid, lds);
+    __syncthreads();
+    cur.template load_lds<2, SWZ>(tl, valid, lds);
+  }
+  cur.compute(tl, valid, tw + TWOFF);
+  if constexpr (sizeof...(REST) == 0) {
+    sink(cur);
+  } else {
+    __syncthreads();
+    fixed_chain_to<SPLIT, SWZ, N, T1, NS * R, TWOFF + NS, FPass<R, N, NS, T1>, F, REST...>(
+        cur, tl, valid, lds, tw, sink);
+  }
+}
+
+template <int R0, int... RS>
+struct FixedLast {
+  static constexpr int rr[] = {R0, RS...};
+  static constexpr int R = rr[sizeof...(RS)];
+  static constexpr int N = FixedGeo<R0, RS...>::N;
+  using Pass = FPass<R, N, N / R, FixedGeo<R0, RS...>::T1>;
+};
+
+template <bool SWZ, int R0, int... RS>
+__global__ __launch_bounds__((FixedGeo<R0, RS...>::WG)) void pwelch_fixed_kernel(
+    const double *__restrict__ x, int64_t nfft, int64_t stride, int64_t seg_begin,
+    int64_t seg_end, int64_t pairs_per_worker, const double *__restrict__ win,
+    const cd *__restrict__ tw, double *__restrict__ partial) {
+  static_assert(sizeof...(RS) >= 1, "at least two passes");
+  using G = FixedGeo<R0, RS...>;
+  using L = FixedLast<R0, RS...>;
+  using First = FPass<R0, G::N, 1, G::T1>;
+  __shared__ double lds[G::TPW * 2 * G::SLOTS];
+  const int sub = G::TPW == 1 ? 0 : (int)threadIdx.x / G::T1;
+  const int tl = (int)threadIdx.x - sub * G::T1;
+  const int64_t worker = (int64_t)blockIdx.x * G::TPW + sub;
+  double *ld = lds + sub * 2 * G::SLOTS;
+  const int64_t npairs = (seg_end - seg_begin + 1) / 2;
+  const int64_t p0 = worker * pairs_per_worker;
+  double acc[L::Pass::J][L::R];
+#pragma unroll
+  for (int jj = 0; jj < L::Pass::J; ++jj)
+#pragma unroll
+    for (int r = 0; r < L::R; ++r) acc[jj][r] = 0.0;
+  for (int64_t it = 0; it < pairs_per_worker; ++it) {
+    const int64_t p = p0 + it;
+    const bool active = p < npairs;
+    const int64_t s0 = seg_begin + 2 * (active ? p : 0);
+    const bool has1 = active && s0 + 1 < seg_end;
+    const double *x0 = opaque_ptr(x) + s0 * stride, *x1 = x0 + stride;
+    // laundered per pair: otherwise the compiler hoists the loop-invariant
+    // window values and twiddle power chains out of the loop, and the
+    // registers they pin halve the occupancy
+    const double *w = opaque_ptr(win);
+    const cd *twp = opaque_ptr(tw);
+    const int tt = opaque_int(tl);
+    First f0;
+#pragma unroll
+    for (int jj = 0; jj < First::J; ++jj) {
+      const int j = tt + jj * G::T1;
+      if (First::act(j, true)) {
+#pragma unroll
+        for (int r = 0; r < R0; ++r) {
+          const int i = j + r * First::NB;
+          double a = 0.0, b = 0.0;
+          if (active && i < nfft) {
+            const double wi = w[i];
+            a = wi * x0[i];
+            if (has1) b = wi * x1[i];
+          }
+          f0.v[jj][r] = {a, b};
+        }
+      }
+    }
+    f0.compute(tt, true, twp);
+    if (it > 0) __syncthreads();  // the previous pair's last exchange reads are done
+    auto sink = [&](const typename L::Pass &c) {
+      if (!active) return;
+#pragma unroll
+      for (int jj = 0; jj < L::Pass::J; ++jj) {
+        const int j = tt + jj * G::T1;
+        if (L::Pass::act(j, true)) {
+#pragma unroll
+          for (int r = 0; r < L::R; ++r)
+            acc[jj][r] += c.v[jj][r].x * c.v[jj][r].x + c.v[jj][r].y * c.v[jj][r].y;
+        }
+      }
+    };
+    fixed_chain_to<false, SWZ, G::N, G::T1, R0, 0, First, decltype(sink), RS...>(f0, tt, true, ld,
+                                                                                twp, sink);
+  }
+  if (p0 < npairs) {
+    double *dst = partial + worker * G::N;
+#pragma unroll
+    for (int jj = 0; jj < L::Pass::J; ++jj) {
+      const int j = tl + jj * G::T1;
+      if (L::Pass::act(j, true)) {
+        constexpr int NSL = G::N / L::R;
+        const int k = j % NSL, o = (j - k) * L::R + k;
+#pragma unroll
+        for (int r = 0; r < L::R; ++r) dst[o + r * NSL] = acc[jj][r];
+      }
+    }
+  }
+}
+
+template <int... RS>
+static int spec_pw_tpw(Spec<RS...>, const MixedDesc &d) {
+  uint64_t codes = 0;
+  int q = 0;
+  for (int r : {RS...}) codes |= (uint64_t)r << (5 * q++);
+  return (d.n == FixedGeo<RS...>::N && d.codes == codes) ? FixedGeo<RS...>::TPW : 0;
+}
+template <class... S>
+static int find_pw_tpw(std::tuple<S...>, const MixedDesc &d) {
+  int t = 0;
+  ((t = t ? t : spec_pw_tpw(S{}, d)), ...);
+  return t;
+}
+int pwelch_fixed_workers_per_block(const MixedDesc &d) { return find_pw_tpw(Specs{}, d); }
+
+template <int... RS>
+static bool spec_pw_launch(Spec<RS...>, const MixedDesc &d, const double *x, int64_t nfft,
+                           int64_t stride, int64_t seg_begin, int64_t seg_end, int64_t ppw,
+                           int64_t nworkers, const double *win, const cd *tw, double *partial,
+                           hipStream_t s) {
+  if (!spec_pw_tpw(Spec<RS...>{}, d)) return false;
+  using G = FixedGeo<RS...>;
+  constexpr int R0 = [] { constexpr int r[] = {RS...}; return r[0]; }();
+  const dim3 grid((unsigned)((nworkers + G::TPW - 1) / G::TPW)), block(G::WG);
+  hipLaunchKernelGGL((pwelch_fixed_kernel<R0 % 2 == 0, RS...>), grid, block, 0, s, x, nfft, stride,
+                     seg_begin, seg_end, ppw, win, tw, partial);
+  return true;
+}
+template <class... S>
+static bool launch_pw_spec(std::tuple<S...>, const MixedDesc &d, const double *x, int64_t nfft,
+                           int64_t stride, int64_t seg_begin, int64_t seg_end, int64_t ppw,
+                           int64_t nworkers, const double *win, const cd *tw, double *partial,
+                           hipStream_t s) {
+  return (spec_pw_launch(S{}, d, x, nfft, stride, seg_begin, seg_end, ppw, nworkers, win, tw,
+                         partial, s) ||
+          ...);
+}
+
+hipError_t launch_pwelch_fixed(const MixedDesc &d, const double *x, int64_t nfft, int64_t stride,
+                               int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,
+                               const double *win, const cd *tw, double *partial, hipStream_t s) {
+  if (nworkers <= 0 || nworkers > 0x7fffffff) return hipErrorInvalidValue;
+  if (!launch_pw_spec(Specs{}, d, x, nfft, stride, seg_begin, seg_end, ppw, nworkers, win, tw,
+                      partial, s))
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 // Radix list of the compiled specialisation for n, if there is one
 // (launch_fft_mixed picks the kernel by n and list). GDSP_MIXED_GENERIC=1
 // disables them. n = 3000: 1.10 ms per 65536 transforms for 25*15*8 against

@@ -1125,6 +1125,24 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
                                         (double *)red.p, s));
     return GDSP_OK;
   }
+  if (p->kind == KIND_MIXED && gdsp::pwelch_fixed_workers_per_block(p->md) > 0 &&
+      !getenv("GDSP_PW_GENERIC")) {
+    // fused path on a compiled specialisation (e.g. NFFT 1000, 3000)
+    const int64_t npairs = (nseg + 1) / 2;
+    int64_t target = 2048 * (int64_t)gdsp::pwelch_fixed_workers_per_block(p->md);
+    if (target > npairs) target = npairs;
+    const int64_t ppw = (npairs + target - 1) / target;
+    const int64_t nworkers = (npairs + ppw - 1) / ppw;
+    DevBuf part, red;
+    STCHK(part.alloc((size_t)nworkers * (size_t)flen * sizeof(double), s, SLOT_PW_PART));
+    STCHK(red.alloc((size_t)gdsp::reduce_scratch_doubles(nworkers, flen) * sizeof(double), s,
+                    SLOT_PW_RED));
+    HIPCHK(gdsp::launch_pwelch_fixed(p->md, d_x, nfft, stride, seg_begin, seg_end, ppw, nworkers,
+                                     d_win_seg, p->tw, (double *)part.p, s));
+    HIPCHK(gdsp::launch_reduce_partials((const double *)part.p, nworkers, flen, d_acc,
+                                        (double *)red.p, s));
+    return GDSP_OK;
+  }
   if (p->kind == KIND_MIXED && p->md_gen.npass >= 2) {
     // fused mixed-radix path (smooth NFFT / Pad up to 4096)
     const int64_t npairs = (nseg + 1) / 2;

@@ -28,6 +28,12 @@ constexpr int kMixedMax = 4096;
 hipError_t launch_pwelch_mixed(const MixedDesc &d, const double *x, int64_t nfft, int64_t stride,
                                int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,
                                const double *win, const cd *tw, double *partial, hipStream_t s);
+// fused Pwelch on a compiled specialisation (d = the plan's specialisation
+// descriptor, d.n = max(pad, nfft)); workers per block, 0 if d is none
+int pwelch_fixed_workers_per_block(const MixedDesc &d);
+hipError_t launch_pwelch_fixed(const MixedDesc &d, const double *x, int64_t nfft, int64_t stride,
+                               int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,
+                               const double *win, const cd *tw, double *partial, hipStream_t s);
 // radix list of a compiled specialisation for n (false: use the generic list)
 bool mixed_fixed_radices(int n, int *rad, int *npass);
 hipError_t launch_fft_mixed(const MixedDesc &d, bool inv, int load, const void *in, cd *out,

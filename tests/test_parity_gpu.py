@@ -205,12 +205,19 @@ WINDOWS = {"hann": "Hann", "hamming": "Hamming", "rectangular": "Rectangular",
     (20000, 32, 16, 16, "hann"),
     (100000, 8192, 4096, 2048, "hamming"),
     (8191, 8192, 4096, 0, "hann"),     # shorter than NFFT: one zero-padded segment
-    # smooth non-power-of-2 lengths: the fused mixed-radix Pwelch kernel
+    # smooth non-power-of-2 lengths: the fused mixed-radix Pwelch kernels
     (30000, 1000, 500, 0, "hann"),
     (20001, 3000, 1500, 0, "hann"),
     (12345, 960, 0, 1200, "hamming"),  # Pad > NFFT, both smooth
     (9999, 1500, 700, 0, "blackman"),
     (50000, 4095, 2000, 0, "hann"),    # 13*7*5*3*3: five passes
+    (30000, 800, 400, 0, "hann"),      # no compiled specialisation: runtime radices
+    # compiled specialisations (pwelch_fixed_kernel): several workers per block,
+    # odd segment counts, no overlap
+    (200000, 480, 240, 0, "hann"),
+    (100000, 2000, 1000, 0, "hamming"),
+    (70001, 1536, 768, 0, "blackman"),
+    (50000, 1000, 0, 0, "rectangular"),
     (3001, 12, 5, 0, "bartlett"),      # two tiny passes
     # materialised path: a single-radix length, and a Bluestein length
     (5000, 7, 3, 0, "hann"),
