@@ -25,16 +25,34 @@ namespace gdsp {
 // (16 complex128 per thread) and LDS (exchange between radix-16 passes).
 // N >= 8192: 512+ threads per transform, so <= 128 VGPRs is what lets two
 // workgroups share a CU (measured 1.27 -> 1.21 ms on the FFT2 8192^2 step).
+// Short transforms (fewer than 16 threads per transform, N <= 128): a
+// wave-instruction of the register layout t + k*T would touch 64 / T rows in
+// runs of only T*16 bytes, so the workgroup's TPW*N contiguous elements are
+// staged through LDS instead: coalesced 16-B-per-lane HBM streams on both
+// sides, real and imaginary halves in turn through one padded buffer
+// (slot = i + i/E keeps the stride-E reads conflict-free). N = 8 went from
+// 1.5 to ~6 TB/s.
+template <int LOG2N>
+struct Stage {
+  using G = Geo<LOG2N>;
+  static constexpr bool ON = G::T < 16 && G::TPW > 1;
+  static constexpr int DOUBLES = ON ? G::WG * (G::E + 1) : 1;
+  __device__ __forceinline__ static int pad(int i) { return i + i / G::E; }
+};
+
 template <int LOG2N, bool INV, int LOAD, bool SPLIT>
 __global__ __launch_bounds__(Geo<LOG2N>::WG, (LOG2N >= 13 && SPLIT ? 4 : 1)) void fft_lds_kernel(
     const void *__restrict__ in, cd *__restrict__ out, int64_t batch,
     const cd *__restrict__ tw, double scale) {
   using G = Geo<LOG2N>;
-  __shared__ double lds[(SPLIT ? 1 : 2) * G::LDS_DOUBLES];
+  using S = Stage<LOG2N>;
+  constexpr int XD = (SPLIT ? 1 : 2) * G::LDS_DOUBLES;
+  __shared__ double lds[XD > S::DOUBLES ? XD : S::DOUBLES];
   const int lt = threadIdx.x;
   const int slot = lt / G::T;
   const int t = lt & (G::T - 1);
-  const int64_t g = xcd_remap(blockIdx.x, gridDim.x) * G::TPW + slot;
+  const int64_t blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t g = blk * G::TPW + slot;
   // Only the last workgroup can hold slots past the batch (TPW > 1); they
   // load a valid row (clamped) and skip the store, so loads stay
   // branch-free and the whole workgroup reaches every barrier.
@@ -43,7 +61,42 @@ __global__ __launch_bounds__(Geo<LOG2N>::WG, (LOG2N >= 13 && SPLIT ? 4 : 1)) voi
   double *lre = lds + slot * G::STRIDE;
   double *lim = SPLIT ? lre : lds + G::LDS_DOUBLES + slot * G::STRIDE;
   cd v[G::E];
-  if constexpr (LOAD == LOAD_COMPLEX) {
+  if constexpr (S::ON) {
+    // element i of the block's chunk is row blk*TPW + i/N, column i%N;
+    // thread (slot, t) owns chunk elements slot*N + t + k*T
+    const int64_t base = blk * G::TPW * G::N, total = batch * G::N;
+    double tmp[2][G::E];
+#pragma unroll
+    for (int q = 0; q < G::E; ++q) {
+      const int64_t idx = base + lt + q * G::WG;
+      cd x = {0.0, 0.0};
+      if (idx < total) {
+        if constexpr (LOAD == LOAD_COMPLEX) x = ld_nt(reinterpret_cast<const cd *>(in) + idx);
+        else x = {ld_nt(reinterpret_cast<const double *>(in) + idx), 0.0};
+      }
+      tmp[0][q] = x.x;
+      tmp[1][q] = INV ? -x.y : x.y;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (LOAD == LOAD_REAL && h == 1) {
+#pragma unroll
+        for (int k = 0; k < G::E; ++k) v[k].y = 0.0;
+        break;
+      }
+      if (h) __syncthreads();
+#pragma unroll
+      for (int q = 0; q < G::E; ++q) lds[S::pad(lt + q * G::WG)] = tmp[h][q];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < G::E; ++k) {
+        const double d = lds[S::pad(slot * G::N + t + k * G::T)];
+        if (h) v[k].y = d;
+        else v[k].x = d;
+      }
+    }
+    __syncthreads();  // the exchanges below reuse the buffer
+  } else if constexpr (LOAD == LOAD_COMPLEX) {
     const cd *src = reinterpret_cast<const cd *>(in) + gl * G::N;
 #pragma unroll
     for (int k = 0; k < G::E; ++k) {
@@ -56,7 +109,28 @@ __global__ __launch_bounds__(Geo<LOG2N>::WG, (LOG2N >= 13 && SPLIT ? 4 : 1)) voi
     for (int k = 0; k < G::E; ++k) v[k] = {ld_nt(&src[t + k * G::T]), 0.0};
   }
   fft_regs<LOG2N, SPLIT>(v, t, tw, lre, lim);
-  if (valid) {
+  if constexpr (S::ON) {
+    const int64_t base = blk * G::TPW * G::N, total = batch * G::N;
+    double tmp[2][G::E];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      __syncthreads();  // the last exchange's (or the previous half's) reads are done
+#pragma unroll
+      for (int k = 0; k < G::E; ++k) {
+        double o = h ? v[k].y : v[k].x;
+        if constexpr (INV) o = h ? -o * scale : o * scale;
+        lds[S::pad(slot * G::N + t + k * G::T)] = o;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < G::E; ++q) tmp[h][q] = lds[S::pad(lt + q * G::WG)];
+    }
+#pragma unroll
+    for (int q = 0; q < G::E; ++q) {
+      const int64_t idx = base + lt + q * G::WG;
+      if (idx < total) st_nt(out + idx, cd{tmp[0][q], tmp[1][q]});
+    }
+  } else if (valid) {
     cd *dst = out + g * G::N;
 #pragma unroll
     for (int k = 0; k < G::E; ++k) {

@@ -122,6 +122,19 @@ def test_fft_sizes_vs_oracle(gdsp, oracle, n):
     assert nrel(gdsp.fft.FFT(x[0]), ref[0]) < TOL
 
 
+@pytest.mark.parametrize("n", [2, 4, 8, 16, 32, 64, 128, 256])
+def test_short_rows_many_blocks(gdsp, oracle, n):
+    # short transforms stage whole workgroup chunks through LDS: several
+    # blocks and a ragged last one, forward / inverse / real input
+    rng = np.random.default_rng(100 + n)
+    batch = (1 << 15) // n + 7
+    x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
+    assert row_nrel(gdsp.fft.FFTBatch(x), oracle.fft_rows(x)) < TOL
+    assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL
+    xr = x.real.copy()
+    assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
+
+
 @pytest.mark.parametrize("n", [1, 2, 8, 1024, 3000, 4096, 1 << 18])
 def test_fft_real(gdsp, oracle, n):
     rng = np.random.default_rng(7 + n)
