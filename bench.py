@@ -43,6 +43,12 @@ SQ_KERNELS = {"radix4096": ["fft_lds_kernel<12"], "bluestein3000": ["fft_mixed_f
               "fft2_8192": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"],
               "fft2_dist": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"]}
 SEED = 0x5EED
+# algorithmic bytes of one launch in the N=1 full-size configuration the
+# committed PMC (profiles/pmc_*.json) and SQ (profiles/r01/sq_counters.json)
+# summaries were measured on
+PROFILED_ALG_BYTES = {"radix4096": 32 * 4096 * 65536, "bluestein3000": 32 * 3000 * 65536,
+                      "chirpz3000": 32 * 3000 * 65536, "fft2_8192": 4 * 16 * 8192 * 8192,
+                      "fft2_dist": 4 * 16 * 8192 * 8192, "pwelch": 8 * (1 << 30)}
 
 
 def parse():
@@ -207,13 +213,18 @@ def main():
     total_samples = samples_per_step * args.steps * world
     value = total_samples / elapsed / 1e9
     achieved = alg_bytes / avg_launch_s / 1e9
+    # the committed PMC / SQ summaries were taken at the N=1 full-size
+    # configuration: scale them to this launch's share of that work (a rank's
+    # shard at N>1, or a --batch override)
+    share = alg_bytes / PROFILED_ALG_BYTES[w]
     traffic = None
     pmc = os.path.join(REPO, "profiles", f"pmc_{w}.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+            t = json.load(f).get("hbm_bytes_per_launch")
+        traffic = None if t is None else int(round(t * share))
 
-    fp64 = fp64_info(w, avg_launch_s)
+    fp64 = fp64_info(w, avg_launch_s, share)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -248,10 +259,11 @@ def main():
         dist.destroy_process_group()
 
 
-def fp64_info(workload: str, launch_s: float):
+def fp64_info(workload: str, launch_s: float, share: float = 1.0):
     """FP64 work of one launch (from the committed SQ counters, FFT2 summed
-    over its kernels) against the FP64 vector peak — the second roofline of
-    the compute-heavy paths (chirp-z, Pwelch)."""
+    over its kernels, times this launch's share of the profiled work)
+    against the FP64 vector peak — the second roofline of the compute-heavy
+    paths (chirp-z, Pwelch)."""
     path = os.path.join(REPO, "profiles", "r01", "sq_counters.json")
     ks = SQ_KERNELS.get("fft2_8192" if workload == "fft2_dist" else workload)
     if not ks or not os.path.exists(path):
@@ -264,6 +276,7 @@ def fp64_info(workload: str, launch_s: float):
         if not hit:
             return None
         flop += hit[0]["f64_flop"]
+    flop *= share
     tf = flop / launch_s / 1e12
     return {"flop_per_launch": flop, "achieved_tflops": round(tf, 2),
             "peak_tflops": FP64_PEAK_TFLOPS, "frac": round(tf / FP64_PEAK_TFLOPS, 4),
