@@ -1,0 +1,21 @@
+// fft_specs2.hip — compiled mixed-radix specialisations, group 2: 720 .. 2500.
+// Each Spec is a radix list (first pass .. last pass); the batched transform
+// and fused Pwelch kernels for it are instantiated here (mixed_fixed.hpp).
+// Radix lists: as few passes as the radices <= 25 allow, full waves where
+// possible, a power-of-2 radix last.
+#include "mixed_fixed.hpp"
+
+GDSP_SPEC_GROUP(specs2,
+                Spec<20, 9, 4>,  // 720
+                Spec<25, 5, 6>,  // 750
+                Spec<16, 6, 8>,  // 768
+                Spec<25, 2, 16>,  // 800
+                Spec<15, 15, 4>,  // 900
+                Spec<15, 9, 8>,  // 1080
+                Spec<16, 9, 8>,  // 1152
+                Spec<16, 10, 8>,  // 1280
+                Spec<15, 6, 16>,  // 1440
+                Spec<20, 5, 16>,  // 1600
+                Spec<15, 15, 8>,  // 1800
+                Spec<15, 9, 16>,  // 2160
+                Spec<25, 10, 10>)  // 2500

@@ -1,0 +1,22 @@
+// fft_specs3.hip — compiled mixed-radix specialisations, group 3: 2560 .. 8000 (above 4096 the exchange goes through LDS as re/im halves).
+// Each Spec is a radix list (first pass .. last pass); the batched transform
+// and fused Pwelch kernels for it are instantiated here (mixed_fixed.hpp).
+// Radix lists: as few passes as the radices <= 25 allow, full waves where
+// possible, a power-of-2 radix last.
+#include "mixed_fixed.hpp"
+
+GDSP_SPEC_GROUP(specs3,
+                Spec<16, 10, 16>,  // 2560
+                Spec<20, 9, 16>,  // 2880
+                Spec<20, 10, 16>,  // 3200
+                Spec<15, 15, 16>,  // 3600
+                Spec<20, 12, 16>,  // 3840
+                Spec<25, 20, 8>,  // 4000
+                Spec<25, 9, 20>,  // 4500
+                Spec<20, 15, 16>,  // 4800
+                Spec<25, 25, 8>,  // 5000
+                Spec<20, 16, 16>,  // 5120
+                Spec<25, 12, 20>,  // 6000
+                Spec<25, 16, 16>,  // 6400
+                Spec<25, 15, 20>,  // 7500
+                Spec<25, 20, 16>)  // 8000

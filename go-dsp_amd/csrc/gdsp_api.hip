@@ -315,7 +315,13 @@ int get_plan_locked(int dev, int64_t n, gdsp_plan **out);
 // a power of 2, too long, or has a prime factor above 13 (-> Bluestein).
 bool mixed_radices(int64_t n, std::vector<int> &rad, bool specs = true) {
   rad.clear();
-  if (n < 2 || n > gdsp::kMixedMax || is_pow2(n)) return false;
+  if (n < 2 || n > gdsp::kMixedSpecMax || is_pow2(n)) return false;
+  if (n > gdsp::kMixedMax) {  // beyond the runtime-radix kernel: specialisations only
+    int fr[16], fnp = 0;
+    if (!specs || !gdsp::mixed_fixed_radices((int)n, fr, &fnp)) return false;
+    rad.assign(fr, fr + fnp);
+    return true;
+  }
   int64_t m = n;
   int a = 0;
   while (m % 2 == 0) {
@@ -386,7 +392,10 @@ int build_mixed(int dev, int64_t n, const std::vector<int> &rad, gdsp_plan *p) {
   // the runtime-radix kernels (fused Pwelch) take the generic list: radices
   // <= 16, no composites (a compiled specialisation's list may hold them)
   std::vector<int> gen;
-  mixed_radices(n, gen, false);
+  if (!mixed_radices(n, gen, false)) {
+    p->md_gen = gdsp::MixedDesc{};  // no runtime-radix list (n > kMixedMax)
+    return GDSP_OK;
+  }
   if (gen == rad) {
     p->md_gen = p->md;
     p->tw_gen = p->tw;

@@ -23,6 +23,8 @@ struct MixedDesc {
   int n, npass, t1, tpw;
 };
 constexpr int kMixedMax = 4096;
+// compiled specialisations (fft_specs*.hip) reach this far (re/im exchange)
+constexpr int kMixedSpecMax = 8192;
 // fused Pwelch over a mixed-radix segment length d.n = max(pad, nfft) with
 // d.npass >= 2 (fft_mixed.hip); same partial layout as launch_pwelch
 hipError_t launch_pwelch_mixed(const MixedDesc &d, const double *x, int64_t nfft, int64_t stride,

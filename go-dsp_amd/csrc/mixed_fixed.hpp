@@ -1,0 +1,438 @@
+// mixed_fixed.hpp — compile-time mixed-radix specialisations: the inlined
+// pass chain (FPass / fixed_chain), the batched transform kernel and the
+// fused Pwelch kernel on it, and GDSP_SPEC_GROUP, which instantiates a list
+// of radix lists in one translation unit (fft_specs*.hip).
+#pragma once
+#include <stdlib.h>
+
+#include <tuple>
+
+#include "mixed_core.hpp"
+
+namespace gdsp {
+
+// ---------------------------------------------------------------------------
+// Compile-time specialisations for frequent lengths (BASELINE config 3 is
+// n = 3000): n, Ns, the thread count and the twiddle offsets are known to the
+// compiler and every pass is inlined. Each pass is load -> twiddle + DFT ->
+// store; between passes the data crosses LDS either as complex128 (one
+// exchange, two barriers) or, with SPLIT, as real then imaginary halves
+// through an n-double buffer (half the LDS, so more workgroups per CU, for
+// four barriers).
+template <int R, int N, int NS, int T1>
+struct FPass {
+  static constexpr int NB = N / R;
+  static constexpr int J = (NB + T1 - 1) / T1;
+  static constexpr bool FULL = NB % T1 == 0;
+  cd v[J][R];
+
+  __device__ __forceinline__ static bool act(int j, bool valid) {
+    return valid && (FULL || j < NB);
+  }
+  template <bool INV, int LOAD>
+  __device__ __forceinline__ void load_hbm(int tl, bool valid, const void *__restrict__ gin) {
+#pragma unroll
+    for (int jj = 0; jj < J; ++jj) {
+      const int j = tl + jj * T1;
+      if (act(j, valid)) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if constexpr (LOAD == LOAD_REAL) {
+            v[jj][r] = {reinterpret_cast<const double *>(gin)[j + r * NB], 0.0};
+          } else {
+            v[jj][r] = reinterpret_cast<const cd *>(gin)[j + r * NB];
+            if constexpr (INV) v[jj][r].y = -v[jj][r].y;
+          }
+        }
+      }
+    }
+  }
+  // PART 0: real halves, 1: imaginary halves (double buffer), 2: complex
+  template <int PART, bool SWZ>
+  __device__ __forceinline__ void load_lds(int tl, bool valid, void *lds) {
+#pragma unroll
+    for (int jj = 0; jj < J; ++jj) {
+      const int j = tl + jj * T1;
+      if (act(j, valid)) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int i = SWZ ? lsw(j + r * NB) : j + r * NB;
+          if constexpr (PART == 2) {
+            v[jj][r] = reinterpret_cast<const cd *>(lds)[i];
+          } else if constexpr (PART == 0) {
+            v[jj][r].x = reinterpret_cast<const double *>(lds)[i];
+          } else {
+            v[jj][r].y = reinterpret_cast<const double *>(lds)[i];
+          }
+        }
+      }
+    }
+  }
+  __device__ __forceinline__ void compute(int tl, bool valid, const cd *__restrict__ tw) {
+#pragma unroll
+    for (int jj = 0; jj < J; ++jj) {
+      const int j = tl + jj * T1;
+      if (act(j, valid)) {
+        if constexpr (NS > 1) twiddle_chain<R>(v[jj], tw[j % NS]);
+        dft_any<R>(v[jj]);
+      }
+    }
+  }
+  template <int PART, bool SWZ>
+  __device__ __forceinline__ void store_lds(int tl, bool valid, void *lds) const {
+#pragma unroll
+    for (int jj = 0; jj < J; ++jj) {
+      const int j = tl + jj * T1;
+      if (act(j, valid)) {
+        const int k = j % NS, o = (j - k) * R + k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int i = SWZ ? lsw(o + r * NS) : o + r * NS;
+          if constexpr (PART == 2) {
+            reinterpret_cast<cd *>(lds)[i] = v[jj][r];
+          } else if constexpr (PART == 0) {
+            reinterpret_cast<double *>(lds)[i] = v[jj][r].x;
+          } else {
+            reinterpret_cast<double *>(lds)[i] = v[jj][r].y;
+          }
+        }
+      }
+    }
+  }
+  template <bool INV>
+  __device__ __forceinline__ void store_hbm(int tl, bool valid, cd *__restrict__ gout,
+                                            double scale) const {
+#pragma unroll
+    for (int jj = 0; jj < J; ++jj) {
+      const int j = tl + jj * T1;
+      if (act(j, valid)) {
+        const int k = j % NS, o = (j - k) * R + k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          cd y = v[jj][r];
+          if constexpr (INV) y = {y.x * scale, -y.y * scale};
+          gout[o + r * NS] = y;
+        }
+      }
+    }
+  }
+};
+
+// exchange prev -> pass (R, NS) through LDS, compute it, then continue
+template <bool INV, bool SPLIT, bool SWZ, int N, int T1, int NS, int TWOFF, class Prev, int R,
+          int... REST>
+__device__ __forceinline__ void fixed_chain(const Prev &prev, int tl, bool valid, cd *gout,
+                                            void *lds, const cd *tw, double scale) {
+  FPass<R, N, NS, T1> cur;
+  if constexpr (SPLIT) {
+    prev.template store_lds<0, SWZ>(tl, valid, lds);
+    __syncthreads();
+    cur.template load_lds<0, SWZ>(tl, valid, lds);
+    __syncthreads();
+    prev.template store_lds<1, SWZ>(tl, valid, lds);
+    __syncthreads();
+    cur.template load_lds<1, SWZ>(tl, valid, lds);
+  } else {
+    prev.template store_lds<2, SWZ>(tl, valid, lds);
+    __syncthreads();
+    cur.template load_lds<2, SWZ>(tl, valid, lds);
+  }
+  cur.compute(tl, valid, tw + TWOFF);
+  if constexpr (sizeof...(REST) == 0) {
+    cur.template store_hbm<INV>(tl, valid, gout, scale);
+  } else {
+    __syncthreads();  // every read of this exchange lands before the next one's writes
+    fixed_chain<INV, SPLIT, SWZ, N, T1, NS * R, TWOFF + NS, FPass<R, N, NS, T1>, REST...>(
+        cur, tl, valid, gout, lds, tw, scale);
+  }
+}
+
+template <int R0, int... RS>
+struct FixedGeo {
+  static constexpr int N = R0 * (RS * ... * 1);
+  static constexpr int need() {
+    int m = 1;
+    for (int r : {R0, RS...}) {
+      const int nb = N / r, jm = r > 16 ? 1 : 16 / r, q = (nb + jm - 1) / jm;
+      m = q > m ? q : m;
+    }
+    return m;
+  }
+  static constexpr int T1 = need();
+  static constexpr int SLOTS = (N + 7) & ~7;
+  // transforms per workgroup: about 256 threads, within 64 KiB of LDS
+  static constexpr int tpw() {
+    int t = 256 / T1 > 1 ? 256 / T1 : 1;
+    while (t > 1 && t * SLOTS * 16 > 65536) --t;
+    return t;
+  }
+  static constexpr int TPW = tpw();
+  static constexpr int WG = TPW * T1;
+};
+
+template <bool INV, int LOAD, bool SPLIT, bool SWZ, int R0, int... RS>
+__global__ __launch_bounds__((FixedGeo<R0, RS...>::WG)) void fft_mixed_fixed_kernel(
+    const void *__restrict__ in, cd *__restrict__ out, int64_t batch, const cd *__restrict__ tw,
+    double scale) {
+  using G = FixedGeo<R0, RS...>;
+  __shared__ double lds[G::TPW * (SPLIT ? G::SLOTS : 2 * G::SLOTS)];
+  const int sub = G::TPW == 1 ? 0 : (int)threadIdx.x / G::T1;
+  const int tl = (int)threadIdx.x - sub * G::T1;
+  const int64_t row = xcd_remap(blockIdx.x, gridDim.x) * G::TPW + sub;
+  const bool valid = row < batch;
+  const void *gin = LOAD == LOAD_REAL
+                        ? (const void *)(reinterpret_cast<const double *>(in) + row * G::N)
+                        : (const void *)(reinterpret_cast<const cd *>(in) + row * G::N);
+  double *ld = lds + sub * (SPLIT ? G::SLOTS : 2 * G::SLOTS);
+  FPass<R0, G::N, 1, G::T1> p0;
+  p0.template load_hbm<INV, LOAD>(tl, valid, gin);
+  p0.compute(tl, valid, tw);
+  if constexpr (sizeof...(RS) == 0)
+    p0.template store_hbm<INV>(tl, valid, out + row * G::N, scale);
+  else
+    fixed_chain<INV, SPLIT, SWZ, G::N, G::T1, R0, 0, FPass<R0, G::N, 1, G::T1>, RS...>(
+        p0, tl, valid, out + row * G::N, ld, tw, scale);
+}
+
+template <bool SPLIT, int... RS>
+static bool launch_fixed(const MixedDesc &d, bool inv, int load, const void *in, cd *out,
+                         int64_t batch, const cd *tw, double scale, hipStream_t s) {
+  using G = FixedGeo<RS...>;
+  // an odd first radix writes stride-R slots that are conflict-free as they
+  // are; an even one goes through the swizzle
+  constexpr int R0 = [] { constexpr int r[] = {RS...}; return r[0]; }();
+  constexpr bool SWZ = R0 % 2 == 0;
+  uint64_t codes = 0;
+  int q = 0;
+  for (int r : {RS...}) codes |= (uint64_t)r << (5 * q++);
+  if (d.n != G::N || d.codes != codes) return false;
+  const dim3 grid((unsigned)((batch + G::TPW - 1) / G::TPW)), block(G::WG);
+  if (inv)
+    hipLaunchKernelGGL((fft_mixed_fixed_kernel<true, LOAD_COMPLEX, SPLIT, SWZ, RS...>), grid,
+                       block, 0, s, in, out, batch, tw, scale);
+  else if (load == LOAD_REAL)
+    hipLaunchKernelGGL((fft_mixed_fixed_kernel<false, LOAD_REAL, SPLIT, SWZ, RS...>), grid,
+                       block, 0, s, in, out, batch, tw, scale);
+  else
+    hipLaunchKernelGGL((fft_mixed_fixed_kernel<false, LOAD_COMPLEX, SPLIT, SWZ, RS...>), grid,
+                       block, 0, s, in, out, batch, tw, scale);
+  return true;
+}
+
+template <int... RS>
+struct Spec {};
+
+template <int... RS>
+static bool spec_radices(Spec<RS...>, int n, int *rad, int *npass) {
+  if (n != (RS * ...)) return false;
+  int q = 0;
+  for (int r : {RS...}) rad[q++] = r;
+  *npass = q;
+  return true;
+}
+template <class... S>
+static bool find_spec(std::tuple<S...>, int n, int *rad, int *npass) {
+  return (spec_radices(S{}, n, rad, npass) || ...);
+}
+template <int... RS>
+static bool spec_launch(Spec<RS...>, const MixedDesc &d, bool inv, int load, const void *in,
+                        cd *out, int64_t batch, const cd *tw, double scale, hipStream_t s) {
+  // above 4096 points the complex exchange would exceed 64 KiB: re/im halves
+  return launch_fixed<(FixedGeo<RS...>::N > 4096), RS...>(d, inv, load, in, out, batch, tw, scale,
+                                                          s);
+}
+template <class... S>
+static bool launch_spec(std::tuple<S...>, const MixedDesc &d, bool inv, int load, const void *in,
+                        cd *out, int64_t batch, const cd *tw, double scale, hipStream_t s) {
+  return (spec_launch(S{}, d, inv, load, in, out, batch, tw, scale, s) || ...);
+}
+
+// ---------------------------------------------------------------------------
+// Fused Welch accumulation on a compiled specialisation (spectral/pwelch.go:
+// 104-122 for smooth NFFT / Pad = a specialised length): the same packed
+// segment pairs as pwelch_kernel (z = w*x_s0 + i*w*x_s1, the k / F-k fold in
+// finalise), but every pass inlined with compile-time radices instead of the
+// runtime-radix pass functions of pwelch_mixed_kernel. Each workgroup slot is
+// one persistent worker; the power sums of the bins a thread's last-pass
+// butterflies produce stay in its registers across the worker's pairs.
+
+// fixed_chain with the last pass handed to a sink instead of stored
+template <bool SPLIT, bool SWZ, int N, int T1, int NS, int TWOFF, class Prev, class F, int R,
+          int... REST>
+__device__ __forceinline__ void fixed_chain_to(const Prev &prev, int tl, bool valid, void *lds,
+                                               const cd *tw, F &sink) {
+  FPass<R, N, NS, T1> cur;
+  if constexpr (SPLIT) {
+    prev.template store_lds<0, SWZ>(tl, valid, lds);
+    __syncthreads();
+    cur.template load_lds<0, SWZ>(tl, valid, lds);
+    __syncthreads();
+    prev.template store_lds<1, SWZ>(tl, valid, lds);
+    __syncthreads();
+    cur.template load_lds<1, SWZ>(tl, valid, lds);
+  } else {
+    prev.template store_lds<2, SWZ>(tl, valid, lds);
+    __syncthreads();
+    cur.template load_lds<2, SWZ>(tl, valid, lds);
+  }
+  cur.compute(tl, valid, tw + TWOFF);
+  if constexpr (sizeof...(REST) == 0) {
+    sink(cur);
+  } else {
+    __syncthreads();
+    fixed_chain_to<SPLIT, SWZ, N, T1, NS * R, TWOFF + NS, FPass<R, N, NS, T1>, F, REST...>(
+        cur, tl, valid, lds, tw, sink);
+  }
+}
+
+template <int R0, int... RS>
+struct FixedLast {
+  static constexpr int rr[] = {R0, RS...};
+  static constexpr int R = rr[sizeof...(RS)];
+  static constexpr int N = FixedGeo<R0, RS...>::N;
+  using Pass = FPass<R, N, N / R, FixedGeo<R0, RS...>::T1>;
+};
+
+template <bool SWZ, int R0, int... RS>
+__global__ __launch_bounds__((FixedGeo<R0, RS...>::WG)) void pwelch_fixed_kernel(
+    const double *__restrict__ x, int64_t nfft, int64_t stride, int64_t seg_begin,
+    int64_t seg_end, int64_t pairs_per_worker, const double *__restrict__ win,
+    const cd *__restrict__ tw, double *__restrict__ partial) {
+  static_assert(sizeof...(RS) >= 1, "at least two passes");
+  using G = FixedGeo<R0, RS...>;
+  using L = FixedLast<R0, RS...>;
+  using First = FPass<R0, G::N, 1, G::T1>;
+  constexpr bool SPL = G::N > 4096;  // re/im halves: the complex exchange would exceed 64 KiB
+  __shared__ double lds[G::TPW * (SPL ? 1 : 2) * G::SLOTS];
+  const int sub = G::TPW == 1 ? 0 : (int)threadIdx.x / G::T1;
+  const int tl = (int)threadIdx.x - sub * G::T1;
+  const int64_t worker = (int64_t)blockIdx.x * G::TPW + sub;
+  double *ld = lds + sub * (SPL ? 1 : 2) * G::SLOTS;
+  const int64_t npairs = (seg_end - seg_begin + 1) / 2;
+  const int64_t p0 = worker * pairs_per_worker;
+  double acc[L::Pass::J][L::R];
+#pragma unroll
+  for (int jj = 0; jj < L::Pass::J; ++jj)
+#pragma unroll
+    for (int r = 0; r < L::R; ++r) acc[jj][r] = 0.0;
+  for (int64_t it = 0; it < pairs_per_worker; ++it) {
+    const int64_t p = p0 + it;
+    const bool active = p < npairs;
+    const int64_t s0 = seg_begin + 2 * (active ? p : 0);
+    const bool has1 = active && s0 + 1 < seg_end;
+    const double *x0 = opaque_ptr(x) + s0 * stride, *x1 = x0 + stride;
+    // laundered per pair: otherwise the compiler hoists the loop-invariant
+    // window values and twiddle power chains out of the loop, and the
+    // registers they pin halve the occupancy
+    const double *w = opaque_ptr(win);
+    const cd *twp = opaque_ptr(tw);
+    const int tt = opaque_int(tl);
+    First f0;
+#pragma unroll
+    for (int jj = 0; jj < First::J; ++jj) {
+      const int j = tt + jj * G::T1;
+      if (First::act(j, true)) {
+#pragma unroll
+        for (int r = 0; r < R0; ++r) {
+          const int i = j + r * First::NB;
+          double a = 0.0, b = 0.0;
+          if (active && i < nfft) {
+            const double wi = w[i];
+            a = wi * x0[i];
+            if (has1) b = wi * x1[i];
+          }
+          f0.v[jj][r] = {a, b};
+        }
+      }
+    }
+    f0.compute(tt, true, twp);
+    if (it > 0) __syncthreads();  // the previous pair's last exchange reads are done
+    auto sink = [&](const typename L::Pass &c) {
+      if (!active) return;
+#pragma unroll
+      for (int jj = 0; jj < L::Pass::J; ++jj) {
+        const int j = tt + jj * G::T1;
+        if (L::Pass::act(j, true)) {
+#pragma unroll
+          for (int r = 0; r < L::R; ++r)
+            acc[jj][r] += c.v[jj][r].x * c.v[jj][r].x + c.v[jj][r].y * c.v[jj][r].y;
+        }
+      }
+    };
+    fixed_chain_to<SPL, SWZ, G::N, G::T1, R0, 0, First, decltype(sink), RS...>(f0, tt, true, ld,
+                                                                              twp, sink);
+  }
+  if (p0 < npairs) {
+    double *dst = partial + worker * G::N;
+#pragma unroll
+    for (int jj = 0; jj < L::Pass::J; ++jj) {
+      const int j = tl + jj * G::T1;
+      if (L::Pass::act(j, true)) {
+        constexpr int NSL = G::N / L::R;
+        const int k = j % NSL, o = (j - k) * L::R + k;
+#pragma unroll
+        for (int r = 0; r < L::R; ++r) dst[o + r * NSL] = acc[jj][r];
+      }
+    }
+  }
+}
+
+template <int... RS>
+static int spec_pw_tpw(Spec<RS...>, const MixedDesc &d) {
+  uint64_t codes = 0;
+  int q = 0;
+  for (int r : {RS...}) codes |= (uint64_t)r << (5 * q++);
+  return (d.n == FixedGeo<RS...>::N && d.codes == codes) ? FixedGeo<RS...>::TPW : 0;
+}
+template <class... S>
+static int find_pw_tpw(std::tuple<S...>, const MixedDesc &d) {
+  int t = 0;
+  ((t = t ? t : spec_pw_tpw(S{}, d)), ...);
+  return t;
+}
+
+template <int... RS>
+static bool spec_pw_launch(Spec<RS...>, const MixedDesc &d, const double *x, int64_t nfft,
+                           int64_t stride, int64_t seg_begin, int64_t seg_end, int64_t ppw,
+                           int64_t nworkers, const double *win, const cd *tw, double *partial,
+                           hipStream_t s) {
+  if (!spec_pw_tpw(Spec<RS...>{}, d)) return false;
+  using G = FixedGeo<RS...>;
+  constexpr int R0 = [] { constexpr int r[] = {RS...}; return r[0]; }();
+  const dim3 grid((unsigned)((nworkers + G::TPW - 1) / G::TPW)), block(G::WG);
+  hipLaunchKernelGGL((pwelch_fixed_kernel<R0 % 2 == 0, RS...>), grid, block, 0, s, x, nfft, stride,
+                     seg_begin, seg_end, ppw, win, tw, partial);
+  return true;
+}
+template <class... S>
+static bool launch_pw_spec(std::tuple<S...>, const MixedDesc &d, const double *x, int64_t nfft,
+                           int64_t stride, int64_t seg_begin, int64_t seg_end, int64_t ppw,
+                           int64_t nworkers, const double *win, const cd *tw, double *partial,
+                           hipStream_t s) {
+  return (spec_pw_launch(S{}, d, x, nfft, stride, seg_begin, seg_end, ppw, nworkers, win, tw,
+                         partial, s) ||
+          ...);
+}
+
+}  // namespace gdsp
+
+// One translation unit per group of specialisations (fft_specs*.hip), so the
+// groups compile in parallel; fft_mixed.hip asks each group in turn.
+#define GDSP_SPEC_GROUP(NAME, ...)                                                            \
+  namespace gdsp {                                                                            \
+  using NAME##_list = std::tuple<__VA_ARGS__>;                                                \
+  bool NAME##_find(int n, int *rad, int *npass) {                                             \
+    return find_spec(NAME##_list{}, n, rad, npass);                                           \
+  }                                                                                           \
+  bool NAME##_launch(const MixedDesc &d, bool inv, int load, const void *in, cd *out,         \
+                     int64_t batch, const cd *tw, double scale, hipStream_t s) {             \
+    return launch_spec(NAME##_list{}, d, inv, load, in, out, batch, tw, scale, s);            \
+  }                                                                                           \
+  int NAME##_pw_tpw(const MixedDesc &d) { return find_pw_tpw(NAME##_list{}, d); }            \
+  bool NAME##_pw_launch(const MixedDesc &d, const double *x, int64_t nfft, int64_t stride,    \
+                        int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,   \
+                        const double *win, const cd *tw, double *partial, hipStream_t s) {   \
+    return launch_pw_spec(NAME##_list{}, d, x, nfft, stride, seg_begin, seg_end, ppw,         \
+                          nworkers, win, tw, partial, s);                                     \
+  }                                                                                           \
+  }

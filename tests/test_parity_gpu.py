@@ -224,7 +224,10 @@ WINDOWS = {"hann": "Hann", "hamming": "Hamming", "rectangular": "Rectangular",
     (12345, 960, 0, 1200, "hamming"),  # Pad > NFFT, both smooth
     (9999, 1500, 700, 0, "blackman"),
     (50000, 4095, 2000, 0, "hann"),    # 13*7*5*3*3: five passes
-    (30000, 800, 400, 0, "hann"),      # no compiled specialisation: runtime radices
+    (30000, 810, 400, 0, "hann"),      # no compiled specialisation: runtime radices
+    (60000, 6000, 3000, 0, "hann"),    # specialisation above 4096 (re/im exchange)
+    (20000, 360, 180, 0, "bartlett"),  # three passes, radix 3 in the middle
+    (9000, 100, 0, 0, "hann"),         # two passes, many workers per block
     # compiled specialisations (pwelch_fixed_kernel): several workers per block,
     # odd segment counts, no overlap
     (200000, 480, 240, 0, "hann"),
@@ -285,7 +288,8 @@ def test_plan_kinds(gdsp):
     assert D.plan(3000).kind == 5  # 2^3 3 5^3: mixed radix
     assert D.plan(4097).kind == 3  # 17 * 241: fused Bluestein
     assert D.plan(10000).kind == 6  # 100 x 100: mixed four-step
-    assert D.plan(5000).kind == 3  # smooth but M = 16384: the fused chirp-z is faster
+    assert D.plan(5000).kind == 5  # a compiled specialisation above 4096 (25*25*8)
+    assert D.plan(5400).kind == 3  # smooth, no specialisation, M = 16384: fused chirp-z
     assert D.plan(8209).kind == 4  # prime, M = 32768: composed Bluestein
     assert D.plan(3000, chirpz=True).kind == 3
     assert D.plan(10000, chirpz=True).kind == 4
@@ -298,12 +302,18 @@ MIXED = [3, 5, 6, 7, 10, 11, 12, 13, 14, 18, 20, 21, 22, 24, 25, 26, 27, 39, 48,
          81, 96, 100, 121, 125, 143, 169, 243, 343, 360, 625, 720, 729, 1000, 1001, 1331, 1536,
          2048 + 1024, 2187, 2197, 2401, 2500, 3000, 3125, 3375, 3840, 4000, 4095, 4050, 19 * 5,
          17 * 3,
-         # the compiled specialisations (fft_mixed.hip Specs)
-         480, 960, 1200, 1500, 1920, 2000, 2400]
+         # the compiled specialisations (fft_specs*.hip): group 0, and the
+         # two-pass / three-pass / above-4096 (re/im exchange) lists of 1-3
+         480, 960, 1200, 1500, 1920, 2000, 2400,
+         120, 160, 500, 600, 640, 750, 768, 800, 900, 1152, 1600, 2160, 2880, 4500, 5000,
+         5120, 6000, 6400, 7500, 8000]
 
 
 @pytest.mark.parametrize("n", MIXED)
 def test_mixed_radix_vs_oracle(gdsp, oracle, n):
+    if n > 4096:  # specialisations only beyond the runtime-radix kernel
+        D = __import__("importlib").import_module("go-dsp_amd.device")
+        assert D.plan(n).kind == 5, n
     rng = np.random.default_rng(1000 + n)
     batch = 5
     x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
