@@ -1,5 +1,7 @@
 // fft_mixed.hip — one-kernel mixed-radix Stockham FFT for non-power-of-2
-// lengths whose prime factors are all in {2, 3, 5, 7, 11, 13} (n <= 4096).
+// lengths whose prime factors are all in {2, 3, 5, 7, 11, 13}: the
+// runtime-radix kernels (n <= 4096) and the dispatch to the compiled
+// specialisations (fft_specs*.hip, n <= 8192).
 //
 // The reference computes every non-power-of-2 length with Bluestein's chirp-z
 // (fft/fft.go:86 -> fft/bluestein.go:68-94): three radix-2 FFTs of
@@ -21,7 +23,6 @@
 #include "mixed_specs.hpp"
 
 #include <stdlib.h>
-
 
 namespace gdsp {
 

@@ -17,7 +17,9 @@ constexpr int kMaxLdsLog2 = 14;
 hipError_t launch_fft_lds(int log2n, bool inv, int load, bool split, const void *in, cd *out,
                           int64_t batch, const cd *tw, double scale, hipStream_t s);
 // Mixed-radix one-kernel transform (fft_mixed.hip): n = prod of the radices
-// in `codes` (5 bits per pass, radices 2,3,4,5,7,8,11,13,16), n <= kMixedMax.
+// in `codes` (5 bits per pass, radices 2,3,4,5,7,8,11,13,16 in the runtime-radix
+// kernels, also 6,9,10,12,15,20,25 in the compiled specialisations), n <= kMixedMax
+// (kMixedSpecMax for a specialisation).
 struct MixedDesc {
   uint64_t codes;
   int n, npass, t1, tpw;
