@@ -48,7 +48,8 @@ SEED = 0x5EED
 # summaries were measured on
 PROFILED_ALG_BYTES = {"radix4096": 32 * 4096 * 65536, "bluestein3000": 32 * 3000 * 65536,
                       "chirpz3000": 32 * 3000 * 65536, "fft2_8192": 4 * 16 * 8192 * 8192,
-                      "fft2_dist": 4 * 16 * 8192 * 8192, "pwelch": 8 * (1 << 30)}
+                      "fft2_dist": 4 * 16 * 8192 * 8192, "pwelch": 8 * (1 << 30),
+                      "fftn_512": 3 * 2 * 16 * 512 ** 3, "wav_decode": 10 * (1 << 30)}
 
 
 def parse():
@@ -58,7 +59,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="radix4096",
                     choices=["radix4096", "bluestein3000", "chirpz3000", "fft2_8192", "fft2_dist",
-                             "pwelch"])
+                             "pwelch", "fftn_512", "wav_decode"])
     ap.add_argument("--batch", type=int, default=0, help="rows per GPU (0 = config default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU seconds for the cpu_baseline sample (0 disables)")
@@ -152,6 +153,43 @@ def main():
                "rows": R, "cols": C, "parallelism": f"rows{world}+alltoall"}
         kernel = "fft2_sharded (all launches and both all-to-alls)"
         metric = "Gsamples/s, fft.FFT2 8192x8192 complex128"
+    elif w == "fftn_512":  # fft.FFTN of a 512^3 complex128 Matrix
+        dims = (512, 512, 512)
+        x = torch.empty(dims, dtype=torch.complex128, device=dev)
+        y = torch.empty_like(x)
+        D.fill_uniform(x, SEED, offset=rank * x.numel() * 2, stream=stream)
+
+        def step():
+            D.fftn(x, y, stream=stream)
+
+        samples_per_step = x.numel()
+        alg_bytes = 3 * 2 * 16 * x.numel()  # each axis: one read + one write
+        cfg = {"workload": "fft.FFTN complex128 512x512x512 (computeFFTN, fft.go:157-192)",
+               "dims": list(dims), "parallelism": f"replicas{world}"}
+        kernel = "fftn (all launches: rows, then two column-tile axes)"
+        metric = "Gsamples/s, fft.FFTN 512^3 complex128"
+    elif w == "wav_decode":  # wav.ReadFloats -> float64 Pwelch input
+        wav = importlib.import_module("go-dsp_amd.wav")
+        count = 1 << 30
+        raw = torch.empty(2 * count, dtype=torch.uint8, device=dev)
+        # synthetic PCM16 little-endian samples: the bytes of a uniform stream
+        u = torch.empty(count // 4, dtype=torch.float64, device=dev)
+        D.fill_uniform(u, SEED, offset=rank * count, stream=stream)
+        torch.cuda.synchronize()
+        raw.view(torch.float64).copy_(u)
+        del u
+        y = torch.empty(count, dtype=torch.float64, device=dev)
+
+        def step():
+            wav.device_floats(raw, count, 1, 16, out=y, stream=stream)
+
+        samples_per_step = count
+        alg_bytes = 10 * count  # 2 B PCM16 in, 8 B float64 out
+        cfg = {"workload": "wav.ReadFloats PCM16 -> float64 Pwelch input, 2^30 samples "
+                           "(wav.go:135-161)", "samples": count, "format": "PCM16",
+               "parallelism": f"replicas{world}"}
+        kernel = "wav_decode_vec_kernel<16, f64>"
+        metric = "Gsamples/s, wav.ReadFloats PCM16 2^30 samples"
     else:  # pwelch: 2^30 samples total, NFFT 4096, 50 % overlap, Hann (strong scaling)
         Dd = importlib.import_module("go-dsp_amd.distributed")
         nfft, nov = 4096, 2048
@@ -209,6 +247,14 @@ def main():
         ref = oracle.fft_rows(xs)
         err = max(float(np.linalg.norm(a - b) / np.linalg.norm(b)) for a, b in zip(ys, ref))
         check = {"rows": len(rows), "max_nrel_vs_oracle": err}
+    if rank == 0 and args.check_rows > 0 and w == "wav_decode":
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import numpy as np
+        import oracle
+        m = 1 << 20
+        ref = oracle.wav_floats(raw[:2 * m].cpu().numpy().tobytes(), m, 1, 16)
+        got = y[:m].cpu().numpy()
+        check = {"samples": m, "bit_exact": bool(np.array_equal(got, ref.astype(np.float64)))}
 
     total_samples = samples_per_step * args.steps * world
     value = total_samples / elapsed / 1e9
@@ -242,7 +288,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if w in ("pwelch", "fft2_dist") else "weak",
             "vs_baseline": None,
-            "dtype": "f64 (complex128)",
+            "dtype": "pcm16 -> f64" if w == "wav_decode" else "f64 (complex128)",
             "data": "synthetic (splitmix64 uniform[-1,1), generated in HBM)",
             "config": cfg,
             "roofline": {"bound": "hbm", "kernel": kernel,
@@ -308,6 +354,35 @@ def cpu_baseline(workload: str, seconds: float):
                 "kind": "port",
                 "sample": f"spectral.Pwelch on a {n}-sample prefix of the stream "
                           f"(NFFT 4096, 50% overlap, {dt:.1f} s), {pool}"}
+    if workload == "wav_decode":
+        # wav.ReadFloats's conversion restated (oracle/oracle.c), one thread
+        raw = oracle.fill_uniform(1 << 21, SEED).view(np.uint8)
+        count = raw.size // 2
+        done = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            oracle.wav_floats(raw, count, 1, 16)
+            done += count
+        dt = time.perf_counter() - t0
+        return {"value": round(done / dt / 1e9, 6), "unit": "Gsamples/s", "cores": 1,
+                "kind": "port",
+                "sample": f"{done} PCM16 samples ({dt:.1f} s) through the ReadFloats "
+                          f"restatement (wav/wav.go:135-161), float32 out as the reference"}
+    if workload == "fftn_512":
+        # computeFFTN (fft.go:157-192): 3 x 512^2 line FFTs of 512; the
+        # strided gather/scatter of axes 0 and 1 is not charged (favours the CPU)
+        x = oracle.fill_uniform(2 * 512 * 256, SEED).view(np.complex128).reshape(256, 512)
+        done = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            oracle.fft_rows_threaded(x, cores)
+            done += 256
+        dt = time.perf_counter() - t0
+        t_fftn = 3 * 512 * 512 * dt / done
+        return {"value": round(512 ** 3 / t_fftn / 1e9, 6), "unit": "Gsamples/s",
+                "cores": cores, "kind": "port",
+                "sample": f"{done} fft.FFT calls of N=512 ({dt:.1f} s) extrapolated to the "
+                          f"786432 line FFTs of one 512^3 FFTN, {pool}"}
     if workload == "fft2_dist":
         workload = "fft2_8192"
     n = {"radix4096": 4096, "bluestein3000": 3000, "chirpz3000": 3000, "fft2_8192": 8192}[workload]

@@ -84,6 +84,23 @@ def fft2(x, out=None, inverse: bool = False, work=None, stream=None):
     return out
 
 
+def fftn(x, out=None, inverse: bool = False, stream=None):
+    """FFTN/IFFTN (fft/fft.go:157-192) of a contiguous complex128 CUDA tensor
+    of any rank: every axis in turn (gdsp_fftn_device)."""
+    torch = _torch()
+    assert x.is_cuda and x.dtype == torch.complex128 and x.is_contiguous() and x.dim() >= 1
+    if out is None:
+        out = torch.empty_like(x)
+    assert out.shape == x.shape and out.is_contiguous()
+    if x.numel() == 0:
+        return out
+    dims = (ctypes.c_int64 * x.dim())(*x.shape)
+    with torch.cuda.device(x.device):
+        check(lib().gdsp_fftn_device(_ptr(x), _ptr(out), dims, x.dim(), int(inverse),
+                                     _stream_ptr(stream, x.device)), "fftn_device")
+    return out
+
+
 def fft_axis(x, axis: int, out=None, inverse: bool = False, stream=None):
     """The 1-D FFT/IFFT along one axis of a contiguous complex128 CUDA tensor
     (gdsp_fft_axis_device; axis 0 of a matrix = computeFFT2's column pass)."""

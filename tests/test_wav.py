@@ -139,10 +139,13 @@ def test_device_feeder_formats(gdsp, oracle):
         if fmt == 3:
             raw = rng.standard_normal(count).astype("<f4").tobytes()
         want = oracle.wav_floats(raw, count, fmt, bits)
-        # odd offset: the data chunk of a file uploaded whole is not aligned
-        dev = torch.frombuffer(bytearray(b"x" + raw), dtype=torch.uint8).cuda()[1:]
-        got = gdsp.wav.device_floats(dev, count, fmt, bits).cpu().numpy()
-        assert np.array_equal(got, want.astype(np.float64))
+        # aligned: the 16-B-per-lane kernel plus the byte-load tail (count is
+        # not a multiple of the samples per load); odd offset: the data chunk
+        # of a file uploaded whole is not aligned, byte loads throughout
+        for off in (0, 1):
+            dev = torch.frombuffer(bytearray(b"x" * off + raw), dtype=torch.uint8).cuda()[off:]
+            got = gdsp.wav.device_floats(dev, count, fmt, bits).cpu().numpy()
+            assert np.array_equal(got, want.astype(np.float64)), (fmt, off)
         host32 = gdsp.wav.read_floats(raw, count, fmt, bits)
         assert np.array_equal(host32.view(np.uint32), want.view(np.uint32))
         host64 = gdsp.wav.read_floats(raw, count, fmt, bits, f64=True)

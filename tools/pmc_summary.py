@@ -16,7 +16,10 @@ KERNELS = {"radix4096": "fft_lds_kernel<12", "bluestein3000": "fft_mixed_fixed_k
            "chirpz3000": "bluestein_kernel<13",
            "pwelch": "pwelch_half_kernel<12",
            # one FFT2 step = row pass + the two column-tile launches: summed
-           "fft2_8192": ["fft_lds_kernel<13", "colfft_tile_kernel<7", "colfft_tile_kernel<6"]}
+           "fft2_8192": ["fft_lds_kernel<13", "colfft_tile_kernel<7", "colfft_tile_kernel<6"],
+           # one FFTN step = the row pass + two column-tile axes
+           "fftn_512": ["fft_lds_kernel<9", ("colfft_tile_kernel<9", 2)],
+           "wav_decode": "wav_decode_vec_kernel"}
 
 
 def values(w, counter, kernel):
@@ -30,10 +33,11 @@ def main(w, tag):
     f_kib = w_kib = 0.0
     fetch = write = []
     for k in ks:
+        k, mult = k if isinstance(k, tuple) else (k, 1)  # launches of k per step
         fetch, pf = values(w, "FETCH_SIZE", k)
         write, pw = values(w, "WRITE_SIZE", k)
-        f_kib += statistics.median(fetch)
-        w_kib += statistics.median(write)
+        f_kib += mult * statistics.median(fetch)
+        w_kib += mult * statistics.median(write)
     out = {
         "workload": w, "kernel": KERNELS[w], "launches": [len(fetch), len(write)],
         "fetch_size_kib": f_kib, "write_size_kib": w_kib,
