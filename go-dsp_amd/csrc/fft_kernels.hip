@@ -494,8 +494,8 @@ __global__ void power_partials_kernel(const cd *__restrict__ buf, int64_t nrows,
 //   B: q = k1 < R1, rows R2*k1 + j, DFT_R2, out rows k1 + R1*k2.
 // TWIDDLE: 0 none; 1 times W_R^(q*j) (FFT2 four-step, q = row group);
 // 2 times W_R^(col*j) (1-D four-step: the column is the n2 index).
-template <int LOG2L, bool CONJ_IN, int TWIDDLE, bool CONJ_SCALE_OUT>
-__global__ __launch_bounds__(256) void colfft_tile_kernel(
+template <int LOG2L, bool CONJ_IN, int TWIDDLE, bool CONJ_SCALE_OUT, int WGT = 256>
+__global__ __launch_bounds__(WGT) void colfft_tile_kernel(
     const cd *__restrict__ in, cd *__restrict__ out, int64_t C, int64_t in_step,
     int64_t in_stride, int64_t out_step, int64_t out_stride, const cd *__restrict__ twl,
     const cd *__restrict__ twr, int log2r, double scale, int64_t mat_stride) {
@@ -503,7 +503,7 @@ __global__ __launch_bounds__(256) void colfft_tile_kernel(
   static_assert(G::T <= 256, "tile column length too large");
   in += (int64_t)blockIdx.z * mat_stride;
   out += (int64_t)blockIdx.z * mat_stride;
-  constexpr int CW = 256 / G::T;
+  constexpr int CW = WGT / G::T;
   __shared__ double lds[G::NPASS > 1 ? CW * G::N : 1];
   const int lt = threadIdx.x;
   const int c = lt & (CW - 1);
@@ -889,16 +889,16 @@ hipError_t launch_power_partials(const cd *buf, int64_t nrows, int64_t flen, int
   return hipGetLastError();
 }
 
-template <int LOG2L>
-static hipError_t launch_colfft_t(bool conj_in, int twiddle, bool conj_scale_out, const cd *in,
+template <int LOG2L, int WGT>
+static hipError_t launch_colfft_w(bool conj_in, int twiddle, bool conj_scale_out, const cd *in,
                                   cd *out, int64_t C, int64_t ngroups, int64_t in_step,
                                   int64_t in_stride, int64_t out_step, int64_t out_stride,
                                   const cd *twl, const cd *twr, int log2r, double scale,
                                   int64_t batch, int64_t mat_stride, hipStream_t s) {
-  constexpr int CW = 256 / Geo<LOG2L>::T;
+  constexpr int CW = WGT / Geo<LOG2L>::T;
   const dim3 grid((unsigned)((C + CW - 1) / CW), (unsigned)ngroups, (unsigned)batch);
 #define GDSP_CF(A, B, D)                                                                      \
-  hipLaunchKernelGGL((colfft_tile_kernel<LOG2L, A, B, D>), grid, dim3(256), 0, s, in, out, C, \
+  hipLaunchKernelGGL((colfft_tile_kernel<LOG2L, A, B, D, WGT>), grid, dim3(WGT), 0, s, in, out, C, \
                      in_step, in_stride, out_step, out_stride, twl, twr, log2r, scale,         \
                      mat_stride)
   if (twiddle == 1) {
@@ -916,6 +916,27 @@ static hipError_t launch_colfft_t(bool conj_in, int twiddle, bool conj_scale_out
   }
 #undef GDSP_CF
   return hipGetLastError();
+}
+
+
+template <int LOG2L>
+static hipError_t launch_colfft_t(bool conj_in, int twiddle, bool conj_scale_out, const cd *in,
+                                  cd *out, int64_t C, int64_t ngroups, int64_t in_step,
+                                  int64_t in_stride, int64_t out_step, int64_t out_stride,
+                                  const cd *twl, const cd *twr, int log2r, double scale,
+                                  int64_t batch, int64_t mat_stride, hipStream_t s) {
+  // 512-column-thread tiles for 512-point columns: 16 columns = 256-B row
+  // segments instead of 128 (FFTN 512^3: 2.41-2.51 -> 2.28 ms); shorter
+  // columns keep 256 threads (their segments are already 512 B - 1 KiB, and
+  // 512 threads measured slower on the FFT2 8192^2 column tiles)
+  if constexpr (LOG2L >= 9) {
+    return launch_colfft_w<LOG2L, 512>(conj_in, twiddle, conj_scale_out, in, out, C, ngroups,
+                                       in_step, in_stride, out_step, out_stride, twl, twr, log2r,
+                                       scale, batch, mat_stride, s);
+  }
+  return launch_colfft_w<LOG2L, 256>(conj_in, twiddle, conj_scale_out, in, out, C, ngroups,
+                                     in_step, in_stride, out_step, out_stride, twl, twr, log2r,
+                                     scale, batch, mat_stride, s);
 }
 
 hipError_t launch_colfft(int log2l, bool conj_in, int twiddle, bool conj_scale_out, const cd *in,
