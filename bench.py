@@ -49,7 +49,8 @@ SEED = 0x5EED
 PROFILED_ALG_BYTES = {"radix4096": 32 * 4096 * 65536, "bluestein3000": 32 * 3000 * 65536,
                       "chirpz3000": 32 * 3000 * 65536, "fft2_8192": 4 * 16 * 8192 * 8192,
                       "fft2_dist": 4 * 16 * 8192 * 8192, "pwelch": 8 * (1 << 30),
-                      "fftn_512": 3 * 2 * 16 * 512 ** 3, "wav_decode": 10 * (1 << 30)}
+                      "fftn_512": 3 * 2 * 16 * 512 ** 3, "wav_decode": 10 * (1 << 30),
+                      "fft_2p20": 32 * (1 << 20)}
 
 
 def parse():
@@ -59,7 +60,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="radix4096",
                     choices=["radix4096", "bluestein3000", "chirpz3000", "fft2_8192", "fft2_dist",
-                             "pwelch", "fftn_512", "wav_decode"])
+                             "pwelch", "fftn_512", "wav_decode", "fft_2p20"])
     ap.add_argument("--batch", type=int, default=0, help="rows per GPU (0 = config default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU seconds for the cpu_baseline sample (0 disables)")
@@ -153,6 +154,22 @@ def main():
                "rows": R, "cols": C, "parallelism": f"rows{world}+alltoall"}
         kernel = "fft2_sharded (all launches and both all-to-alls)"
         metric = "Gsamples/s, fft.FFT2 8192x8192 complex128"
+    elif w == "fft_2p20":  # the reference's own BenchmarkFFT (fft/fft_test.go:262-280)
+        n = 1 << 20
+        x = torch.empty((1, n), dtype=torch.complex128, device=dev)
+        y = torch.empty_like(x)
+        D.fill_uniform(x, SEED, offset=rank * n * 2, stream=stream)
+
+        def step():
+            D.fft_batch(x, y, stream=stream)
+
+        samples_per_step = n
+        alg_bytes = 32 * n
+        cfg = {"workload": "fft.FFT of one N=2^20 complex128 vector (BenchmarkFFT, "
+                           "fft/fft_test.go:262-280), device-resident", "n": n, "batch": 1,
+               "parallelism": f"replicas{world}", "algorithm": "four-step (3 launches)"}
+        kernel = "four-step (colfft tile, row FFTs, transpose)"
+        metric = "Gsamples/s, fft.FFT N=2^20 (BenchmarkFFT)"
     elif w == "fftn_512":  # fft.FFTN of a 512^3 complex128 Matrix
         dims = (512, 512, 512)
         x = torch.empty(dims, dtype=torch.complex128, device=dev)
@@ -247,6 +264,14 @@ def main():
         ref = oracle.fft_rows(xs)
         err = max(float(np.linalg.norm(a - b) / np.linalg.norm(b)) for a, b in zip(ys, ref))
         check = {"rows": len(rows), "max_nrel_vs_oracle": err}
+    if rank == 0 and args.check_rows > 0 and w == "fft_2p20":
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import numpy as np
+        import oracle
+        ref = oracle.fft(x[0].cpu().numpy())
+        got = y[0].cpu().numpy()
+        check = {"rows": 1, "max_nrel_vs_oracle": float(np.linalg.norm(got - ref) /
+                                                         np.linalg.norm(ref))}
     if rank == 0 and args.check_rows > 0 and w == "wav_decode":
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import numpy as np
@@ -275,6 +300,21 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(w, args.cpu_seconds)
+    host_api = None
+    if rank == 0 and w == "fft_2p20":
+        # fft.FFT on a host vector, the way BenchmarkFFT calls it: H2D +
+        # transform + D2H through the C ABI's pinned staging (PCIe-inclusive;
+        # reported beside value, never as value)
+        xh = x[0].cpu().numpy()
+        gdsp.fft.FFT(xh)
+        reps = 20
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            gdsp.fft.FFT(xh)
+        dt = (time.perf_counter() - t0) / reps
+        host_api = {"ms_per_call": round(dt * 1e3, 4), "gsamples_s": round(xh.size / dt / 1e9, 4),
+                    "note": "gdsp.fft.FFT on a host numpy vector (C ABI host-pointer path, "
+                            "PCIe-inclusive)"}
 
     if rank == 0:
         line = {
@@ -300,6 +340,8 @@ def main():
             "cpu_baseline": cpu,
             "parity": check,
         }
+        if host_api is not None:
+            line["host_api"] = host_api
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -368,6 +410,19 @@ def cpu_baseline(workload: str, seconds: float):
                 "kind": "port",
                 "sample": f"{done} PCM16 samples ({dt:.1f} s) through the ReadFloats "
                           f"restatement (wav/wav.go:135-161), float32 out as the reference"}
+    if workload == "fft_2p20":
+        # BenchmarkFFT restated: one N=2^20 fft.FFT with the reference's worker
+        # pool (GOMAXPROCS = NumCPU, capped at the box's 16-core share)
+        x = oracle.fill_uniform(2 * (1 << 20), SEED).view(np.complex128).reshape(1, 1 << 20)
+        done = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            oracle.fft_rows_threaded(x, cores)
+            done += 1
+        dt = time.perf_counter() - t0
+        return {"value": round(done * (1 << 20) / dt / 1e9, 6), "unit": "Gsamples/s",
+                "cores": cores, "kind": "port",
+                "sample": f"{done} fft.FFT calls of N=2^20 ({dt:.1f} s), {pool}"}
     if workload == "fftn_512":
         # computeFFTN (fft.go:157-192): 3 x 512^2 line FFTs of 512; the
         # strided gather/scatter of axes 0 and 1 is not charged (favours the CPU)

@@ -19,7 +19,9 @@ KERNELS = {"radix4096": "fft_lds_kernel<12", "bluestein3000": "fft_mixed_fixed_k
            "fft2_8192": ["fft_lds_kernel<13", "colfft_tile_kernel<7", "colfft_tile_kernel<6"],
            # one FFTN step = the row pass + two column-tile axes
            "fftn_512": ["fft_lds_kernel<9", ("colfft_tile_kernel<9", 2)],
-           "wav_decode": "wav_decode_vec_kernel"}
+           "wav_decode": "wav_decode_vec_kernel",
+           # one 2^20 four-step: column tiles, row FFTs, transpose
+           "fft_2p20": ["colfft_tile_kernel<7", "fft_lds_kernel<13", "transpose_kernel"]}
 
 
 def values(w, counter, kernel):
