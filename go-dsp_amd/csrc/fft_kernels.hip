@@ -498,7 +498,7 @@ template <int LOG2L, bool CONJ_IN, int TWIDDLE, bool CONJ_SCALE_OUT, int WGT = 2
 __global__ __launch_bounds__(WGT) void colfft_tile_kernel(
     const cd *__restrict__ in, cd *__restrict__ out, int64_t C, int64_t in_step,
     int64_t in_stride, int64_t out_step, int64_t out_stride, const cd *__restrict__ twl,
-    const cd *__restrict__ twr, int log2r, double scale, int64_t mat_stride) {
+    const cd *__restrict__ twr, int log2r, double scale, int64_t mat_stride, int64_t twn) {
   using G = Geo<LOG2L>;
   static_assert(G::T <= 256, "tile column length too large");
   in += (int64_t)blockIdx.z * mat_stride;
@@ -525,12 +525,14 @@ __global__ __launch_bounds__(WGT) void colfft_tile_kernel(
     // W^(m*t) and the step W^(m*T) from the table, the rest by recurrence
     // (two table reads per thread instead of E scattered ones: for N = 2^20
     // the table is 16 MiB and the scattered reads missed L2)
+    // table index m*j mod N: a mask for power-of-2 N, else twn = N (the
+    // power-of-2-column mixed four-step)
     const int64_t mask = ((int64_t)1 << log2r) - 1;
     const int64_t m = TWIDDLE == 1 ? q : col;
     cd w = {1.0, 0.0}, wstep = {1.0, 0.0};
     if constexpr (TWIDDLE != 0) {
-      w = twr[(m * t) & mask];
-      wstep = twr[(m * G::T) & mask];
+      w = twr[twn ? (m * t) % twn : (m * t) & mask];
+      wstep = twr[twn ? (m * G::T) % twn : (m * G::T) & mask];
     }
 #pragma unroll
     for (int k = 0; k < G::E; ++k) {
@@ -894,13 +896,13 @@ static hipError_t launch_colfft_w(bool conj_in, int twiddle, bool conj_scale_out
                                   cd *out, int64_t C, int64_t ngroups, int64_t in_step,
                                   int64_t in_stride, int64_t out_step, int64_t out_stride,
                                   const cd *twl, const cd *twr, int log2r, double scale,
-                                  int64_t batch, int64_t mat_stride, hipStream_t s) {
+                                  int64_t batch, int64_t mat_stride, int64_t twn, hipStream_t s) {
   constexpr int CW = WGT / Geo<LOG2L>::T;
   const dim3 grid((unsigned)((C + CW - 1) / CW), (unsigned)ngroups, (unsigned)batch);
 #define GDSP_CF(A, B, D)                                                                      \
   hipLaunchKernelGGL((colfft_tile_kernel<LOG2L, A, B, D, WGT>), grid, dim3(WGT), 0, s, in, out, C, \
                      in_step, in_stride, out_step, out_stride, twl, twr, log2r, scale,         \
-                     mat_stride)
+                     mat_stride, twn)
   if (twiddle == 1) {
     if (conj_in) GDSP_CF(true, 1, false);
     else GDSP_CF(false, 1, false);
@@ -924,7 +926,7 @@ static hipError_t launch_colfft_t(bool conj_in, int twiddle, bool conj_scale_out
                                   cd *out, int64_t C, int64_t ngroups, int64_t in_step,
                                   int64_t in_stride, int64_t out_step, int64_t out_stride,
                                   const cd *twl, const cd *twr, int log2r, double scale,
-                                  int64_t batch, int64_t mat_stride, hipStream_t s) {
+                                  int64_t batch, int64_t mat_stride, int64_t twn, hipStream_t s) {
   // 512-column-thread tiles for 512-point columns: 16 columns = 256-B row
   // segments instead of 128 (FFTN 512^3: 2.41-2.51 -> 2.28 ms); shorter
   // columns keep 256 threads (their segments are already 512 B - 1 KiB, and
@@ -932,18 +934,18 @@ static hipError_t launch_colfft_t(bool conj_in, int twiddle, bool conj_scale_out
   if constexpr (LOG2L >= 9) {
     return launch_colfft_w<LOG2L, 512>(conj_in, twiddle, conj_scale_out, in, out, C, ngroups,
                                        in_step, in_stride, out_step, out_stride, twl, twr, log2r,
-                                       scale, batch, mat_stride, s);
+                                       scale, batch, mat_stride, twn, s);
   }
   return launch_colfft_w<LOG2L, 256>(conj_in, twiddle, conj_scale_out, in, out, C, ngroups,
                                      in_step, in_stride, out_step, out_stride, twl, twr, log2r,
-                                     scale, batch, mat_stride, s);
+                                     scale, batch, mat_stride, twn, s);
 }
 
 hipError_t launch_colfft(int log2l, bool conj_in, int twiddle, bool conj_scale_out, const cd *in,
                          cd *out, int64_t C, int64_t ngroups, int64_t in_step, int64_t in_stride,
                          int64_t out_step, int64_t out_stride, const cd *twl, const cd *twr,
                          int log2r, double scale, int64_t batch, int64_t mat_stride,
-                         hipStream_t s) {
+                         hipStream_t s, int64_t twn) {
   if (twiddle && conj_scale_out) return hipErrorInvalidValue;
   if (batch < 1 || batch > 65535) return hipErrorInvalidValue;
   switch (log2l) {
@@ -951,7 +953,7 @@ hipError_t launch_colfft(int log2l, bool conj_in, int twiddle, bool conj_scale_o
   case L:                                                                                     \
     return launch_colfft_t<L>(conj_in, twiddle, conj_scale_out, in, out, C, ngroups, in_step, \
                               in_stride, out_step, out_stride, twl, twr, log2r, scale, batch, \
-                              mat_stride, s);
+                              mat_stride, twn, s);
     GDSP_CFC(4) GDSP_CFC(5) GDSP_CFC(6) GDSP_CFC(7) GDSP_CFC(8) GDSP_CFC(9)
 #undef GDSP_CFC
     default: return hipErrorInvalidValue;

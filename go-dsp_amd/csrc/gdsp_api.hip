@@ -295,8 +295,11 @@ struct gdsp_plan {
   gdsp::MixedDesc md{};
   gdsp::MixedDesc md_gen{};  // generic radix list (runtime-radix kernels)
   cd *tw_gen = nullptr;
-  // mixed four-step (KIND_MIXED4): n = n1 * n2, one-kernel sub-plans, tw = T_n
+  // mixed four-step (KIND_MIXED4): n = n1 * n2, one-kernel sub-plans, tw = T_n;
+  // pow2col: n1 is a power of 2 in [16, 512], so the column DFT runs on
+  // row-segment tiles (3 HBM passes instead of 5)
   int64_t n1 = 0, n2 = 0;
+  bool pow2col = false;
   gdsp_plan *p1 = nullptr, *p2 = nullptr;
   // Bluestein (fft/bluestein.go): M = NextPowerOf2(2n-1), chirp = conj(w),
   // bhat = FFT_M(b)/M
@@ -451,6 +454,20 @@ bool mixed4_split(int64_t n, int64_t &n1, int64_t &n2) {
   return false;
 }
 
+// n = R * C with R a power of 2 in [16, 512] (column tiles) and C a
+// one-kernel length; the largest such R (shortest rows) wins.
+bool pow2col_split(int64_t n, int64_t &r, int64_t &c) {
+  for (int64_t R = (int64_t)1 << gdsp::kColMaxLog2; R >= ((int64_t)1 << gdsp::kColMinLog2);
+       R >>= 1) {
+    if (n % R == 0 && one_kernel_len(n / R)) {
+      r = R;
+      c = n / R;
+      return true;
+    }
+  }
+  return false;
+}
+
 int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   p->device = dev;
   p->n = n;
@@ -465,6 +482,16 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   }
   std::vector<int> rad;
   if (!chirpz && mixed_radices(n, rad)) return build_mixed(dev, n, rad, p);
+  if (!chirpz && next_pow2_ref(2 * n - 1) > ((int64_t)1 << gdsp::kMaxLdsLog2) &&
+      pow2col_split(n, p->n1, p->n2)) {
+    // n = 2^a * C with 2^a in [16, 512] and C a one-kernel length: the
+    // power-of-2 four-step structure (column tiles, rows of C, transpose)
+    p->kind = KIND_MIXED4;
+    p->pow2col = true;
+    STCHK(get_plan_locked(dev, p->n1, &p->p1));
+    STCHK(get_plan_locked(dev, p->n2, &p->p2));
+    return upload_twiddles(dev, n, &p->tw);
+  }
   if (!chirpz && next_pow2_ref(2 * n - 1) > ((int64_t)1 << gdsp::kMaxLdsLog2) &&
       mixed4_split(n, p->n1, p->n2)) {
     // smooth n beyond one kernel, where Bluestein would be the composed
@@ -638,6 +665,32 @@ int exec_fourstep(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bo
 int exec_mixed4(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
                 hipStream_t s) {
   const int64_t N = p->n, N1 = p->n1, N2 = p->n2;
+  if (p->pow2col) {
+    // as exec_fourstep with R = N1 (power of 2) and C = N2 (any one-kernel
+    // length): column DFT_R on row-segment tiles times W_N^(col*k1) (table
+    // index mod N), rows DFT_C, conj/scale-fused transpose R x C -> C x R
+    const int lr = ilog2(N1);
+    DevBuf work;
+    STCHK(work.alloc((size_t)batch * (size_t)N * sizeof(cd), s, SLOT_MX0));
+    cd *w = (cd *)work.p;
+    const cd *src = (const cd *)in;
+    if (load == gdsp::LOAD_REAL) {
+      HIPCHK(gdsp::launch_real_to_complex((const double *)in, w, batch * N, s));
+      src = w;
+    }
+    for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+      const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+      HIPCHK(gdsp::launch_colfft(lr, inv, 2, false, src + b0 * N, w + b0 * N, N2, 1, 0, 1, 0, 1,
+                                 p->p1->tw, p->tw, 0, 1.0, nb, N, s, N));
+    }
+    STCHK(exec_plan(p->p2, w, w, batch * N1, false, gdsp::LOAD_COMPLEX, s));
+    for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+      const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+      HIPCHK(gdsp::launch_transpose(w + b0 * N, out + b0 * N, N1, N2, s, nb, inv,
+                                    1.0 / (double)N));
+    }
+    return GDSP_OK;
+  }
   const size_t bytes = (size_t)batch * (size_t)N * sizeof(cd);
   DevBuf b1, b2;
   STCHK(b1.alloc(bytes, s, SLOT_MX0));

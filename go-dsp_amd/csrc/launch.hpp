@@ -68,12 +68,13 @@ hipError_t launch_power_partials(const cd *buf, int64_t nrows, int64_t flen, int
                                  double *partial, hipStream_t s);
 // FFT2 column pass on row-segment tiles; 4 <= log2l <= 9 (see fft_kernels.hip)
 constexpr int kColMinLog2 = 4, kColMaxLog2 = 9;
-// twiddle: 0 none, 1 W_R^(group*j), 2 W_R^(col*j)
+// twiddle: 0 none, 1 W_R^(group*j), 2 W_R^(col*j); table index mod 2^log2r, or mod
+// twn when twn > 0 (a non-power-of-2 N)
 hipError_t launch_colfft(int log2l, bool conj_in, int twiddle, bool conj_scale_out, const cd *in,
                          cd *out, int64_t C, int64_t ngroups, int64_t in_step, int64_t in_stride,
                          int64_t out_step, int64_t out_stride, const cd *twl, const cd *twr,
                          int log2r, double scale, int64_t batch, int64_t mat_stride,
-                         hipStream_t s);
+                         hipStream_t s, int64_t twn = 0);
 // batch <= 65535 matrices of rows x cols, consecutive; optional conj+scale
 // out, and twiddle tw[r*c] (source row r, column c; needs r*c < twn)
 hipError_t launch_transpose(const cd *in, cd *out, int64_t rows, int64_t cols, hipStream_t s,
