@@ -301,6 +301,65 @@ hipError_t launch_pwelch_mixed(const MixedDesc &d, const double *x, int64_t nfft
   return hipGetLastError();
 }
 
+// Column pass of the mixed four-step for n = L * C with a single-radix L
+// (every length dft_any has, <= 25): x as L rows x C columns, one thread per
+// column holds the whole column in registers (no LDS), so each wave-
+// instruction is a contiguous 1 KiB row segment. Column c: DFT_L over its L
+// rows, times W_n^(c*k) (c*k < n: a direct table read), written in place of
+// the rows. The rows DFT_C and the transpose follow (exec_mixed4).
+template <int L, bool CONJ_IN>
+__global__ __launch_bounds__(256) void colradix_kernel(const cd *__restrict__ in,
+                                                       cd *__restrict__ out, int64_t C, int64_t n,
+                                                       int64_t batch, const cd *__restrict__ tw) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t b = blockIdx.y;
+  if (c >= C || b >= batch) return;
+  const cd *src = in + b * n + c;
+  cd v[L];
+#pragma unroll
+  for (int r = 0; r < L; ++r) {
+    v[r] = ld_nt(src + r * C);
+    if constexpr (CONJ_IN) v[r].y = -v[r].y;
+  }
+  dft_any<L>(v);
+  cd *dst = out + b * n + c;
+  st_nt(dst, v[0]);
+#pragma unroll
+  for (int k = 1; k < L; ++k) st_nt(dst + k * C, cmul(v[k], tw[c * k]));
+}
+
+bool colradix_supported(int L) {
+  switch (L) {
+    case 2: case 3: case 4: case 5: case 6: case 7: case 8: case 9: case 10: case 11: case 12:
+    case 13: case 15: case 16: case 20: case 25:
+      return true;
+    default:
+      return false;
+  }
+}
+
+hipError_t launch_colradix(int L, bool conj_in, const cd *in, cd *out, int64_t C, int64_t n,
+                           int64_t batch, const cd *tw, hipStream_t s) {
+  if (batch < 1 || batch > 65535 || C < 1) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((C + 255) / 256), (unsigned)batch);
+  switch (L) {
+#define GDSP_CR(LL)                                                                          \
+  case LL:                                                                                   \
+    if (conj_in)                                                                             \
+      hipLaunchKernelGGL((colradix_kernel<LL, true>), grid, dim3(256), 0, s, in, out, C, n,  \
+                         batch, tw);                                                         \
+    else                                                                                     \
+      hipLaunchKernelGGL((colradix_kernel<LL, false>), grid, dim3(256), 0, s, in, out, C, n, \
+                         batch, tw);                                                         \
+    return hipGetLastError();
+    GDSP_CR(2) GDSP_CR(3) GDSP_CR(4) GDSP_CR(5) GDSP_CR(6) GDSP_CR(7) GDSP_CR(8) GDSP_CR(9)
+    GDSP_CR(10) GDSP_CR(11) GDSP_CR(12) GDSP_CR(13) GDSP_CR(15) GDSP_CR(16) GDSP_CR(20)
+    GDSP_CR(25)
+#undef GDSP_CR
+    default: return hipErrorInvalidValue;
+  }
+}
+
 // Radix list of the compiled specialisation for n, if there is one
 // (launch_fft_mixed picks the kernel by n and list). GDSP_MIXED_GENERIC=1
 // disables them. n = 3000: 1.10 ms per 65536 transforms for 25*15*8 against

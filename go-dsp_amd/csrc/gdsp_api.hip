@@ -297,9 +297,10 @@ struct gdsp_plan {
   cd *tw_gen = nullptr;
   // mixed four-step (KIND_MIXED4): n = n1 * n2, one-kernel sub-plans, tw = T_n;
   // pow2col: n1 is a power of 2 in [16, 512], so the column DFT runs on
-  // row-segment tiles (3 HBM passes instead of 5)
+  // row-segment tiles; radixcol: n1 <= 25 is one radix, a column per thread
+  // (either way 3 HBM passes instead of 5)
   int64_t n1 = 0, n2 = 0;
-  bool pow2col = false;
+  bool pow2col = false, radixcol = false;
   gdsp_plan *p1 = nullptr, *p2 = nullptr;
   // Bluestein (fft/bluestein.go): M = NextPowerOf2(2n-1), chirp = conj(w),
   // bhat = FFT_M(b)/M
@@ -468,6 +469,19 @@ bool pow2col_split(int64_t n, int64_t &r, int64_t &c) {
   return false;
 }
 
+// n = L * C with L a single radix (<= 25, largest first) and C a one-kernel
+// length.
+bool radixcol_split(int64_t n, int64_t &l, int64_t &c) {
+  for (int L : {25, 20, 16, 15, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2}) {
+    if (gdsp::colradix_supported(L) && n % L == 0 && one_kernel_len(n / L)) {
+      l = L;
+      c = n / L;
+      return true;
+    }
+  }
+  return false;
+}
+
 int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   p->device = dev;
   p->n = n;
@@ -489,6 +503,13 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
     p->kind = KIND_MIXED4;
     p->pow2col = true;
     STCHK(get_plan_locked(dev, p->n1, &p->p1));
+    STCHK(get_plan_locked(dev, p->n2, &p->p2));
+    return upload_twiddles(dev, n, &p->tw);
+  }
+  if (!chirpz && next_pow2_ref(2 * n - 1) > ((int64_t)1 << gdsp::kMaxLdsLog2) &&
+      radixcol_split(n, p->n1, p->n2)) {
+    p->kind = KIND_MIXED4;
+    p->radixcol = true;
     STCHK(get_plan_locked(dev, p->n2, &p->p2));
     return upload_twiddles(dev, n, &p->tw);
   }
@@ -665,11 +686,11 @@ int exec_fourstep(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bo
 int exec_mixed4(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
                 hipStream_t s) {
   const int64_t N = p->n, N1 = p->n1, N2 = p->n2;
-  if (p->pow2col) {
+  if (p->pow2col || p->radixcol) {
     // as exec_fourstep with R = N1 (power of 2) and C = N2 (any one-kernel
     // length): column DFT_R on row-segment tiles times W_N^(col*k1) (table
     // index mod N), rows DFT_C, conj/scale-fused transpose R x C -> C x R
-    const int lr = ilog2(N1);
+    const int lr = p->pow2col ? ilog2(N1) : 0;
     DevBuf work;
     STCHK(work.alloc((size_t)batch * (size_t)N * sizeof(cd), s, SLOT_MX0));
     cd *w = (cd *)work.p;
@@ -680,8 +701,11 @@ int exec_mixed4(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool
     }
     for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
       const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
-      HIPCHK(gdsp::launch_colfft(lr, inv, 2, false, src + b0 * N, w + b0 * N, N2, 1, 0, 1, 0, 1,
-                                 p->p1->tw, p->tw, 0, 1.0, nb, N, s, N));
+      if (p->radixcol)
+        HIPCHK(gdsp::launch_colradix((int)N1, inv, src + b0 * N, w + b0 * N, N2, N, nb, p->tw, s));
+      else
+        HIPCHK(gdsp::launch_colfft(lr, inv, 2, false, src + b0 * N, w + b0 * N, N2, 1, 0, 1, 0, 1,
+                                   p->p1->tw, p->tw, 0, 1.0, nb, N, s, N));
     }
     STCHK(exec_plan(p->p2, w, w, batch * N1, false, gdsp::LOAD_COMPLEX, s));
     for (int64_t b0 = 0; b0 < batch; b0 += 65535) {

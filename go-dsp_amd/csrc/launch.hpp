@@ -66,6 +66,12 @@ hipError_t launch_segments_to_complex(const double *x, int64_t nfft, int64_t fle
                                       const double *win, cd *buf, hipStream_t s);
 hipError_t launch_power_partials(const cd *buf, int64_t nrows, int64_t flen, int64_t rpp,
                                  double *partial, hipStream_t s);
+// Column pass of the mixed four-step for a single-radix column length L
+// (fft_mixed.hip): DFT_L down each of the C columns of batch L x C matrices
+// (matrix stride n = L*C), times W_n^(col*k), in place allowed
+bool colradix_supported(int L);
+hipError_t launch_colradix(int L, bool conj_in, const cd *in, cd *out, int64_t C, int64_t n,
+                           int64_t batch, const cd *tw, hipStream_t s);
 // FFT2 column pass on row-segment tiles; 4 <= log2l <= 9 (see fft_kernels.hip)
 constexpr int kColMinLog2 = 4, kColMaxLog2 = 9;
 // twiddle: 0 none, 1 W_R^(group*j), 2 W_R^(col*j); table index mod 2^log2r, or mod

@@ -287,7 +287,8 @@ def test_plan_kinds(gdsp):
     assert D.plan(1 << 16).kind == 2
     assert D.plan(3000).kind == 5  # 2^3 3 5^3: mixed radix
     assert D.plan(4097).kind == 3  # 17 * 241: fused Bluestein
-    assert D.plan(10000).kind == 6  # 100 x 100: mixed four-step
+    assert D.plan(10000).kind == 6  # 16 x 625: mixed four-step (power-of-2 columns)
+    assert D.plan(44100).kind == 6  # 25 x 1764: mixed four-step (single-radix columns)
     assert D.plan(5000).kind == 5  # a compiled specialisation above 4096 (25*25*8)
     assert D.plan(5400).kind == 3  # smooth, no specialisation, M = 16384: fused chirp-z
     assert D.plan(8209).kind == 4  # prime, M = 32768: composed Bluestein
@@ -343,7 +344,10 @@ def test_chirpz_plan_vs_oracle(gdsp, oracle, n):
 # smooth lengths beyond one kernel: four-step over one-kernel factors
 # (audio rates 44100 = 210^2, 48000; 2^16 * 3; 10^6) and neighbours that are
 # not smooth (8209 prime, 4100 = 4 * 25 * 41) and stay Bluestein
-MIXED4 = [4100, 5000, 6000, 8190, 10000, 44100, 48000, 3 << 16, 8209, 100000, 1000000]
+MIXED4 = [4100, 5000, 6000, 8190, 10000, 44100, 48000, 3 << 16, 8209, 100000, 1000000,
+          # single-radix columns (25 x 3528, 25 x 882, 9 x 2187) and power-of-2
+          # columns (16 x 1875): three passes
+          88200, 22050, 19683, 30000]
 
 
 @pytest.mark.parametrize("n", MIXED4)
