@@ -19,4 +19,7 @@ GDSP_SPEC_GROUP(specs1,
                 Spec<25, 16>,  // 400
                 Spec<25, 20>,  // 500
                 Spec<25, 6, 4>,  // 600
-                Spec<16, 10, 4>)  // 640
+                Spec<16, 10, 4>,  // 640
+                Spec<25, 15>,  // 375 (four-step rows)
+                Spec<25, 25>,  // 625 (four-step rows)
+                Spec<7, 3, 6, 7>)  // 882 (four-step rows)

@@ -18,4 +18,9 @@ GDSP_SPEC_GROUP(specs2,
                 Spec<20, 5, 16>,  // 1600
                 Spec<15, 15, 8>,  // 1800
                 Spec<15, 9, 16>,  // 2160
-                Spec<25, 10, 10>)  // 2500
+                Spec<25, 10, 10>,  // 2500
+                Spec<25, 5, 9>,  // 1125 (four-step rows)
+                Spec<9, 7, 7, 4>,  // 1764 (four-step rows)
+                Spec<25, 3, 25>,  // 1875 (four-step rows)
+                Spec<9, 3, 9, 9>,  // 2187
+                Spec<25, 6, 15>)  // 2250 (four-step rows)

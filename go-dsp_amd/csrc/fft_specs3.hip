@@ -19,4 +19,8 @@ GDSP_SPEC_GROUP(specs3,
                 Spec<25, 12, 20>,  // 6000
                 Spec<25, 16, 16>,  // 6400
                 Spec<25, 15, 20>,  // 7500
-                Spec<25, 20, 16>)  // 8000
+                Spec<25, 20, 16>,  // 8000
+                Spec<25, 5, 25>,  // 3125 (four-step rows)
+                Spec<12, 6, 7, 7>,  // 3528 (four-step rows)
+                Spec<25, 6, 25>,  // 3750 (four-step rows)
+                Spec<25, 5, 25, 2>)  // 6250 (four-step rows)
