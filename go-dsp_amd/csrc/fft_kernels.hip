@@ -283,7 +283,7 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_kernel(
     fft_regs<LOG2F, SPLIT, true, LOG2E>(v, tt, tw, lre, lim, it == 0);
     if (active) {
 #pragma unroll
-      for (int k = 0; k < G::E; ++k) acc[k] += v[k].x * v[k].x + v[k].y * v[k].y;
+      for (int k = 0; k < G::E; ++k) acc[k] = fma(v[k].y, v[k].y, fma(v[k].x, v[k].x, acc[k]));
     }
   }
   if (worker * pairs_per_worker < npairs) {
@@ -408,7 +408,7 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_ker
       fft_regs<LOG2F, SPLIT, 1, LOG2E>(v, opaque_int(t), tw, lre, lim, it == 0);
     if (active) {
 #pragma unroll
-      for (int k = 0; k < E; ++k) acc[k] += v[k].x * v[k].x + v[k].y * v[k].y;
+      for (int k = 0; k < E; ++k) acc[k] = fma(v[k].y, v[k].y, fma(v[k].x, v[k].x, acc[k]));
     }
   }
   if (p0 < npairs) {

@@ -355,7 +355,7 @@ __global__ __launch_bounds__((FixedGeo<R0, RS...>::WG)) void pwelch_fixed_kernel
         if (L::Pass::act(j, true)) {
 #pragma unroll
           for (int r = 0; r < L::R; ++r)
-            acc[jj][r] += c.v[jj][r].x * c.v[jj][r].x + c.v[jj][r].y * c.v[jj][r].y;
+            acc[jj][r] = fma(c.v[jj][r].y, c.v[jj][r].y, fma(c.v[jj][r].x, c.v[jj][r].x, acc[jj][r]));
         }
       }
     };
