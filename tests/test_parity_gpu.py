@@ -467,3 +467,45 @@ def test_concurrent_host_calls(gdsp, oracle):
         t.join()
     assert not fails, fails
     assert max(errs.values()) < TOL, errs
+
+
+def test_random_lengths_every_plan_kind(gdsp, oracle):
+    # 40 seeded random lengths in [2, 40000]: powers of 2, compiled and
+    # runtime-radix mixed lengths, both four-step column forms, the general
+    # five-pass form and fused / composed Bluestein, forward, inverse and real
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    rng = np.random.default_rng(20261016)
+    lengths = sorted(set(int(v) for v in rng.integers(2, 40001, 40)))
+    kinds = set()
+    for n in lengths:
+        batch = 2
+        x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
+        assert row_nrel(gdsp.fft.FFTBatch(x), oracle.fft_rows(x)) < TOL, n
+        assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL, n
+        assert row_nrel(gdsp.fft.FFTRealBatch(x.real.copy()),
+                        oracle.fft_rows(x.real.astype(np.complex128))) < TOL, n
+        kinds.add(D.plan(n).kind)
+    assert {3, 4} <= kinds, kinds  # random lengths are mostly Bluestein's
+
+
+def test_random_smooth_lengths(gdsp, oracle):
+    # seeded random 13-smooth lengths up to 200000: one-kernel mixed radix
+    # (compiled or runtime radices), the power-of-2-column and single-radix-
+    # column four-steps and the general five-pass form
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    rng = np.random.default_rng(7)
+    lengths = set()
+    while len(lengths) < 40:
+        n = 1
+        for p, emax in ((2, 10), (3, 6), (5, 5), (7, 3), (11, 1), (13, 1)):
+            n *= p ** int(rng.integers(0, emax + 1))
+        if 2 <= n <= 200000 and n & (n - 1):
+            lengths.add(n)
+    kinds = set()
+    for n in sorted(lengths):
+        batch = 2
+        x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
+        assert row_nrel(gdsp.fft.FFTBatch(x), oracle.fft_rows(x)) < TOL, n
+        assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL, n
+        kinds.add(D.plan(n).kind)
+    assert {5, 6} <= kinds, kinds
