@@ -16,4 +16,7 @@ GDSP_SPEC_GROUP(specs0,
                 Spec<15, 16, 8>,  // 1920
                 Spec<15, 8, 4>,  // 480
                 Spec<12, 16, 8>,  // 1536
-                Spec<12, 16, 16>)  // 3072
+                Spec<12, 16, 16>,  // 3072
+                Spec<9, 7, 7>,  // 441 (44.1 kHz audio frames)
+                Spec<15, 7, 7>,  // 735 (44.1 kHz audio frames)
+                Spec<9, 3, 7, 7>)  // 1323 (44.1 kHz audio frames)

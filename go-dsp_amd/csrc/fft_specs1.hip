@@ -22,4 +22,6 @@ GDSP_SPEC_GROUP(specs1,
                 Spec<16, 10, 4>,  // 640
                 Spec<25, 15>,  // 375 (four-step rows)
                 Spec<25, 25>,  // 625 (four-step rows)
-                Spec<7, 3, 6, 7>)  // 882 (four-step rows)
+                Spec<7, 3, 6, 7>,  // 882 (four-step rows)
+                Spec<7, 5, 6, 7>,  // 1470 (44.1 kHz audio frames)
+                Spec<9, 5, 7, 7>)  // 2205 (44.1 kHz audio frames)

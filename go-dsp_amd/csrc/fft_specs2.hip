@@ -23,4 +23,6 @@ GDSP_SPEC_GROUP(specs2,
                 Spec<9, 7, 7, 4>,  // 1764 (four-step rows)
                 Spec<25, 3, 25>,  // 1875 (four-step rows)
                 Spec<9, 3, 9, 9>,  // 2187
-                Spec<25, 6, 15>)  // 2250 (four-step rows)
+                Spec<25, 6, 15>,  // 2250 (four-step rows)
+                Spec<9, 6, 7, 7>,  // 2646 (44.1 kHz audio frames)
+                Spec<12, 5, 7, 7>)  // 2940 (44.1 kHz audio frames)

@@ -23,4 +23,6 @@ GDSP_SPEC_GROUP(specs3,
                 Spec<25, 5, 25>,  // 3125 (four-step rows)
                 Spec<12, 6, 7, 7>,  // 3528 (four-step rows)
                 Spec<25, 6, 25>,  // 3750 (four-step rows)
-                Spec<25, 5, 25, 2>)  // 6250 (four-step rows)
+                Spec<25, 5, 25, 2>,  // 6250 (four-step rows)
+                Spec<15, 6, 7, 7>,  // 4410 (44.1 kHz audio frames)
+                Spec<20, 6, 7, 7>)  // 5880 (44.1 kHz audio frames)

@@ -309,7 +309,9 @@ MIXED = [3, 5, 6, 7, 10, 11, 12, 13, 14, 18, 20, 21, 22, 24, 25, 26, 27, 39, 48,
          120, 160, 500, 600, 640, 750, 768, 800, 900, 1152, 1600, 2160, 2880, 4500, 5000,
          5120, 6000, 6400, 7500, 8000,
          # four-step row lengths (two to four passes, radix 7 included)
-         375, 882, 1125, 1764, 1875, 2250, 3528, 3750, 6250]
+         375, 882, 1125, 1764, 1875, 2250, 3528, 3750, 6250,
+         # 44.1 kHz audio frame lengths (radix 7 twice)
+         441, 735, 1323, 1470, 2205, 2646, 2940, 4410, 5880]
 
 
 @pytest.mark.parametrize("n", MIXED)
