@@ -176,12 +176,20 @@ void host_copy(void *dst, const void *src, size_t n) {
   }
   const size_t part = (n / k + 63) & ~(size_t)63;
   std::thread th[3];
+  size_t rest = n;  // this thread also copies [rest, n) if a thread could not start
   unsigned used = 0;
-  for (unsigned i = 1; i < k && i * part < n; ++i, ++used) {
+  for (unsigned i = 1; i < k && i * part < n; ++i) {
     const size_t off = i * part, c = std::min(part, n - off);
-    th[i - 1] = std::thread([=] { memcpy((char *)dst + off, (const char *)src + off, c); });
+    try {
+      th[used] = std::thread([=] { memcpy((char *)dst + off, (const char *)src + off, c); });
+      ++used;
+    } catch (...) {  // nothing may throw past the C ABI
+      rest = off;
+      break;
+    }
   }
   memcpy(dst, src, std::min(part, n));
+  if (rest < n) memcpy((char *)dst + rest, (const char *)src + rest, n - rest);
   for (unsigned i = 0; i < used; ++i) th[i].join();
 }
 
