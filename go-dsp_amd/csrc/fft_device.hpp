@@ -10,8 +10,16 @@
 // W_{Ns*R}^{(j%Ns)*r}. Each thread owns E (<=16) elements at t + k*T, so the
 // first load and the last store are fully coalesced 16-byte-per-lane streams.
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#else  // hipRTC (mixed_jit.cpp): no system headers; its runtime header has the types
+using __hip_internal::int16_t;
+using __hip_internal::int64_t;
+using __hip_internal::uint16_t;
+using __hip_internal::uint32_t;
+using __hip_internal::uint64_t;
+#endif
 
 namespace gdsp {
 

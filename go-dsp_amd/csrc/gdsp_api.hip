@@ -303,6 +303,7 @@ struct gdsp_plan {
   gdsp::MixedDesc md{};
   gdsp::MixedDesc md_gen{};  // generic radix list (runtime-radix kernels)
   cd *tw_gen = nullptr;
+  gdsp::JitSpec *jit = nullptr;  // runtime-compiled specialisation of md (mixed_jit.hip)
   // mixed four-step (KIND_MIXED4): n = n1 * n2, one-kernel sub-plans, tw = T_n;
   // pow2col: n1 is a power of 2 in [16, 512], so the column DFT runs on
   // row-segment tiles; radixcol: n1 <= 25 is one radix, a column per thread
@@ -447,7 +448,9 @@ bool one_kernel_len(int64_t m) {
   if (m < 2) return false;
   if (is_pow2(m)) return ilog2(m) <= gdsp::kMaxLdsLog2;
   std::vector<int> rad;
-  return mixed_radices(m, rad);
+  if (mixed_radices(m, rad)) return true;
+  int jr[4], jnp = 0;  // a runtime-compiled specialisation (else the sub-plan takes Bluestein)
+  return gdsp::jit_enabled() && gdsp::jit_radices((int)m, jr, &jnp);
 }
 
 // n = n1 * n2 with both factors one-kernel lengths, n1 <= n2 as balanced as
@@ -503,6 +506,19 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
     return upload_twiddles(dev, n, &p->tw);
   }
   std::vector<int> rad;
+  int fr[16], fnp = 0;
+  if (!chirpz && n <= gdsp::kMixedSpecMax && !gdsp::mixed_fixed_radices((int)n, fr, &fnp) &&
+      gdsp::jit_enabled()) {
+    // smooth length without a compiled specialisation: compile one (hipRTC);
+    // if that fails it takes the runtime-radix kernel or Bluestein below
+    int jr[4], jnp = 0;
+    if (gdsp::jit_radices((int)n, jr, &jnp)) {
+      if (gdsp::JitSpec *j = gdsp::jit_spec_build(dev, jr, jnp, (int)n)) {
+        p->jit = j;
+        return build_mixed(dev, n, std::vector<int>(jr, jr + jnp), p);
+      }
+    }
+  }
   if (!chirpz && mixed_radices(n, rad)) return build_mixed(dev, n, rad, p);
   if (!chirpz && next_pow2_ref(2 * n - 1) > ((int64_t)1 << gdsp::kMaxLdsLog2) &&
       pow2col_split(n, p->n1, p->n2)) {
@@ -787,7 +803,10 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
       return GDSP_OK;
     }
     case KIND_MIXED:
-      HIPCHK(gdsp::launch_fft_mixed(p->md, inv, load, in, out, batch, p->tw, scale, s));
+      if (p->jit)
+        HIPCHK(gdsp::jit_launch_fft(p->jit, inv, load, in, out, batch, p->tw, scale, s));
+      else
+        HIPCHK(gdsp::launch_fft_mixed(p->md, inv, load, in, out, batch, p->tw, scale, s));
       return GDSP_OK;
     case KIND_MIXED4:
       return exec_mixed4(p, in, out, batch, inv, load, s);
@@ -1244,11 +1263,12 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
                                         (double *)red.p, s));
     return GDSP_OK;
   }
-  if (p->kind == KIND_MIXED && gdsp::pwelch_fixed_workers_per_block(p->md) > 0 &&
+  if (p->kind == KIND_MIXED && (p->jit || gdsp::pwelch_fixed_workers_per_block(p->md) > 0) &&
       !getenv("GDSP_PW_GENERIC")) {
     // fused path on a compiled specialisation (e.g. NFFT 1000, 3000)
     const int64_t npairs = (nseg + 1) / 2;
-    int64_t target = 2048 * (int64_t)gdsp::pwelch_fixed_workers_per_block(p->md);
+    const int wpb = p->jit ? gdsp::jit_pw_tpw(p->jit) : gdsp::pwelch_fixed_workers_per_block(p->md);
+    int64_t target = 2048 * (int64_t)wpb;
     if (target > npairs) target = npairs;
     const int64_t ppw = (npairs + target - 1) / target;
     const int64_t nworkers = (npairs + ppw - 1) / ppw;
@@ -1256,8 +1276,12 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
     STCHK(part.alloc((size_t)nworkers * (size_t)flen * sizeof(double), s, SLOT_PW_PART));
     STCHK(red.alloc((size_t)gdsp::reduce_scratch_doubles(nworkers, flen) * sizeof(double), s,
                     SLOT_PW_RED));
-    HIPCHK(gdsp::launch_pwelch_fixed(p->md, d_x, nfft, stride, seg_begin, seg_end, ppw, nworkers,
+    if (p->jit)
+      HIPCHK(gdsp::jit_launch_pwelch(p->jit, d_x, nfft, stride, seg_begin, seg_end, ppw, nworkers,
                                      d_win_seg, p->tw, (double *)part.p, s));
+    else
+      HIPCHK(gdsp::launch_pwelch_fixed(p->md, d_x, nfft, stride, seg_begin, seg_end, ppw,
+                                       nworkers, d_win_seg, p->tw, (double *)part.p, s));
     HIPCHK(gdsp::launch_reduce_partials((const double *)part.p, nworkers, flen, d_acc,
                                         (double *)red.p, s));
     return GDSP_OK;

@@ -1,8 +1,10 @@
 // launch.hpp — host launchers of the gfx950 kernels (fft_kernels.hip), used by
 // the C ABI layer (gdsp_api.hip). Internal to libgdspfft.
 #pragma once
+#ifndef __HIPCC_RTC__  // the device-side parts are also compiled by hipRTC (mixed_jit.cpp)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 namespace gdsp {
 
@@ -14,8 +16,6 @@ enum { LOAD_COMPLEX = 0, LOAD_REAL = 1 };
 // fused Bluestein kernel (M) / the fused Pwelch kernel
 constexpr int kMaxLdsLog2 = 14;
 
-hipError_t launch_fft_lds(int log2n, bool inv, int load, bool split, const void *in, cd *out,
-                          int64_t batch, const cd *tw, double scale, hipStream_t s);
 // Mixed-radix one-kernel transform (fft_mixed.hip): n = prod of the radices
 // in `codes` (5 bits per pass, radices 2,3,4,5,7,8,11,13,16 in the runtime-radix
 // kernels, also 6,9,10,12,15,20,25 in the compiled specialisations), n <= kMixedMax
@@ -27,6 +27,11 @@ struct MixedDesc {
 constexpr int kMixedMax = 4096;
 // compiled specialisations (fft_specs*.hip) reach this far (re/im exchange)
 constexpr int kMixedSpecMax = 8192;
+
+#ifndef __HIPCC_RTC__
+
+hipError_t launch_fft_lds(int log2n, bool inv, int load, bool split, const void *in, cd *out,
+                          int64_t batch, const cd *tw, double scale, hipStream_t s);
 // fused Pwelch over a mixed-radix segment length d.n = max(pad, nfft) with
 // d.npass >= 2 (fft_mixed.hip); same partial layout as launch_pwelch
 hipError_t launch_pwelch_mixed(const MixedDesc &d, const double *x, int64_t nfft, int64_t stride,
@@ -38,6 +43,18 @@ int pwelch_fixed_workers_per_block(const MixedDesc &d);
 hipError_t launch_pwelch_fixed(const MixedDesc &d, const double *x, int64_t nfft, int64_t stride,
                                int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,
                                const double *win, const cd *tw, double *partial, hipStream_t s);
+// runtime-compiled specialisations (mixed_jit.hip, hipRTC): a radix list for
+// a smooth n <= kMixedSpecMax without a compiled one, and its kernels
+struct JitSpec;
+bool jit_enabled();
+bool jit_radices(int n, int *rad, int *npass);
+JitSpec *jit_spec_build(int dev, const int *rad, int np, int n);  // nullptr: not built
+hipError_t jit_launch_fft(const JitSpec *j, bool inv, int load, const void *in, cd *out,
+                          int64_t batch, const cd *tw, double scale, hipStream_t s);
+int jit_pw_tpw(const JitSpec *j);
+hipError_t jit_launch_pwelch(const JitSpec *j, const double *x, int64_t nfft, int64_t stride,
+                             int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,
+                             const double *win, const cd *tw, double *partial, hipStream_t s);
 // radix list of a compiled specialisation for n (false: use the generic list)
 bool mixed_fixed_radices(int n, int *rad, int *npass);
 hipError_t launch_fft_mixed(const MixedDesc &d, bool inv, int load, const void *in, cd *out,
@@ -99,5 +116,7 @@ hipError_t launch_wav_decode(const void *in, int64_t count, int audio_format, in
                              void *out, bool f64, hipStream_t s);
 hipError_t launch_fill_uniform(double *out, int64_t count, uint64_t seed, uint64_t offset,
                                hipStream_t s);
+
+#endif  // __HIPCC_RTC__
 
 }  // namespace gdsp

@@ -3,9 +3,11 @@
 // fused Pwelch kernel on it, and GDSP_SPEC_GROUP, which instantiates a list
 // of radix lists in one translation unit (fft_specs*.hip).
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <stdlib.h>
 
 #include <tuple>
+#endif
 
 #include "mixed_core.hpp"
 
@@ -152,7 +154,8 @@ struct FixedGeo {
   static constexpr int N = R0 * (RS * ... * 1);
   static constexpr int need() {
     int m = 1;
-    for (int r : {R0, RS...}) {
+    constexpr int rl[] = {R0, RS...};  // (no std::initializer_list under hipRTC)
+    for (int r : rl) {
       const int nb = N / r, jm = r > 16 ? 1 : 16 / r, q = (nb + jm - 1) / jm;
       m = q > m ? q : m;
     }
@@ -194,6 +197,7 @@ __global__ __launch_bounds__((FixedGeo<R0, RS...>::WG)) void fft_mixed_fixed_ker
         p0, tl, valid, out + row * G::N, ld, tw, scale);
 }
 
+#ifndef __HIPCC_RTC__  // host-side launch helpers
 template <bool SPLIT, int... RS>
 static bool launch_fixed(const MixedDesc &d, bool inv, int load, const void *in, cd *out,
                          int64_t batch, const cd *tw, double scale, hipStream_t s) {
@@ -247,6 +251,8 @@ static bool launch_spec(std::tuple<S...>, const MixedDesc &d, bool inv, int load
   return (spec_launch(S{}, d, inv, load, in, out, batch, tw, scale, s) || ...);
 }
 
+#endif  // __HIPCC_RTC__
+
 // ---------------------------------------------------------------------------
 // Fused Welch accumulation on a compiled specialisation (spectral/pwelch.go:
 // 104-122 for smooth NFFT / Pad = a specialised length): the same packed
@@ -287,7 +293,7 @@ __device__ __forceinline__ void fixed_chain_to(const Prev &prev, int tl, bool va
 
 template <int R0, int... RS>
 struct FixedLast {
-  static constexpr int rr[] = {R0, RS...};
+  static constexpr int rr[sizeof...(RS) + 1] = {R0, RS...};
   static constexpr int R = rr[sizeof...(RS)];
   static constexpr int N = FixedGeo<R0, RS...>::N;
   using Pass = FPass<R, N, N / R, FixedGeo<R0, RS...>::T1>;
@@ -377,6 +383,7 @@ __global__ __launch_bounds__((FixedGeo<R0, RS...>::WG)) void pwelch_fixed_kernel
   }
 }
 
+#ifndef __HIPCC_RTC__
 template <int... RS>
 static int spec_pw_tpw(Spec<RS...>, const MixedDesc &d) {
   uint64_t codes = 0;
@@ -413,9 +420,11 @@ static bool launch_pw_spec(std::tuple<S...>, const MixedDesc &d, const double *x
                          partial, s) ||
           ...);
 }
+#endif  // __HIPCC_RTC__
 
 }  // namespace gdsp
 
+#ifndef __HIPCC_RTC__
 // One translation unit per group of specialisations (fft_specs*.hip), so the
 // groups compile in parallel; fft_mixed.hip asks each group in turn.
 #define GDSP_SPEC_GROUP(NAME, ...)                                                            \
@@ -436,3 +445,4 @@ static bool launch_pw_spec(std::tuple<S...>, const MixedDesc &d, const double *x
                           nworkers, win, tw, partial, s);                                     \
   }                                                                                           \
   }
+#endif  // __HIPCC_RTC__

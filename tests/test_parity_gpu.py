@@ -290,7 +290,7 @@ def test_plan_kinds(gdsp):
     assert D.plan(10000).kind == 6  # 16 x 625: mixed four-step (power-of-2 columns)
     assert D.plan(44100).kind == 6  # 25 x 1764: mixed four-step (single-radix columns)
     assert D.plan(5000).kind == 5  # a compiled specialisation above 4096 (25*25*8)
-    assert D.plan(5400).kind == 3  # smooth, no specialisation, M = 16384: fused chirp-z
+    assert D.plan(5400).kind == 5  # smooth, no compiled specialisation: hipRTC-compiled one
     assert D.plan(8209).kind == 4  # prime, M = 32768: composed Bluestein
     assert D.plan(3000, chirpz=True).kind == 3
     assert D.plan(10000, chirpz=True).kind == 4
@@ -511,3 +511,30 @@ def test_random_smooth_lengths(gdsp, oracle):
         assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL, n
         kinds.add(D.plan(n).kind)
     assert {5, 6} <= kinds, kinds
+
+
+@pytest.mark.parametrize("n,kind", [(810, 5), (1001, 5), (4095, 5), (4320, 5), (5400, 5),
+                                    (6144, 5), (7000, 5), (7680, 5), (8190, 3)])
+def test_jit_specialisations(gdsp, oracle, n, kind):
+    # smooth lengths without a compiled specialisation get one compiled at
+    # plan creation (mixed_jit.hip, hipRTC); above 4096 they would otherwise
+    # be Bluestein. 8190 = 13 * 630 needs 630 threads per transform in its
+    # radix-13 pass (> 512), so it stays Bluestein.
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    assert D.plan(n).kind == kind, n
+    rng = np.random.default_rng(4000 + n)
+    x = rng.uniform(-1, 1, (3, n)) + 1j * rng.uniform(-1, 1, (3, n))
+    assert row_nrel(gdsp.fft.FFTBatch(x), oracle.fft_rows(x)) < TOL
+    assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL
+    assert row_nrel(gdsp.fft.FFTRealBatch(x.real.copy()),
+                    oracle.fft_rows(x.real.astype(np.complex128))) < TOL
+
+
+@pytest.mark.parametrize("nfft,nov", [(810, 405), (5400, 2700)])
+def test_jit_pwelch(gdsp, oracle, nfft, nov):
+    rng = np.random.default_rng(nfft)
+    x = rng.standard_normal(40 * nfft)
+    o = gdsp.spectral.PwelchOptions(NFFT=nfft, Noverlap=nov)
+    p, f = gdsp.spectral.Pwelch(x, 3.0, o)
+    pr, fr = oracle.pwelch(x, 3.0, nfft=nfft, noverlap=nov)
+    assert nrel(p, pr) < TOL and nrel(f, fr) == 0.0
