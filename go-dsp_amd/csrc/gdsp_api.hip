@@ -403,7 +403,9 @@ int make_mixed_desc(int dev, int64_t n, const std::vector<int> &rad, gdsp::Mixed
   int t1 = 1;
   while (t1 < need) t1 <<= 1;
   if (t1 > 64) t1 = (need + 63) / 64 * 64;
-  if (t1 > 512) return fail(GDSP_ERR_UNSUPPORTED, "mixed-radix geometry");
+  // (the runtime-radix kernels check t1 <= 512 themselves; a compiled or
+  // runtime-compiled specialisation may use up to 1024 threads per transform)
+  if (t1 > 1024) return fail(GDSP_ERR_UNSUPPORTED, "mixed-radix geometry");
   d.t1 = t1;
   d.tpw = std::max(1, std::min(256 / t1, gdsp::kMixedMax / (int)n));
   std::vector<cd> h;

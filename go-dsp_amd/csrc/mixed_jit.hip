@@ -5,7 +5,8 @@
 // the runtime-radix kernel (2.5-4 TB/s, n <= 4096) or Bluestein (n > 4096).
 // At plan creation such a length gets a radix list chosen like the compiled
 // ones (as few passes as radices <= 25 allow, full waves, a power-of-2 radix
-// last), and the same kernel templates (mixed_fixed.hpp) are compiled for it
+// last; at most 512 threads per transform where a list allows it, else up to
+// 1024), and the same kernel templates (mixed_fixed.hpp) are compiled for it
 // with hipRTC: the batched transform (forward, inverse, real input) and the
 // fused Pwelch kernel, ~0.5-1 s once per length and process. Any failure
 // (no hipRTC, no headers, a compile error) leaves the plan on the runtime-
@@ -57,10 +58,11 @@ void fixed_geo(const int *rad, int np, int *t1, int *tpw) {
 struct Choice {
   int rad[4], np = 0;
   double eff = 0;
-  bool pow2last = false;
+  bool pow2last = false, wide = false;  // wide: more than 512 threads per transform
 };
 
 bool better(const Choice &a, const Choice &b) {  // a before b?
+  if (a.wide != b.wide) return !a.wide;
   if (a.np != b.np) return a.np < b.np;
   if (a.eff != b.eff) return a.eff > b.eff;
   if (a.pow2last != b.pow2last) return a.pow2last;
@@ -72,10 +74,11 @@ void search(int n, int depth, int maxdepth, Choice &cur, Choice &best) {
     if (n != 1) return;
     int t1 = 0, tpw = 0;
     fixed_geo(cur.rad, depth, &t1, &tpw);
-    if (t1 > 512) return;
+    if (t1 > 1024) return;
     const int wg = t1 * tpw, waves = (wg + 63) / 64;
     Choice c = cur;
     c.np = depth;
+    c.wide = t1 > 512;
     c.eff = (double)wg / (waves * 64);
     const int last = cur.rad[depth - 1];
     c.pow2last = (last & (last - 1)) == 0;
@@ -119,7 +122,7 @@ bool jit_enabled() {
 bool jit_radices(int n, int *rad, int *npass) {
   if (n < 2 || n > kMixedSpecMax || (n & (n - 1)) == 0) return false;
   Choice cur, best;
-  for (int k = 2; k <= 4 && best.np == 0; ++k) search(n, 0, k, cur, best);
+  for (int k = 2; k <= 4; ++k) search(n, 0, k, cur, best);
   if (best.np == 0) return false;
   for (int q = 0; q < best.np; ++q) rad[q] = best.rad[q];
   *npass = best.np;

@@ -514,12 +514,13 @@ def test_random_smooth_lengths(gdsp, oracle):
 
 
 @pytest.mark.parametrize("n,kind", [(810, 5), (1001, 5), (4095, 5), (4320, 5), (5400, 5),
-                                    (6144, 5), (7000, 5), (7680, 5), (8190, 3)])
+                                    (6144, 5), (7000, 5), (7680, 5), (8190, 5), (6561, 5),
+                                    (7290, 5), (8191, 3)])
 def test_jit_specialisations(gdsp, oracle, n, kind):
     # smooth lengths without a compiled specialisation get one compiled at
     # plan creation (mixed_jit.hip, hipRTC); above 4096 they would otherwise
-    # be Bluestein. 8190 = 13 * 630 needs 630 threads per transform in its
-    # radix-13 pass (> 512), so it stays Bluestein.
+    # be Bluestein. 8190 = 13 * 10 * 9 * 7, 6561 = 9^4 and 7290 = 10 * 9^3 need
+    # 630-910 threads per transform (radix 9/13 passes); 8191 is prime.
     D = __import__("importlib").import_module("go-dsp_amd.device")
     assert D.plan(n).kind == kind, n
     rng = np.random.default_rng(4000 + n)
@@ -530,7 +531,7 @@ def test_jit_specialisations(gdsp, oracle, n, kind):
                     oracle.fft_rows(x.real.astype(np.complex128))) < TOL
 
 
-@pytest.mark.parametrize("nfft,nov", [(810, 405), (5400, 2700)])
+@pytest.mark.parametrize("nfft,nov", [(810, 405), (5400, 2700), (8190, 4095)])
 def test_jit_pwelch(gdsp, oracle, nfft, nov):
     rng = np.random.default_rng(nfft)
     x = rng.standard_normal(40 * nfft)
