@@ -305,7 +305,7 @@ hipError_t launch_pwelch_mixed(const MixedDesc &d, const double *x, int64_t nfft
 // (every length dft_any has, <= 25): x as L rows x C columns, one thread per
 // column holds the whole column in registers (no LDS), so each wave-
 // instruction is a contiguous 1 KiB row segment. Column c: DFT_L over its L
-// rows, times W_n^(c*k) (c*k < n: a direct table read), written in place of
+// rows, times W_n^(c*k) (from W_n^c by recurrence), written in place of
 // the rows. The rows DFT_C and the transpose follow (exec_mixed4).
 template <int L, bool CONJ_IN>
 __global__ __launch_bounds__(256) void colradix_kernel(const cd *__restrict__ in,
@@ -324,8 +324,15 @@ __global__ __launch_bounds__(256) void colradix_kernel(const cd *__restrict__ in
   dft_any<L>(v);
   cd *dst = out + b * n + c;
   st_nt(dst, v[0]);
+  // W_n^(c*k) = (W_n^c)^k: one table read and a recurrence (L - 1 reads per
+  // column would scatter over an n-entry table that misses L2 at large n)
+  const cd w1 = tw[c];
+  cd w = w1;
 #pragma unroll
-  for (int k = 1; k < L; ++k) st_nt(dst + k * C, cmul(v[k], tw[c * k]));
+  for (int k = 1; k < L; ++k) {
+    st_nt(dst + k * C, cmul(v[k], w));
+    if (k + 1 < L) w = cmul(w, w1);
+  }
 }
 
 bool colradix_supported(int L) {

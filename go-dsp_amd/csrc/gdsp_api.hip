@@ -310,6 +310,8 @@ struct gdsp_plan {
   // (either way 3 HBM passes instead of 5)
   int64_t n1 = 0, n2 = 0;
   bool pow2col = false, radixcol = false;
+  // mixcol: n1 in [26, 1016] smooth, its column pass runtime-compiled
+  gdsp::JitCol *mixcol = nullptr;
   gdsp_plan *p1 = nullptr, *p2 = nullptr;
   // Bluestein (fft/bluestein.go): M = NextPowerOf2(2n-1), chirp = conj(w),
   // bhat = FFT_M(b)/M
@@ -495,6 +497,30 @@ bool radixcol_split(int64_t n, int64_t &l, int64_t &c) {
   return false;
 }
 
+// n = L * C with L in [26, 1016] a smooth non-power-of-2 length (the
+// column pass, colfixed_kernel compiled for L's radix list) and C a
+// one-kernel length; the smallest such L (widest column tiles) whose column
+// kernel builds wins.
+bool mixcol_build(int dev, int64_t n, gdsp_plan *p) {
+  if (!gdsp::jit_enabled()) return false;
+  for (int64_t L = 26; L <= 1016; ++L) {
+    if (n % L || is_pow2(L) || !one_kernel_len(n / L) || !one_kernel_len(L)) continue;
+    gdsp_plan *p1 = nullptr;
+    if (get_plan_locked(dev, L, &p1) != GDSP_OK || p1->kind != KIND_MIXED) continue;
+    int rad[16], np = p1->md.npass;
+    if (np < 2 || np > 16) continue;
+    for (int q = 0; q < np; ++q) rad[q] = (int)((p1->md.codes >> (5 * q)) & 31);
+    gdsp::JitCol *col = gdsp::jit_col_build(dev, rad, np);
+    if (!col) continue;
+    p->mixcol = col;
+    p->n1 = L;
+    p->n2 = n / L;
+    p->p1 = p1;
+    return true;
+  }
+  return false;
+}
+
 int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   p->device = dev;
   p->n = n;
@@ -536,6 +562,13 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
       radixcol_split(n, p->n1, p->n2)) {
     p->kind = KIND_MIXED4;
     p->radixcol = true;
+    STCHK(get_plan_locked(dev, p->n2, &p->p2));
+    return upload_twiddles(dev, n, &p->tw);
+  }
+  if (!chirpz && next_pow2_ref(2 * n - 1) > ((int64_t)1 << gdsp::kMaxLdsLog2) &&
+      mixcol_build(dev, n, p)) {
+    // the same three-launch structure with a runtime-compiled column pass
+    p->kind = KIND_MIXED4;
     STCHK(get_plan_locked(dev, p->n2, &p->p2));
     return upload_twiddles(dev, n, &p->tw);
   }
@@ -712,7 +745,7 @@ int exec_fourstep(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bo
 int exec_mixed4(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
                 hipStream_t s) {
   const int64_t N = p->n, N1 = p->n1, N2 = p->n2;
-  if (p->pow2col || p->radixcol) {
+  if (p->pow2col || p->radixcol || p->mixcol) {
     // as exec_fourstep with R = N1 (power of 2) and C = N2 (any one-kernel
     // length): column DFT_R on row-segment tiles times W_N^(col*k1) (table
     // index mod N), rows DFT_C, conj/scale-fused transpose R x C -> C x R
@@ -727,7 +760,10 @@ int exec_mixed4(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool
     }
     for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
       const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
-      if (p->radixcol)
+      if (p->mixcol)
+        HIPCHK(gdsp::jit_launch_col(p->mixcol, inv, src + b0 * N, w + b0 * N, N2, N, nb,
+                                    p->p1->tw, p->tw, s));
+      else if (p->radixcol)
         HIPCHK(gdsp::launch_colradix((int)N1, inv, src + b0 * N, w + b0 * N, N2, N, nb, p->tw, s));
       else
         HIPCHK(gdsp::launch_colfft(lr, inv, 2, false, src + b0 * N, w + b0 * N, N2, 1, 0, 1, 0, 1,

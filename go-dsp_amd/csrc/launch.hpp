@@ -49,6 +49,11 @@ struct JitSpec;
 bool jit_enabled();
 bool jit_radices(int n, int *rad, int *npass);
 JitSpec *jit_spec_build(int dev, const int *rad, int np, int n);  // nullptr: not built
+// colfixed_kernel (mixed_fixed.hpp) for the column length prod(rad)
+struct JitCol;
+JitCol *jit_col_build(int dev, const int *rad, int np);  // nullptr: not built
+hipError_t jit_launch_col(const JitCol *j, bool conj_in, const cd *in, cd *out, int64_t C,
+                          int64_t n, int64_t batch, const cd *tw, const cd *twn, hipStream_t s);
 hipError_t jit_launch_fft(const JitSpec *j, bool inv, int load, const void *in, cd *out,
                           int64_t batch, const cd *tw, double scale, hipStream_t s);
 int jit_pw_tpw(const JitSpec *j);

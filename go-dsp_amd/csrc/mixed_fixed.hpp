@@ -383,6 +383,72 @@ __global__ __launch_bounds__((FixedGeo<R0, RS...>::WG)) void pwelch_fixed_kernel
   }
 }
 
+// ---------------------------------------------------------------------------
+// Column pass of the mixed four-step for n = L * C (x as L rows x C columns)
+// with a smooth L that has a radix list (26 <= L <= 1016; L <= 25 is
+// colradix_kernel, a power of 2 colfft_tile_kernel). A workgroup takes W
+// adjacent columns; thread (t, c) = threadIdx.x / W, % W works on column c,
+// so every wave-instruction of the first pass's loads and the last pass's
+// stores covers 64 / W row segments of W * 16 B, all of a thread's loads in
+// flight at once. The exchanges between passes go through LDS per column
+// (column stride SL odd, so the 16-B lanes of a row land on distinct banks).
+// Column c's DFT_L[k] is written times W_n^(c*k) (two table reads and a
+// recurrence per butterfly) in place of the rows; the rows DFT_C and the transpose follow
+// (exec_mixed4). Compiled at plan creation with hipRTC (mixed_jit.hip).
+template <int W, bool SPLIT, bool CONJ_IN, bool SWZ, int R0, int... RS>
+__global__ __launch_bounds__((W * FixedGeo<R0, RS...>::T1)) void colfixed_kernel(
+    const cd *__restrict__ in, cd *__restrict__ out, int64_t C, int64_t n,
+    const cd *__restrict__ tw, const cd *__restrict__ twn) {
+  using G = FixedGeo<R0, RS...>;
+  using First = FPass<R0, G::N, 1, G::T1>;
+  using Last = typename FixedLast<R0, RS...>::Pass;
+  constexpr int SL = G::SLOTS + 1;  // per column, in complex (or, with SPLIT, double) slots
+  __shared__ double lds[W * SL * (SPLIT ? 1 : 2)];
+  const int tid = (int)threadIdx.x, c = tid % W, tl = tid / W;
+  const int64_t col = (int64_t)blockIdx.x * W + c;
+  const bool valid = col < C;
+  const cd *src = in + (int64_t)blockIdx.y * n + col;
+  cd *dst = out + (int64_t)blockIdx.y * n + col;
+  double *ld = lds + c * SL * (SPLIT ? 1 : 2);
+  First p0;
+#pragma unroll
+  for (int jj = 0; jj < First::J; ++jj) {
+    const int j = tl + jj * G::T1;
+    if (First::act(j, valid)) {
+#pragma unroll
+      for (int r = 0; r < R0; ++r) {
+        cd v = ld_nt(src + (int64_t)(j + r * First::NB) * C);
+        if constexpr (CONJ_IN) v.y = -v.y;
+        p0.v[jj][r] = v;
+      }
+    }
+  }
+  p0.compute(tl, valid, tw);
+  auto sink = [&](const Last &q) {
+#pragma unroll
+    for (int jj = 0; jj < Last::J; ++jj) {
+      const int j = tl + jj * G::T1;
+      if (Last::act(j, valid)) {
+        constexpr int RL = FixedLast<R0, RS...>::R, NSL = G::N / RL;  // as FPass::store_hbm
+        const int k0 = j % NSL, o = (j - k0) * RL + k0;
+        // W_n^(col*k) for k = o + r*NSL: two table reads and a recurrence
+        // (one read per element would scatter over an n-entry table that
+        // does not stay in L2 at n ~ 10^6)
+        cd w = twn[col * o];
+        const cd ws = twn[col * NSL];
+#pragma unroll
+        for (int r = 0; r < RL; ++r) {
+          const int64_t k = o + r * NSL;
+          st_nt(dst + k * C, cmul(q.v[jj][r], w));
+          if (r + 1 < RL) w = cmul(w, ws);
+        }
+      }
+    }
+  };
+  fixed_chain_to<SPLIT, SWZ, G::N, G::T1, R0, 0, First, decltype(sink), RS...>(p0, tl, valid, ld,
+                                                                               tw, sink);
+}
+
 #ifndef __HIPCC_RTC__
 template <int... RS>
 static int spec_pw_tpw(Spec<RS...>, const MixedDesc &d) {

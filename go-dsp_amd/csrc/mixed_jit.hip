@@ -33,6 +33,12 @@ struct JitSpec {
   int n = 0, wg = 0, tpw = 0;
 };
 
+struct JitCol {  // colfixed_kernel for one column length
+  hipModule_t mod = nullptr;
+  hipFunction_t fwd = nullptr, inv = nullptr;
+  int l = 0, w = 0, wg = 0;
+};
+
 namespace {
 
 // the radices dft_any has (mixed_core.hpp)
@@ -129,64 +135,141 @@ bool jit_radices(int n, int *rad, int *npass) {
   return true;
 }
 
-JitSpec *jit_spec_build(int dev, const int *rad, int np, int n) {
-  if (!jit_enabled()) return nullptr;
+namespace {
+
+// Compile `names` (kernel template instances of mixed_fixed.hpp) for device
+// dev into one module; fs[q] = the kernel of names[q]. false on any failure.
+bool compile_module(int dev, const std::vector<std::string> &names, const std::string &what,
+                    hipModule_t *mod, std::vector<hipFunction_t> &fs) {
   hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return nullptr;
-  std::string list;
-  for (int q = 0; q < np; ++q) list += ", " + std::to_string(rad[q]);
-  const bool split = n > 4096, swz = rad[0] % 2 == 0;  // as spec_launch / launch_fixed
-  const std::string sp = split ? "true" : "false", sw = swz ? "true" : "false";
-  const std::string names[4] = {
-      "&gdsp::fft_mixed_fixed_kernel<false, 0, " + sp + ", " + sw + list + ">",
-      "&gdsp::fft_mixed_fixed_kernel<true, 0, " + sp + ", " + sw + list + ">",
-      "&gdsp::fft_mixed_fixed_kernel<false, 1, " + sp + ", " + sw + list + ">",
-      "&gdsp::pwelch_fixed_kernel<" + sw + list + ">"};
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
   const char *src = "#include \"mixed_fixed.hpp\"\n";
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src, "gdsp_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
-    return nullptr;
+    return false;
   for (const auto &nm : names) hiprtcAddNameExpression(prog, nm.c_str());
   const std::string arch = std::string("--offload-arch=") + prop.gcnArchName;
   const std::string inc = "-I" + include_dir();
   const char *opts[] = {arch.c_str(), "-O3", "-std=c++17", inc.c_str()};
-  JitSpec *j = nullptr;
+  bool ok = false;
+  *mod = nullptr;
   const hiprtcResult rc = hiprtcCompileProgram(prog, 4, opts);
   if (rc == HIPRTC_SUCCESS) {
     size_t cs = 0;
     hiprtcGetCodeSize(prog, &cs);
     std::vector<char> code(cs);
     hiprtcGetCode(prog, code.data());
-    j = new JitSpec;
-    j->n = n;
-    int t1 = 0;
-    fixed_geo(rad, np, &t1, &j->tpw);
-    j->wg = t1 * j->tpw;
-    hipFunction_t *fs[4] = {&j->fwd, &j->inv, &j->real, &j->pw};
-    bool ok = hipModuleLoadData(&j->mod, code.data()) == hipSuccess;
-    for (int q = 0; ok && q < 4; ++q) {
+    fs.assign(names.size(), nullptr);
+    ok = hipModuleLoadData(mod, code.data()) == hipSuccess;
+    for (size_t q = 0; ok && q < names.size(); ++q) {
       const char *low = nullptr;
       ok = hiprtcGetLoweredName(prog, names[q].c_str(), &low) == HIPRTC_SUCCESS && low &&
-           hipModuleGetFunction(fs[q], j->mod, low) == hipSuccess;
+           hipModuleGetFunction(&fs[q], *mod, low) == hipSuccess;
     }
-    if (!ok) {
-      if (j->mod) (void)hipModuleUnload(j->mod);
-      delete j;
-      j = nullptr;
+    if (!ok && *mod) {
+      (void)hipModuleUnload(*mod);
+      *mod = nullptr;
     }
   } else if (verbose()) {
     size_t ls = 0;
     hiprtcGetProgramLogSize(prog, &ls);
     std::string log(ls, '\0');
     if (ls) hiprtcGetProgramLog(prog, &log[0]);
-    fprintf(stderr, "gdsp: hipRTC specialisation for n = %d failed (%s; %s %s):\n%s\n", n,
+    fprintf(stderr, "gdsp: hipRTC %s failed (%s; %s %s):\n%s\n", what.c_str(),
             hiprtcGetErrorString(rc), arch.c_str(), inc.c_str(), log.c_str());
   }
   hiprtcDestroyProgram(&prog);
-  if (verbose())
-    fprintf(stderr, "gdsp: hipRTC specialisation for n = %d (%s): %s\n", n, list.c_str() + 2,
-            j ? "built" : "not built");
+  if (verbose()) fprintf(stderr, "gdsp: hipRTC %s: %s\n", what.c_str(), ok ? "built" : "not built");
+  return ok;
+}
+
+std::string radix_list(const int *rad, int np) {
+  std::string list;
+  for (int q = 0; q < np; ++q) list += ", " + std::to_string(rad[q]);
+  return list;
+}
+
+}  // namespace
+
+JitSpec *jit_spec_build(int dev, const int *rad, int np, int n) {
+  if (!jit_enabled()) return nullptr;
+  const std::string list = radix_list(rad, np);
+  const bool split = n > 4096, swz = rad[0] % 2 == 0;  // as spec_launch / launch_fixed
+  const std::string sp = split ? "true" : "false", sw = swz ? "true" : "false";
+  const std::vector<std::string> names = {
+      "&gdsp::fft_mixed_fixed_kernel<false, 0, " + sp + ", " + sw + list + ">",
+      "&gdsp::fft_mixed_fixed_kernel<true, 0, " + sp + ", " + sw + list + ">",
+      "&gdsp::fft_mixed_fixed_kernel<false, 1, " + sp + ", " + sw + list + ">",
+      "&gdsp::pwelch_fixed_kernel<" + sw + list + ">"};
+  hipModule_t mod = nullptr;
+  std::vector<hipFunction_t> fs;
+  if (!compile_module(dev, names, "specialisation for n = " + std::to_string(n) + " (" +
+                                      list.substr(2) + ")",
+                      &mod, fs))
+    return nullptr;
+  JitSpec *j = new JitSpec;
+  j->mod = mod;
+  j->n = n;
+  j->fwd = fs[0];
+  j->inv = fs[1];
+  j->real = fs[2];
+  j->pw = fs[3];
+  int t1 = 0;
+  fixed_geo(rad, np, &t1, &j->tpw);
+  j->wg = t1 * j->tpw;
   return j;
+}
+
+JitCol *jit_col_build(int dev, const int *rad, int np) {
+  if (!jit_enabled() || np < 2) return nullptr;
+  int L = 1;
+  for (int q = 0; q < np; ++q) L *= rad[q];
+  int t1 = 0, tpw = 0;
+  fixed_geo(rad, np, &t1, &tpw);
+  // columns per workgroup: the widest power of 2 <= 64 whose LDS (column
+  // stride SL = slots + 1, odd) fits 80 KiB (two workgroups per CU), within
+  // 1024 threads. The exchanges go as real / imaginary halves (SPLIT), which
+  // doubles the width the LDS allows. Per 2^27 samples, 16 complex-exchange
+  // columns -> this: 390625 3.15 -> 2.73 ms, 3^13 3.18 -> 2.98, 10^6 2.80
+  // both (GDSP_COL_LDS / GDSP_COL_SPLIT=0 to compare)
+  const int sl = ((L + 7) & ~7) + 1;
+  int lds_max = 81920;
+  if (const char *e = getenv("GDSP_COL_LDS")) lds_max = atoi(e);
+  const char *se = getenv("GDSP_COL_SPLIT");
+  const bool split = !(se && se[0] == '0');
+  const int bytes = split ? 8 : 16;
+  int w = 64;
+  while (w > 1 && (w * sl * bytes > lds_max || w * t1 > 1024)) w >>= 1;
+  if (w * sl * bytes > 163840 || w * t1 > 1024) return nullptr;
+  const std::string list = radix_list(rad, np), sw = rad[0] % 2 == 0 ? "true" : "false";
+  const std::string ws = std::to_string(w) + (split ? ", true" : ", false");
+  const std::vector<std::string> names = {
+      "&gdsp::colfixed_kernel<" + ws + ", false, " + sw + list + ">",
+      "&gdsp::colfixed_kernel<" + ws + ", true, " + sw + list + ">"};
+  hipModule_t mod = nullptr;
+  std::vector<hipFunction_t> fs;
+  if (!compile_module(dev, names, "column pass for L = " + std::to_string(L) + " (" +
+                                      list.substr(2) + "), " + ws + " columns",
+                      &mod, fs))
+    return nullptr;
+  JitCol *j = new JitCol;
+  j->mod = mod;
+  j->fwd = fs[0];
+  j->inv = fs[1];
+  j->l = L;
+  j->w = w;
+  j->wg = w * t1;
+  return j;
+}
+
+hipError_t jit_launch_col(const JitCol *j, bool conj_in, const cd *in, cd *out, int64_t C,
+                          int64_t n, int64_t batch, const cd *tw, const cd *twn, hipStream_t s) {
+  if (batch < 1 || batch > 65535 || C < 1 || C * j->l != n) return hipErrorInvalidValue;
+  const int64_t gx = (C + j->w - 1) / j->w;
+  if (gx > 0x7fffffff) return hipErrorInvalidValue;
+  void *args[] = {(void *)&in, (void *)&out, (void *)&C, (void *)&n, (void *)&tw, (void *)&twn};
+  return hipModuleLaunchKernel(conj_in ? j->inv : j->fwd, (unsigned)gx, (unsigned)batch, 1,
+                               (unsigned)j->wg, 1, 1, 0, s, args, nullptr);
 }
 
 hipError_t jit_launch_fft(const JitSpec *j, bool inv, int load, const void *in, cd *out,

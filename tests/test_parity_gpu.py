@@ -351,7 +351,11 @@ def test_chirpz_plan_vs_oracle(gdsp, oracle, n):
 MIXED4 = [4100, 5000, 6000, 8190, 10000, 44100, 48000, 3 << 16, 8209, 100000, 1000000,
           # single-radix columns (25 x 3528, 25 x 882, 9 x 2187) and power-of-2
           # columns (16 x 1875): three passes
-          88200, 22050, 19683, 30000]
+          88200, 22050, 19683, 30000,
+          # runtime-compiled mixed-radix columns (colfixed_kernel): 16-column
+          # tiles (125 x 3125, 75 x 8000, 125 x 8008, 243 x 6561), 8 columns
+          # (343 x 2401) and 4 columns (630 x 7875): three passes
+          390625, 600000, 1001000, 1594323, 823543, 4961250]
 
 
 @pytest.mark.parametrize("n", MIXED4)
@@ -359,7 +363,20 @@ def test_mixed_fourstep_vs_oracle(gdsp, oracle, n):
     rng = np.random.default_rng(3000 + n)
     batch = 3 if n <= 100000 else 1
     x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
-    assert row_nrel(gdsp.fft.FFTBatch(x), oracle.fft_rows(x)) < TOL
+    y = gdsp.fft.FFTBatch(x)
+    if n > 2000000:
+        # The reference's chirp angle pi/n*k^2 is not reduced (bluestein.go:53),
+        # so its own error grows with n: at 4961250 the oracle is 5.5e-10
+        # normwise and 1.1e-9 max-abs from the exact DFT, against 7e-16 for
+        # the engine (scripts/acc_probe.py). Here the bound against the oracle
+        # is the reference tests' own 1e-8 (Float64Equal), the engine is held
+        # to the exact DFT, and the inverse to a round trip (the oracle takes
+        # ~16 s per transform at this size).
+        assert row_nrel(y, oracle.fft_rows(x)) < 1e-8
+        assert row_nrel(y, np.fft.fft(x, axis=1)) < 1e-13
+        assert row_nrel(gdsp.fft.FFTBatch(y, inverse=True), x) < TOL
+        return
+    assert row_nrel(y, oracle.fft_rows(x)) < TOL
     assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL
     xr = rng.uniform(-1, 1, (batch, n))
     assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
