@@ -555,17 +555,23 @@ __global__ __launch_bounds__(WGT) void colfft_tile_kernel(
 // Options: conj + scale on the way out; times tw[r*c] (conjugated if
 // tw_conj; the caller guarantees r*c < twn, as rows*cols = twn in the
 // mixed four-step's W_N^(n2*k1) step).
+template <int TR, int TC>
 __global__ __launch_bounds__(256) void transpose_kernel(const cd *__restrict__ in,
                                                         cd *__restrict__ out, int64_t rows,
                                                         int64_t cols, int64_t batch,
                                                         int conj_scale, double scale,
                                                         const cd *__restrict__ tw, int64_t twn,
                                                         int tw_conj) {
-  __shared__ cd tile[32][33];
-  const int64_t tiles_c = (cols + 31) / 32;
-  const int64_t tiles_r = (rows + 31) / 32;
+  // TR rows x TC columns per tile: loads are TC * 16 B row segments, stores
+  // TR * 16 B column segments; the LDS row stride TC + 1 is odd, so the
+  // column reads are conflict-free
+  constexpr int LY = 256 / TC, SY = 256 / TR;
+  __shared__ cd tile[TR][TC + 1];
+  const int64_t tiles_c = (cols + TC - 1) / TC;
+  const int64_t tiles_r = (rows + TR - 1) / TR;
   const int64_t per = tiles_c * tiles_r;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  const int lx = threadIdx.x % TC, ly = threadIdx.x / TC;
+  const int sx = threadIdx.x % TR, sy = threadIdx.x / TR;
   // (a register-prefetch variant, next tile's loads issued before this
   // tile's stores, measured 853 -> 1385 us on 2048 16x4096 matrices)
   for (int64_t tg = blockIdx.x; tg < per * batch; tg += gridDim.x) {
@@ -574,24 +580,31 @@ __global__ __launch_bounds__(256) void transpose_kernel(const cd *__restrict__ i
     const cd *src = in + b * rows * cols;
     cd *dst = out + b * rows * cols;
 #pragma unroll
-    for (int i = 0; i < 32; i += 8) {
-      const int64_t r = tr * 32 + ty + i, c = tc * 32 + tx;
-      if (r < rows && c < cols) tile[ty + i][tx] = ld_nt(&src[r * cols + c]);
+    for (int i = 0; i < TR; i += LY) {
+      const int64_t r = tr * TR + ly + i, c = tc * TC + lx;
+      if (r < rows && c < cols) tile[ly + i][lx] = ld_nt(&src[r * cols + c]);
     }
     __syncthreads();
+    const int64_t r = tr * TR + sx;
+    cd w = {1.0, 0.0}, ws = {1.0, 0.0};
+    if (tw && r < rows) {  // W^(r*c) for c = c0 + sy + SY*i: two reads and a recurrence
+      w = tw[r * (tc * TC + sy) % twn];
+      ws = tw[r * SY % twn];
+      if (tw_conj) {
+        w.y = -w.y;
+        ws.y = -ws.y;
+      }
+    }
 #pragma unroll
-    for (int i = 0; i < 32; i += 8) {
-      const int64_t c = tc * 32 + ty + i, r = tr * 32 + tx;
+    for (int i = 0; i < TC; i += SY) {
+      const int64_t c = tc * TC + sy + i;
       if (r < rows && c < cols) {
-        cd o = tile[tx][ty + i];
-        if (tw) {
-          cd w = tw[r * c];
-          if (tw_conj) w.y = -w.y;
-          o = cmul(o, w);
-        }
+        cd o = tile[sx][sy + i];
+        if (tw) o = cmul(o, w);
         if (conj_scale) o = {o.x * scale, -o.y * scale};
         st_nt(&dst[c * rows + r], o);
       }
+      if (tw && i + SY < TC) w = cmul(w, ws);
     }
     __syncthreads();
   }
@@ -965,11 +978,22 @@ hipError_t launch_transpose(const cd *in, cd *out, int64_t rows, int64_t cols, h
                             int64_t twn, bool tw_conj) {
   if (batch < 1 || batch > 65535) return hipErrorInvalidValue;
   if (tw && (rows - 1) * (cols - 1) >= twn) return hipErrorInvalidValue;  // r*c < twn
-  const int64_t tiles = ((rows + 31) / 32) * ((cols + 31) / 32) * batch;
+  // tile shape (rows x columns): 32 x 64 by default; GDSP_TRANSPOSE=32 (32 x
+  // 32) and 64 (64 x 64) to compare
+  static const int shape = getenv("GDSP_TRANSPOSE") ? atoi(getenv("GDSP_TRANSPOSE")) : 0;
+  const int tr = shape == 64 ? 64 : 32, tc = shape == 32 ? 32 : 64;
+  const int64_t tiles = ((rows + tr - 1) / tr) * ((cols + tc - 1) / tc) * batch;
   const int64_t cap = 256 * 32;  // 32 tile-loop workgroups per CU
   const unsigned nb = (unsigned)(tiles < cap ? tiles : cap);
-  hipLaunchKernelGGL(transpose_kernel, dim3(nb), dim3(256), 0, s, in, out, rows, cols, batch,
-                     (int)conj_scale, scale, tw, twn, (int)tw_conj);
+  if (shape == 32)
+    hipLaunchKernelGGL((transpose_kernel<32, 32>), dim3(nb), dim3(256), 0, s, in, out, rows, cols,
+                       batch, (int)conj_scale, scale, tw, twn, (int)tw_conj);
+  else if (shape == 64)
+    hipLaunchKernelGGL((transpose_kernel<64, 64>), dim3(nb), dim3(256), 0, s, in, out, rows, cols,
+                       batch, (int)conj_scale, scale, tw, twn, (int)tw_conj);
+  else
+    hipLaunchKernelGGL((transpose_kernel<32, 64>), dim3(nb), dim3(256), 0, s, in, out, rows, cols,
+                       batch, (int)conj_scale, scale, tw, twn, (int)tw_conj);
   return hipGetLastError();
 }
 

@@ -116,3 +116,31 @@ print("ok")
     env = dict(os.environ, GDSP_MIXED_GENERIC="1", REPO=REPO)
     r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_paths_without_runtime_compiler():
+    """GDSP_JIT=0: lengths the runtime compiler would take keep the paths it
+    replaces (runtime-radix kernel, chirp-z, the five-pass four-step with its
+    twiddled transpose), which must still agree with the oracle."""
+    code = r'''
+import importlib, os, sys
+sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
+import numpy as np, oracle
+g = importlib.import_module("go-dsp_amd")
+D = importlib.import_module("go-dsp_amd.device")
+import torch
+rng = np.random.default_rng(5)
+for n, kind, batch in ((810, 5, 5), (5400, 3, 3), (390625, 6, 1), (600000, 6, 1)):
+    assert D.plan(n).kind == kind, (n, D.plan(n).kind)
+    x = rng.standard_normal((batch, n)) + 1j * rng.standard_normal((batch, n))
+    for inv in (False, True):
+        y = g.fft.FFTBatch(x, inverse=inv)
+        ref = oracle.ifft_rows(x) if inv else oracle.fft_rows(x)
+        err = max(np.linalg.norm(a - b) / np.linalg.norm(b) for a, b in zip(y, ref))
+        assert err < 1e-9, (n, inv, err)
+print("ok")
+'''
+    env = dict(os.environ, GDSP_JIT="0", REPO=REPO)
+    r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
