@@ -556,3 +556,15 @@ def test_jit_pwelch(gdsp, oracle, nfft, nov):
     p, f = gdsp.spectral.Pwelch(x, 3.0, o)
     pr, fr = oracle.pwelch(x, 3.0, nfft=nfft, noverlap=nov)
     assert nrel(p, pr) < TOL and nrel(f, fr) == 0.0
+
+
+@pytest.mark.parametrize("n", [17, 101, 1009, 2053, 2741, 3001, 3571])
+def test_chirpz_primes(gdsp, oracle, n):
+    # primes take the fused chirp-z kernel (M = NextPowerOf2(2n - 1), as
+    # bluestein.go:70), forward, inverse and real input
+    rng = np.random.default_rng(7000 + n)
+    x = rng.uniform(-1, 1, (5, n)) + 1j * rng.uniform(-1, 1, (5, n))
+    assert row_nrel(gdsp.fft.FFTBatch(x), oracle.fft_rows(x)) < TOL
+    assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL
+    xr = x.real.copy()
+    assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
