@@ -530,6 +530,25 @@ def test_random_smooth_lengths(gdsp, oracle):
     assert {5, 6} <= kinds, kinds
 
 
+def test_random_large_smooth_lengths(gdsp, oracle):
+    # seeded random 13-smooth lengths in (200000, 2000000]: the three-pass
+    # column splits (power-of-2, single-radix and runtime-compiled mixed-radix
+    # columns) and whatever falls through to the five-pass form. Forward only
+    # (the oracle takes 0.5-2 s per transform here); the inverse path is the
+    # same kernels with conj in / conj + scale out, covered at smaller sizes.
+    rng = np.random.default_rng(11)
+    lengths = set()
+    while len(lengths) < 8:
+        n = 1
+        for p, emax in ((2, 12), (3, 8), (5, 6), (7, 4), (11, 2), (13, 2)):
+            n *= p ** int(rng.integers(0, emax + 1))
+        if 200000 < n <= 2000000 and n & (n - 1):
+            lengths.add(n)
+    for n in sorted(lengths):
+        x = rng.uniform(-1, 1, (1, n)) + 1j * rng.uniform(-1, 1, (1, n))
+        assert row_nrel(gdsp.fft.FFTBatch(x), oracle.fft_rows(x)) < TOL, n
+
+
 @pytest.mark.parametrize("n,kind", [(810, 5), (1001, 5), (4095, 5), (4320, 5), (5400, 5),
                                     (6144, 5), (7000, 5), (7680, 5), (8190, 5), (6561, 5),
                                     (7290, 5), (8191, 3)])
