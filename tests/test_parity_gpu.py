@@ -488,6 +488,36 @@ def test_concurrent_host_calls(gdsp, oracle):
     assert max(errs.values()) < TOL, errs
 
 
+def test_concurrent_runtime_compiled_plans(gdsp, oracle):
+    # six threads whose first call each builds a plan through hipRTC at the
+    # same time (lengths used nowhere else in the suite): one-kernel mixed
+    # radix (1890, 2310, 5292, 6930, 2730) and a runtime-compiled column pass
+    # (700000 = 100 x 7000)
+    import threading
+    sizes = [1890, 2310, 5292, 6930, 2730, 700000]
+    errs, fails = {}, []
+
+    def work(i):
+        try:
+            n = sizes[i]
+            rng = np.random.default_rng(90 + i)
+            b = 1 if n > 100000 else 3
+            x = rng.standard_normal((b, n)) + 1j * rng.standard_normal((b, n))
+            y = gdsp.fft.FFTBatch(x)
+            z = gdsp.fft.FFTBatch(y, inverse=True)
+            errs[i] = max(row_nrel(y, oracle.fft_rows(x)), row_nrel(z, x))
+        except Exception as ex:  # surfaced below
+            fails.append((i, repr(ex)))
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(len(sizes))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not fails, fails
+    assert max(errs.values()) < TOL, errs
+
+
 def test_random_lengths_every_plan_kind(gdsp, oracle):
     # 40 seeded random lengths in [2, 40000]: powers of 2, compiled and
     # runtime-radix mixed lengths, both four-step column forms, the general
