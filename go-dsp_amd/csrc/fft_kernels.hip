@@ -736,6 +736,20 @@ hipError_t launch_fft_lds(int log2n, bool inv, int load, bool split, const void 
 template <int LOG2M, bool INV>
 static hipError_t launch_blu_t(const cd *in, cd *out, int64_t n, int64_t batch, const cd *twm,
                                const cd *chirp, const cd *bhat, double scale, hipStream_t s) {
+  // M = 8192 / 16384: 32 points per thread (three passes, two exchanges, one
+  // twiddle stage fewer; 254 VGPRs, 2 waves per SIMD) beat 16 (four passes,
+  // 124 VGPRs, 4 waves per SIMD): chirp-z 3000 3.44 against 3.56 ms, primes
+  // 4099..8191 (M = 16384) 2-5 % (GDSP_BLU_E16=1 to compare)
+  if constexpr (LOG2M == 13 || LOG2M == 14) {
+    static const bool e32 = getenv("GDSP_BLU_E16") == nullptr;
+    if (e32) {
+      using G5 = Geo<LOG2M, 5>;
+      const int64_t nb5 = (batch + G5::TPW - 1) / G5::TPW;
+      hipLaunchKernelGGL((bluestein_kernel<LOG2M, INV, true, 5>), dim3((unsigned)nb5),
+                         dim3(G5::WG), 0, s, in, out, n, batch, twm, chirp, bhat, scale);
+      return hipGetLastError();
+    }
+  }
   using G = Geo<LOG2M>;
   const int64_t nblk = (batch + G::TPW - 1) / G::TPW;
   hipLaunchKernelGGL((bluestein_kernel<LOG2M, INV, true>), dim3((unsigned)nblk), dim3(G::WG), 0,

@@ -48,8 +48,11 @@ def main(tag, workloads):
     res = {w: collect(w) for w in workloads}
     dst = os.path.join(REPO, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
-    with open(os.path.join(dst, "sq_counters.json"), "w") as f:
-        json.dump(res, f, indent=1, sort_keys=True)
+    path = os.path.join(dst, "sq_counters.json")
+    merged = json.load(open(path)) if os.path.exists(path) else {}
+    merged.update(res)  # the workloads re-measured replace their entries
+    with open(path, "w") as f:
+        json.dump(merged, f, indent=1, sort_keys=True)
     for w, ks in res.items():
         print("==", w)
         for k, m in ks.items():
