@@ -40,11 +40,12 @@ struct Stage {
   __device__ __forceinline__ static int pad(int i) { return i + i / G::E; }
 };
 
-template <int LOG2N, bool INV, int LOAD, bool SPLIT>
-__global__ __launch_bounds__(Geo<LOG2N>::WG, (LOG2N >= 13 && SPLIT ? 4 : 1)) void fft_lds_kernel(
-    const void *__restrict__ in, cd *__restrict__ out, int64_t batch,
-    const cd *__restrict__ tw, double scale) {
-  using G = Geo<LOG2N>;
+template <int LOG2N, bool INV, int LOAD, bool SPLIT, int LOG2E = 4>
+__global__ __launch_bounds__((Geo<LOG2N, LOG2E>::WG),
+                             (LOG2N >= 13 && SPLIT ? (LOG2E == 4 ? 4 : 2) : 1)) void
+fft_lds_kernel(const void *__restrict__ in, cd *__restrict__ out, int64_t batch,
+               const cd *__restrict__ tw, double scale) {
+  using G = Geo<LOG2N, LOG2E>;
   using S = Stage<LOG2N>;
   constexpr int XD = (SPLIT ? 1 : 2) * G::LDS_DOUBLES;
   __shared__ double lds[XD > S::DOUBLES ? XD : S::DOUBLES];
@@ -108,7 +109,7 @@ __global__ __launch_bounds__(Geo<LOG2N>::WG, (LOG2N >= 13 && SPLIT ? 4 : 1)) voi
 #pragma unroll
     for (int k = 0; k < G::E; ++k) v[k] = {ld_nt(&src[t + k * G::T]), 0.0};
   }
-  fft_regs<LOG2N, SPLIT>(v, t, tw, lre, lim);
+  fft_regs<LOG2N, SPLIT, 0, LOG2E>(v, t, tw, lre, lim);
   if constexpr (S::ON) {
     const int64_t base = blk * G::TPW * G::N, total = batch * G::N;
     double tmp[2][G::E];
@@ -687,6 +688,20 @@ static inline unsigned blocks_for(int64_t work, int per) {
 template <int LOG2N, bool INV, int LOAD, bool SPLIT>
 static hipError_t launch_lds_t(const void *in, cd *out, int64_t batch, const cd *tw,
                                double scale, hipStream_t s) {
+  // N = 16384: one 139 KiB workgroup per CU either way; 32 points per thread
+  // (512 threads, three passes) 0.918-0.930 against 0.966-0.969 ms per 2^27
+  // samples for 16 (1024 threads, four passes), alternating runs
+  // (GDSP_LDS14_E16=1 to compare)
+  if constexpr (LOG2N == 14) {
+    static const bool e32 = getenv("GDSP_LDS14_E16") == nullptr;
+    if (e32) {
+      using G5 = Geo<LOG2N, 5>;
+      const int64_t nb5 = (batch + G5::TPW - 1) / G5::TPW;
+      hipLaunchKernelGGL((fft_lds_kernel<LOG2N, INV, LOAD, SPLIT, 5>), dim3((unsigned)nb5),
+                         dim3(G5::WG), 0, s, in, out, batch, tw, scale);
+      return hipGetLastError();
+    }
+  }
   using G = Geo<LOG2N>;
   const int64_t nblk = (batch + G::TPW - 1) / G::TPW;
   hipLaunchKernelGGL((fft_lds_kernel<LOG2N, INV, LOAD, SPLIT>), dim3((unsigned)nblk),
