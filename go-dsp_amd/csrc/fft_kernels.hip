@@ -873,7 +873,15 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
 #undef GDSP_PWH
     // F = 16384: the exchange buffer alone takes 136 KiB, so the window is
     // re-read from L1/L2 instead of living in LDS
-    case 14: return launch_pwh_t<14, 1>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
+    case 14: {
+      // 32 points per thread (512 threads): 2.25-2.27 against 2.37-2.40 ms at
+      // 2^28 samples for 16 (1024 threads); both spill (GDSP_PWH14_E16=1)
+      static const bool e32 = getenv("GDSP_PWH14_E16") == nullptr;
+      if (e32)
+        return launch_pwh_t<14, 1, 1, 5>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial,
+                                         s);
+      return launch_pwh_t<14, 1>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
+    }
     default: return hipErrorInvalidValue;
   }
 }

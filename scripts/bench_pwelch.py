@@ -23,7 +23,8 @@ if __name__ == "__main__":
     x = torch.empty(total, dtype=torch.float64, device="cuda")
     D.fill_uniform(x, 0x5EED)
     s = torch.cuda.Stream()
-    for nfft, nov in CASES:
+    cases = [tuple(int(v) for v in a.split(":")) for a in sys.argv[1:]] or CASES  # "nfft:nov"
+    for nfft, nov in cases:
         o = gdsp.spectral.PwelchOptions(NFFT=nfft, Noverlap=nov)
         sh = Dd.plan_pwelch(total, 1, 0, nfft, 0, nov)
         Dd.pwelch(x, 1.0, o, sh, stream=s)
