@@ -144,3 +144,31 @@ print("ok")
     env = dict(os.environ, GDSP_JIT="0", REPO=REPO)
     r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_runtime_compiler_failure_falls_back():
+    """A failed runtime compilation (here: the headers are not where
+    GDSP_JIT_INCLUDE points) leaves each plan on the path it replaces, with
+    the same results: the runtime compiler is a speed path only."""
+    code = r'''
+import importlib, os, sys
+sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
+import numpy as np, oracle
+g = importlib.import_module("go-dsp_amd")
+D = importlib.import_module("go-dsp_amd.device")
+import torch
+rng = np.random.default_rng(6)
+for n, kind in ((810, 5), (4320, 3), (390625, 6)):
+    assert D.plan(n).kind == kind, (n, D.plan(n).kind)
+    x = rng.standard_normal((1, n)) + 1j * rng.standard_normal((1, n))
+    y = g.fft.FFTBatch(x)
+    err = np.linalg.norm(y - oracle.fft_rows(x)) / np.linalg.norm(y)
+    assert err < 1e-9, (n, err)
+print("ok")
+'''
+    env = dict(os.environ, GDSP_JIT_INCLUDE="/nonexistent-gdsp-headers", GDSP_JIT_VERBOSE="1",
+               REPO=REPO)
+    r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+    assert "not built" in r.stderr, r.stderr[-2000:]
