@@ -453,7 +453,7 @@ bool one_kernel_len(int64_t m) {
   if (is_pow2(m)) return ilog2(m) <= gdsp::kMaxLdsLog2;
   std::vector<int> rad;
   if (mixed_radices(m, rad)) return true;
-  int jr[4], jnp = 0;  // a runtime-compiled specialisation (else the sub-plan takes Bluestein)
+  int jr[5], jnp = 0;  // a runtime-compiled specialisation (else the sub-plan takes Bluestein)
   return gdsp::jit_enabled() && gdsp::jit_radices((int)m, jr, &jnp);
 }
 
@@ -539,7 +539,7 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
       gdsp::jit_enabled()) {
     // smooth length without a compiled specialisation: compile one (hipRTC);
     // if that fails it takes the runtime-radix kernel or Bluestein below
-    int jr[4], jnp = 0;
+    int jr[5], jnp = 0;
     if (gdsp::jit_radices((int)n, jr, &jnp)) {
       if (gdsp::JitSpec *j = gdsp::jit_spec_build(dev, jr, jnp, (int)n)) {
         p->jit = j;

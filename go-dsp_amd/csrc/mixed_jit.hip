@@ -62,7 +62,7 @@ void fixed_geo(const int *rad, int np, int *t1, int *tpw) {
 }
 
 struct Choice {
-  int rad[4], np = 0;
+  int rad[5], np = 0;
   double eff = 0;
   bool pow2last = false, wide = false;  // wide: more than 512 threads per transform
 };
@@ -129,6 +129,9 @@ bool jit_radices(int n, int *rad, int *npass) {
   if (n < 2 || n > kMixedSpecMax || (n & (n - 1)) == 0) return false;
   Choice cur, best;
   for (int k = 2; k <= 4; ++k) search(n, 0, k, cur, best);
+  // five passes only where no shorter list exists (2 * 7^4 = 4802, 2 * 3^4
+  // * 7^2 = 7938, ...: chirp-z otherwise)
+  if (best.np == 0) search(n, 0, 5, cur, best);
   if (best.np == 0) return false;
   for (int q = 0; q < best.np; ++q) rad[q] = best.rad[q];
   *npass = best.np;

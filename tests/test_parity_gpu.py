@@ -581,12 +581,13 @@ def test_random_large_smooth_lengths(gdsp, oracle):
 
 @pytest.mark.parametrize("n,kind", [(810, 5), (1001, 5), (4095, 5), (4320, 5), (5400, 5),
                                     (6144, 5), (7000, 5), (7680, 5), (8190, 5), (6561, 5),
-                                    (7290, 5), (8191, 3)])
+                                    (7290, 5), (4802, 5), (7938, 5), (8191, 3)])
 def test_jit_specialisations(gdsp, oracle, n, kind):
     # smooth lengths without a compiled specialisation get one compiled at
     # plan creation (mixed_jit.hip, hipRTC); above 4096 they would otherwise
     # be Bluestein. 8190 = 13 * 10 * 9 * 7, 6561 = 9^4 and 7290 = 10 * 9^3 need
-    # 630-910 threads per transform (radix 9/13 passes); 8191 is prime.
+    # 630-910 threads per transform (radix 9/13 passes); 4802 = 2 * 7^4 and
+    # 7938 = 2 * 3^4 * 7^2 have no list shorter than five passes; 8191 is prime.
     D = __import__("importlib").import_module("go-dsp_amd.device")
     assert D.plan(n).kind == kind, n
     rng = np.random.default_rng(4000 + n)
