@@ -21,8 +21,11 @@ g = importlib.import_module("go-dsp_amd")
 D = importlib.import_module("go-dsp_amd.device")
 
 
+PRIMES = (2, 3, 5, 7, 11, 13, 17, 19, 23) if os.environ.get("SWEEP23") else (2, 3, 5, 7, 11, 13)
+
+
 def smooth(n):
-    for p in (2, 3, 5, 7, 11, 13):
+    for p in PRIMES:
         while n % p == 0:
             n //= p
     return n == 1
@@ -37,7 +40,8 @@ if __name__ == "__main__":
     rng = np.random.default_rng(1)
     worst, count, kinds, t_build = 0.0, 0, {}, 0.0
     for n in range(lo, hi + 1):
-        if not smooth(n) or n & (n - 1) == 0:
+        if not smooth(n) or n & (n - 1) == 0 or (os.environ.get("SWEEP23") and all(
+                n % p for p in (17, 19, 23))):
             continue
         t0 = time.perf_counter()
         k = D.plan(n).kind

@@ -355,7 +355,9 @@ MIXED4 = [4100, 5000, 6000, 8190, 10000, 44100, 48000, 3 << 16, 8209, 100000, 10
           # runtime-compiled mixed-radix columns (colfixed_kernel): 16-column
           # tiles (125 x 3125, 75 x 8000, 125 x 8008, 243 x 6561), 8 columns
           # (343 x 2401) and 4 columns (630 x 7875): three passes
-          390625, 600000, 1001000, 1594323, 823543, 4961250]
+          390625, 600000, 1001000, 1594323, 823543, 4961250,
+          # 17 * 2^16: power-of-2 columns, rows of 2176 = 17 * 128
+          1114112]
 
 
 @pytest.mark.parametrize("n", MIXED4)
@@ -581,7 +583,10 @@ def test_random_large_smooth_lengths(gdsp, oracle):
 
 @pytest.mark.parametrize("n,kind", [(810, 5), (1001, 5), (4095, 5), (4320, 5), (5400, 5),
                                     (6144, 5), (7000, 5), (7680, 5), (8190, 5), (6561, 5),
-                                    (7290, 5), (4802, 5), (7938, 5), (8191, 3)])
+                                    (7290, 5), (4802, 5), (7938, 5), (8191, 3),
+                                    # radices 17, 19, 23 (runtime-compiled lists only)
+                                    (323, 5), (529, 5), (4352, 5), (7600, 5), (6900, 5),
+                                    (7429, 5)])
 def test_jit_specialisations(gdsp, oracle, n, kind):
     # smooth lengths without a compiled specialisation get one compiled at
     # plan creation (mixed_jit.hip, hipRTC); above 4096 they would otherwise
