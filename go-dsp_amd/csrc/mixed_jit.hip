@@ -41,8 +41,9 @@ struct JitCol {  // colfixed_kernel for one column length
 
 namespace {
 
-// the radices dft_any has (mixed_core.hpp); 17, 19 and 23 only here
-constexpr int kRadices[] = {25, 23, 20, 19, 17, 16, 15, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2};
+// the radices dft_any has (mixed_core.hpp); 17 .. 31 only here (31 is also
+// the largest a 5-bit MixedDesc code holds)
+constexpr int kRadices[] = {31, 29, 25, 23, 20, 19, 17, 16, 15, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2};
 
 // FixedGeo (mixed_fixed.hpp) on the host: threads per transform, transforms
 // per workgroup

@@ -21,7 +21,9 @@ g = importlib.import_module("go-dsp_amd")
 D = importlib.import_module("go-dsp_amd.device")
 
 
-PRIMES = (2, 3, 5, 7, 11, 13, 17, 19, 23) if os.environ.get("SWEEP23") else (2, 3, 5, 7, 11, 13)
+# SWEEP23=1: the lengths whose largest prime factor is 17..31 instead
+BIG = (17, 19, 23, 29, 31)
+PRIMES = (2, 3, 5, 7, 11, 13) + (BIG if os.environ.get("SWEEP23") else ())
 
 
 def smooth(n):
@@ -41,7 +43,7 @@ if __name__ == "__main__":
     worst, count, kinds, t_build = 0.0, 0, {}, 0.0
     for n in range(lo, hi + 1):
         if not smooth(n) or n & (n - 1) == 0 or (os.environ.get("SWEEP23") and all(
-                n % p for p in (17, 19, 23))):
+                n % p for p in BIG)):
             continue
         t0 = time.perf_counter()
         k = D.plan(n).kind

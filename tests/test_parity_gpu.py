@@ -586,7 +586,7 @@ def test_random_large_smooth_lengths(gdsp, oracle):
                                     (7290, 5), (4802, 5), (7938, 5), (8191, 3),
                                     # radices 17, 19, 23 (runtime-compiled lists only)
                                     (323, 5), (529, 5), (4352, 5), (7600, 5), (6900, 5),
-                                    (7429, 5)])
+                                    (7429, 5), (899, 5), (7936, 5), (6293, 5)])
 def test_jit_specialisations(gdsp, oracle, n, kind):
     # smooth lengths without a compiled specialisation get one compiled at
     # plan creation (mixed_jit.hip, hipRTC); above 4096 they would otherwise
