@@ -446,15 +446,19 @@ int build_mixed(int dev, int64_t n, const std::vector<int> &rad, gdsp_plan *p) {
   return make_mixed_desc(dev, n, gen, p->md_gen, &p->tw_gen);
 }
 
-// Lengths one kernel transforms per row: powers of 2 up to the LDS limit, or
-// the mixed-radix set.
+// Lengths one kernel transforms per row: powers of 2 up to the LDS limit,
+// the mixed-radix set, and every other m <= 8192 through the fused chirp-z
+// kernel (M = NextPowerOf2(2m - 1) <= 16384), so a length with a large prime
+// factor but a smooth cofactor (8191 * 64) still gets a three-pass four-step
+// instead of the composed chirp-z over 2n-point rows.
 bool one_kernel_len(int64_t m) {
   if (m < 2) return false;
   if (is_pow2(m)) return ilog2(m) <= gdsp::kMaxLdsLog2;
   std::vector<int> rad;
   if (mixed_radices(m, rad)) return true;
-  int jr[5], jnp = 0;  // a runtime-compiled specialisation (else the sub-plan takes Bluestein)
-  return gdsp::jit_enabled() && gdsp::jit_radices((int)m, jr, &jnp);
+  int jr[5], jnp = 0;  // a runtime-compiled specialisation
+  if (gdsp::jit_enabled() && gdsp::jit_radices((int)m, jr, &jnp)) return true;
+  return next_pow2_ref(2 * m - 1) <= ((int64_t)1 << gdsp::kMaxLdsLog2);
 }
 
 // n = n1 * n2 with both factors one-kernel lengths, n1 <= n2 as balanced as

@@ -292,6 +292,7 @@ def test_plan_kinds(gdsp):
     assert D.plan(5000).kind == 5  # a compiled specialisation above 4096 (25*25*8)
     assert D.plan(5400).kind == 5  # smooth, no compiled specialisation: hipRTC-compiled one
     assert D.plan(8209).kind == 4  # prime, M = 32768: composed Bluestein
+    assert D.plan(8191 * 64).kind == 6  # power-of-2 columns, fused chirp-z rows of 8191
     assert D.plan(3000, chirpz=True).kind == 3
     assert D.plan(10000, chirpz=True).kind == 4
     assert D.plan(4096, chirpz=True).kind == 3  # forced chirp-z on a power of 2
@@ -357,7 +358,10 @@ MIXED4 = [4100, 5000, 6000, 8190, 10000, 44100, 48000, 3 << 16, 8209, 100000, 10
           # (343 x 2401) and 4 columns (630 x 7875): three passes
           390625, 600000, 1001000, 1594323, 823543, 4961250,
           # 17 * 2^16: power-of-2 columns, rows of 2176 = 17 * 128
-          1114112]
+          1114112,
+          # rows through the fused chirp-z kernel: 64 x 8191, 100 x 4099,
+          # 143 x 1009, 91 x 7919
+          524224, 409900, 144287, 720629]
 
 
 @pytest.mark.parametrize("n", MIXED4)
