@@ -566,6 +566,21 @@ def test_random_smooth_lengths(gdsp, oracle):
     assert {5, 6} <= kinds, kinds
 
 
+def test_random_lengths_beyond_one_kernel(gdsp, oracle):
+    # seeded arbitrary lengths in (8192, 300000]: three-pass splits with
+    # mixed-radix or chirp-z rows, the five-pass form and the composed
+    # chirp-z (a prime factor above 8192), forward and inverse
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    rng = np.random.default_rng(424242)
+    kinds = set()
+    for n in sorted(set(int(v) for v in rng.integers(8193, 300001, 14))):
+        x = rng.uniform(-1, 1, (1, n)) + 1j * rng.uniform(-1, 1, (1, n))
+        assert row_nrel(gdsp.fft.FFTBatch(x), oracle.fft_rows(x)) < TOL, n
+        assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL, n
+        kinds.add(D.plan(n).kind)
+    assert {4, 6} <= kinds, kinds
+
+
 def test_random_large_smooth_lengths(gdsp, oracle):
     # seeded random 13-smooth lengths in (200000, 2000000]: the three-pass
     # column splits (power-of-2, single-radix and runtime-compiled mixed-radix
