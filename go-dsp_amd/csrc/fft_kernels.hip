@@ -611,6 +611,55 @@ __global__ __launch_bounds__(256) void transpose_kernel(const cd *__restrict__ i
   }
 }
 
+// The final transpose of a composed chirp-z FFT_M (M = rows * cols, the
+// four-step's output order), with the chirp-z step that follows folded in.
+// Output index k = c * rows + r of matrix b:
+//   mode 1: out[b*M + k] = conj(v * bhat[k])          (between the two FFTs)
+//   mode 2: out[b*n + k] = conj(v) * chirp[k], k < n   (the result; an
+//           inverse conjugates and scales it)
+// Tiles as transpose_kernel<32, 64>.
+__global__ __launch_bounds__(256) void transpose_blu_kernel(const cd *__restrict__ in,
+                                                            cd *__restrict__ out, int64_t rows,
+                                                            int64_t cols, int64_t batch, int mode,
+                                                            int64_t n, const cd *__restrict__ tab,
+                                                            int inv, double scale) {
+  constexpr int TR = 32, TC = 64, LY = 256 / TC, SY = 256 / TR;
+  __shared__ cd tile[TR][TC + 1];
+  const int64_t M = rows * cols;
+  const int64_t tiles_c = (cols + TC - 1) / TC, tiles_r = (rows + TR - 1) / TR;
+  const int64_t per = tiles_c * tiles_r;
+  const int lx = threadIdx.x % TC, ly = threadIdx.x / TC;
+  const int sx = threadIdx.x % TR, sy = threadIdx.x / TR;
+  for (int64_t tg = blockIdx.x; tg < per * batch; tg += gridDim.x) {
+    const int64_t b = tg / per, tb = tg - b * per;
+    const int64_t tr = tb / tiles_c, tc = tb - tr * tiles_c;
+    const cd *src = in + b * M;
+#pragma unroll
+    for (int i = 0; i < TR; i += LY) {
+      const int64_t r = tr * TR + ly + i, c = tc * TC + lx;
+      if (r < rows && c < cols) tile[ly + i][lx] = ld_nt(&src[r * cols + c]);
+    }
+    __syncthreads();
+    const int64_t r = tr * TR + sx;
+#pragma unroll
+    for (int i = 0; i < TC; i += SY) {
+      const int64_t c = tc * TC + sy + i;
+      if (r < rows && c < cols) {
+        const int64_t k = c * rows + r;
+        const cd v = tile[sx][sy + i];
+        if (mode == 1) {
+          st_nt(&out[b * M + k], conjg(cmul(v, tab[k])));
+        } else if (k < n) {
+          cd y = cmul(conjg(v), tab[k]);
+          if (inv) y = {y.x * scale, -y.y * scale};
+          st_nt(&out[b * n + k], y);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 __global__ void real_to_complex_kernel(const double *__restrict__ in, cd *__restrict__ out,
                                        int64_t count) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1034,6 +1083,19 @@ hipError_t launch_transpose(const cd *in, cd *out, int64_t rows, int64_t cols, h
   else
     hipLaunchKernelGGL((transpose_kernel<32, 64>), dim3(nb), dim3(256), 0, s, in, out, rows, cols,
                        batch, (int)conj_scale, scale, tw, twn, (int)tw_conj);
+  return hipGetLastError();
+}
+
+hipError_t launch_transpose_blu(const cd *in, cd *out, int64_t rows, int64_t cols, int64_t batch,
+                                int mode, int64_t n, const cd *tab, bool inv, double scale,
+                                hipStream_t s) {
+  if (batch < 1 || batch > 65535 || (mode != 1 && mode != 2)) return hipErrorInvalidValue;
+  if (mode == 2 && n > rows * cols) return hipErrorInvalidValue;
+  const int64_t tiles = ((rows + 31) / 32) * ((cols + 63) / 64) * batch;
+  const int64_t cap = 256 * 32;
+  const unsigned nb = (unsigned)(tiles < cap ? tiles : cap);
+  hipLaunchKernelGGL(transpose_blu_kernel, dim3(nb), dim3(256), 0, s, in, out, rows, cols, batch,
+                     mode, n, tab, (int)inv, scale);
   return hipGetLastError();
 }
 

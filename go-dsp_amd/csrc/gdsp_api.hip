@@ -809,12 +809,59 @@ int exec_mixed4(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool
   return GDSP_OK;
 }
 
+// log2 of the column and row lengths exec_fourstep uses for a 2^ln FFT
+void fourstep_split(int ln, int *lr, int *lc) {
+  if (ln - 13 >= gdsp::kColMinLog2 && ln - 13 <= gdsp::kColMaxLog2) {
+    *lc = 13;
+    *lr = ln - 13;
+  } else if (ln - 13 < gdsp::kColMinLog2) {
+    *lr = gdsp::kColMinLog2;
+    *lc = ln - *lr;
+  } else {
+    *lr = gdsp::kColMaxLog2;
+    *lc = ln - *lr;  // rows longer than 8192 recurse
+  }
+}
+
 int exec_bluestein_composed(const gdsp_plan *p, const cd *in, cd *out, int64_t batch, bool inv,
                             hipStream_t s) {
   DevBuf a;
   STCHK(a.alloc((size_t)batch * (size_t)p->m * sizeof(cd), s, SLOT_BLU));
   cd *da = (cd *)a.p;
   HIPCHK(gdsp::launch_chirp_premul(in, da, p->n, p->m, batch, p->chirp, inv, s));
+  int lr = 0, lc = 0;
+  fourstep_split(p->log2m, &lr, &lc);
+  static const bool unfused = getenv("GDSP_BLU_UNFUSED") != nullptr;
+  if (!unfused && lc <= 13 && p->mplan->kind == KIND_GLOBAL) {
+    // both FFT_M as exec_fourstep's column tiles + rows, each final
+    // transpose carrying the chirp-z step after it: conj(A * bhat) into da,
+    // then conj(r) * chirp into out (two passes over M fewer)
+    const int64_t M = p->m, R = (int64_t)1 << lr, C = (int64_t)1 << lc;
+    gdsp_plan *pr = nullptr, *pcol = nullptr;
+    STCHK(get_plan(R, &pr));
+    STCHK(get_plan(C, &pcol));
+    DevBuf work;
+    STCHK(work.alloc((size_t)batch * (size_t)M * sizeof(cd), s, SLOT_FS0));
+    cd *w = (cd *)work.p;
+    for (int pass = 1; pass <= 2; ++pass) {
+      for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+        const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+        HIPCHK(gdsp::launch_colfft(lr, false, 2, false, da + b0 * M, w + b0 * M, C, 1, 0, 1, 0, 1,
+                                   pr->tw, p->mplan->tw, p->log2m, 1.0, nb, M, s));
+      }
+      STCHK(exec_plan_depth(pcol, w, w, batch * R, false, gdsp::LOAD_COMPLEX, s, 1));
+      for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+        const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+        if (pass == 1)
+          HIPCHK(gdsp::launch_transpose_blu(w + b0 * M, da + b0 * M, R, C, nb, 1, p->n, p->bhat,
+                                            false, 1.0, s));
+        else
+          HIPCHK(gdsp::launch_transpose_blu(w + b0 * M, out + b0 * p->n, R, C, nb, 2, p->n,
+                                            p->chirp, inv, 1.0 / (double)p->n, s));
+      }
+    }
+    return GDSP_OK;
+  }
   STCHK(exec_plan(p->mplan, da, da, batch, false, gdsp::LOAD_COMPLEX, s));
   HIPCHK(gdsp::launch_bhat_mul_conj(da, p->m, batch, p->bhat, s));
   STCHK(exec_plan(p->mplan, da, da, batch, false, gdsp::LOAD_COMPLEX, s));

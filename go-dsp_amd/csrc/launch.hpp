@@ -108,6 +108,12 @@ hipError_t launch_colfft(int log2l, bool conj_in, int twiddle, bool conj_scale_o
 hipError_t launch_transpose(const cd *in, cd *out, int64_t rows, int64_t cols, hipStream_t s,
                             int64_t batch = 1, bool conj_scale = false, double scale = 1.0,
                             const cd *tw = nullptr, int64_t twn = 0, bool tw_conj = false);
+// the final transpose of a composed chirp-z FFT_M with the next chirp-z step
+// folded in (fft_kernels.hip transpose_blu_kernel): mode 1 conj(v * bhat),
+// mode 2 the result rows of n
+hipError_t launch_transpose_blu(const cd *in, cd *out, int64_t rows, int64_t cols, int64_t batch,
+                                int mode, int64_t n, const cd *tab, bool inv, double scale,
+                                hipStream_t s);
 hipError_t launch_real_to_complex(const double *in, cd *out, int64_t count, hipStream_t s);
 hipError_t launch_chirp_premul(const cd *in, cd *a, int64_t n, int64_t m, int64_t batch,
                                const cd *chirp, bool conj_in, hipStream_t s);
