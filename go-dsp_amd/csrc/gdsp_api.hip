@@ -592,7 +592,27 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   p->m = next_pow2_ref(2 * n - 1);
   p->log2m = ilog2(p->m);
   p->kind = p->log2m <= gdsp::kMaxLdsLog2 ? KIND_BLUESTEIN : KIND_BLUESTEIN_COMPOSED;
-  STCHK(get_plan_locked(dev, p->m, &p->mplan));
+  if (p->kind == KIND_BLUESTEIN_COMPOSED && !chirpz && !getenv("GDSP_CHIRPZ_POW2")) {
+    // The composed chirp-z is HBM-bound, so its cost follows M: take the
+    // smallest M >= 2n - 1 (below 0.9 of the power of 2) with a three-pass
+    // split (power-of-2 or single-radix columns, one-kernel rows) instead of
+    // bluestein.go:70's power of 2; the convolution, hence the DFT, is the
+    // same. The forced chirp-z plan keeps the reference's M.
+    for (int64_t m = 2 * n - 1; m <= (p->m * 9) / 10; ++m) {
+      int64_t r = 0, c = 0;
+      if (pow2col_split(m, r, c) || radixcol_split(m, r, c)) {
+        gdsp_plan *mp = nullptr;
+        if (get_plan_locked(dev, m, &mp) == GDSP_OK && mp->kind == KIND_MIXED4 &&
+            (mp->pow2col || mp->radixcol)) {
+          p->m = m;
+          p->log2m = 0;
+          p->mplan = mp;
+        }
+        break;
+      }
+    }
+  }
+  if (!p->mplan) STCHK(get_plan_locked(dev, p->m, &p->mplan));
   std::vector<cd> w((size_t)n), chirp((size_t)n), b((size_t)p->m, cd{0.0, 0.0});
   for (int64_t k = 0; k < n; ++k) {
     double sn = 0.0, cs = 1.0;
@@ -746,6 +766,26 @@ int exec_fourstep(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bo
 //   e  transpose -> X (N2 x N1), X[k1 + N1*k2] = Z[k1][k2] (out)
 // Inverse: inverse sub-transforms (1/N1 * 1/N2 = 1/N) and conj(W).
 // The reference runs these lengths through Bluestein (fft/bluestein.go).
+// Column pass (conj in for an inverse) and rows of a three-pass mixed
+// four-step plan, src -> w; the R x C -> C x R transpose is left to the caller.
+int mixed4_col_rows(const gdsp_plan *p, const cd *src, cd *w, int64_t batch, bool inv,
+                    hipStream_t s) {
+  const int64_t N = p->n, N1 = p->n1, N2 = p->n2;
+  const int lr = p->pow2col ? ilog2(N1) : 0;
+  for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+    const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+    if (p->mixcol)
+      HIPCHK(gdsp::jit_launch_col(p->mixcol, inv, src + b0 * N, w + b0 * N, N2, N, nb, p->p1->tw,
+                                  p->tw, s));
+    else if (p->radixcol)
+      HIPCHK(gdsp::launch_colradix((int)N1, inv, src + b0 * N, w + b0 * N, N2, N, nb, p->tw, s));
+    else
+      HIPCHK(gdsp::launch_colfft(lr, inv, 2, false, src + b0 * N, w + b0 * N, N2, 1, 0, 1, 0, 1,
+                                 p->p1->tw, p->tw, 0, 1.0, nb, N, s, N));
+  }
+  return exec_plan(p->p2, w, w, batch * N1, false, gdsp::LOAD_COMPLEX, s);
+}
+
 int exec_mixed4(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
                 hipStream_t s) {
   const int64_t N = p->n, N1 = p->n1, N2 = p->n2;
@@ -753,7 +793,6 @@ int exec_mixed4(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool
     // as exec_fourstep with R = N1 (power of 2) and C = N2 (any one-kernel
     // length): column DFT_R on row-segment tiles times W_N^(col*k1) (table
     // index mod N), rows DFT_C, conj/scale-fused transpose R x C -> C x R
-    const int lr = p->pow2col ? ilog2(N1) : 0;
     DevBuf work;
     STCHK(work.alloc((size_t)batch * (size_t)N * sizeof(cd), s, SLOT_MX0));
     cd *w = (cd *)work.p;
@@ -762,18 +801,7 @@ int exec_mixed4(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool
       HIPCHK(gdsp::launch_real_to_complex((const double *)in, w, batch * N, s));
       src = w;
     }
-    for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
-      const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
-      if (p->mixcol)
-        HIPCHK(gdsp::jit_launch_col(p->mixcol, inv, src + b0 * N, w + b0 * N, N2, N, nb,
-                                    p->p1->tw, p->tw, s));
-      else if (p->radixcol)
-        HIPCHK(gdsp::launch_colradix((int)N1, inv, src + b0 * N, w + b0 * N, N2, N, nb, p->tw, s));
-      else
-        HIPCHK(gdsp::launch_colfft(lr, inv, 2, false, src + b0 * N, w + b0 * N, N2, 1, 0, 1, 0, 1,
-                                   p->p1->tw, p->tw, 0, 1.0, nb, N, s, N));
-    }
-    STCHK(exec_plan(p->p2, w, w, batch * N1, false, gdsp::LOAD_COMPLEX, s));
+    STCHK(mixed4_col_rows(p, src, w, batch, inv, s));
     for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
       const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
       HIPCHK(gdsp::launch_transpose(w + b0 * N, out + b0 * N, N1, N2, s, nb, inv,
@@ -829,9 +857,30 @@ int exec_bluestein_composed(const gdsp_plan *p, const cd *in, cd *out, int64_t b
   STCHK(a.alloc((size_t)batch * (size_t)p->m * sizeof(cd), s, SLOT_BLU));
   cd *da = (cd *)a.p;
   HIPCHK(gdsp::launch_chirp_premul(in, da, p->n, p->m, batch, p->chirp, inv, s));
+  static const bool unfused = getenv("GDSP_BLU_UNFUSED") != nullptr;
+  const gdsp_plan *mp = p->mplan;
+  if (!unfused && mp->kind == KIND_MIXED4 && (mp->pow2col || mp->radixcol || mp->mixcol)) {
+    // smooth M (a three-pass mixed four-step): the same two fused transposes
+    const int64_t M = p->m;
+    DevBuf work;
+    STCHK(work.alloc((size_t)batch * (size_t)M * sizeof(cd), s, SLOT_MX0));
+    cd *w = (cd *)work.p;
+    for (int pass = 1; pass <= 2; ++pass) {
+      STCHK(mixed4_col_rows(mp, da, w, batch, false, s));
+      for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+        const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+        if (pass == 1)
+          HIPCHK(gdsp::launch_transpose_blu(w + b0 * M, da + b0 * M, mp->n1, mp->n2, nb, 1, p->n,
+                                            p->bhat, false, 1.0, s));
+        else
+          HIPCHK(gdsp::launch_transpose_blu(w + b0 * M, out + b0 * p->n, mp->n1, mp->n2, nb, 2,
+                                            p->n, p->chirp, inv, 1.0 / (double)p->n, s));
+      }
+    }
+    return GDSP_OK;
+  }
   int lr = 0, lc = 0;
   fourstep_split(p->log2m, &lr, &lc);
-  static const bool unfused = getenv("GDSP_BLU_UNFUSED") != nullptr;
   if (!unfused && lc <= 13 && p->mplan->kind == KIND_GLOBAL) {
     // both FFT_M as exec_fourstep's column tiles + rows, each final
     // transpose carrying the chirp-z step after it: conj(A * bhat) into da,
