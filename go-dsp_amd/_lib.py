@@ -12,7 +12,8 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libgdspfft.so")
+# GDSP_LIB: an alternate build of the same library (A/B builds in experiments)
+LIB_PATH = os.environ.get("GDSP_LIB") or os.path.join(_HERE, "lib", "libgdspfft.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gdsp_fft.h")
 
 GDSP_OK = 0
@@ -68,6 +69,14 @@ SIGNATURES = {
     "gdsp_wav_read_floats": (_I, [_P, _I64, _I, _I, _P, _I]),
     "gdsp_wav_read_floats_device": (_I, [_P, _I64, _I, _I, _P, _I, _P]),
     "gdsp_fill_uniform_device": (_I, [_P, _I64, _U64, _U64, _P]),
+    "gdsp_set_devices": (_I, [ctypes.POINTER(_I), _I]),
+    "gdsp_get_devices": (_I, [ctypes.POINTER(_I), _I]),
+    "gdsp_fft_batch_multi": (_I, [_P, _P, _I64, _I64, _I, ctypes.POINTER(_I), _I]),
+    "gdsp_pwelch_multi": (_I, [_P, _I64, _D, _I64, _I64, _I64, _P, _P, _I, _P, _P,
+                               ctypes.POINTER(_I64), ctypes.POINTER(_I), _I]),
+    "gdsp_batch_shard": (_I, [_I64, _I, _I, ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
+    "gdsp_pwelch_shard": (_I, [_I64, _I64, _I64, _I, _I, ctypes.POINTER(_I64),
+                               ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
 }
 
 _lib = None

@@ -186,6 +186,14 @@ struct Dft<32> {
   __device__ __forceinline__ static void run(cd (&a)[32]) { dft_split<8, 4>(a); }
 };
 
+// XOR-swizzled exchange slots (lds_off); -DGDSP_LDS_PAD16 restores the padded layout
+#ifndef GDSP_LDS_PAD16
+constexpr bool kLdsXor = true;
+#else
+constexpr bool kLdsXor = false;
+#endif
+__host__ __device__ constexpr int clog2(int v) { return v <= 1 ? 0 : 1 + clog2(v / 2); }
+
 // ---------------------------------------------------------------------------
 // Geometry of the one-kernel (LDS-resident) transform of N = 2^LOG2N points
 // with E = 2^LOG2E elements per thread (16 by default; 8 trades one more
@@ -201,7 +209,10 @@ struct Geo {
   static constexpr int NPE = LOG2N >= LOG2E ? LOG2N / LOG2E : 0;  // radix-E passes
   static constexpr int REM = LOG2N >= LOG2E ? LOG2N % LOG2E : LOG2N;
   static constexpr int NPASS = NPE + (REM ? 1 : 0);
-  static constexpr int STRIDE = N + N / 16;        // padded doubles per transform
+  // exchange slot layout: XOR-swizzled (lds_off) when a transform spans at
+  // least 32 threads, padded (one slot per 16 doubles) below
+  static constexpr bool XOR = T >= 32 && kLdsXor;
+  static constexpr int STRIDE = XOR ? N : N + N / 16;  // doubles per transform
   static constexpr int LDS_DOUBLES = NPASS > 1 ? TPW * STRIDE : 1;
   __host__ __device__ static constexpr int radix(int p) { return p < NPE ? EMAX : (1 << REM); }
   __host__ __device__ static constexpr int ns(int p) { return p == 0 ? 1 : ns(p - 1) * radix(p - 1); }
@@ -268,10 +279,22 @@ __device__ __forceinline__ void pass_compute(cd (&v)[E], int t, const cd *__rest
 // LDS offset of element i of a transform: padded contiguous (ILV = 0), or
 // interleaved with ILV transforms (element-major, transform-minor: the
 // column tiles of FFT2, where neighbouring lanes are neighbouring columns).
-template <int ILV>
+//
+// Conflict-free exchange layout (ILV = 0, XOR): slot i ^ ((i >> log2 E) & 15).
+// Pass 0 writes i = E*j + r for 16 consecutive j (one ds_write_b64 lane group,
+// bank (a/4) mod 32): the XOR spreads them over 16 distinct slot residues
+// mod 16; later passes write 16 contiguous slots, and every read is 32
+// contiguous slots (one ds_read_b64 group, bank (a/4) mod 64), both permuted
+// within an aligned 32-slot block. The earlier padding (i + i/16) left the
+// reads 2-way conflicted (slot 32 lands on slot 0's banks) and, at E = 32,
+// the pass-0 writes too (stride 34 = 2 mod 16): 33 % of the chirp-z kernel's
+// LDS-array cycles were bank conflicts. It needs no pad slots either.
+
+template <int ILV, int E = 16, bool XOR = false>
 __device__ __forceinline__ int lds_off(int i) {
-  if constexpr (ILV == 0) return padi(i);
-  else return i * ILV;
+  if constexpr (ILV != 0) return i * ILV;
+  else if constexpr (XOR && kLdsXor) return i ^ ((i >> clog2(E)) & 15);
+  else return padi(i);
 }
 
 template <int N, int E, int T, int R, int NS, bool SPLIT, int ILV = 0>
@@ -284,7 +307,7 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
     const int j = t + b * T;
     const int base = (j / NS) * (NS * R) + (j & (NS - 1));
 #pragma unroll
-    for (int r = 0; r < R; ++r) dst[b + r * B] = lds_off<ILV>(base + r * NS);
+    for (int r = 0; r < R; ++r) dst[b + r * B] = lds_off<ILV, E, (T >= 32)>(base + r * NS);
   }
   if (!first) __syncthreads();
   if constexpr (SPLIT) {
@@ -292,13 +315,13 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
     for (int k = 0; k < E; ++k) lre[dst[k]] = v[k].x;
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < E; ++k) v[k].x = lre[lds_off<ILV>(t + k * T)];
+    for (int k = 0; k < E; ++k) v[k].x = lre[lds_off<ILV, E, (T >= 32)>(t + k * T)];
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < E; ++k) lre[dst[k]] = v[k].y;
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < E; ++k) v[k].y = lre[lds_off<ILV>(t + k * T)];
+    for (int k = 0; k < E; ++k) v[k].y = lre[lds_off<ILV, E, (T >= 32)>(t + k * T)];
   } else {
 #pragma unroll
     for (int k = 0; k < E; ++k) {
@@ -308,7 +331,7 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < E; ++k)
-      v[k] = {lre[lds_off<ILV>(t + k * T)], lim[lds_off<ILV>(t + k * T)]};
+      v[k] = {lre[lds_off<ILV, E, (T >= 32)>(t + k * T)], lim[lds_off<ILV, E, (T >= 32)>(t + k * T)]};
   }
 }
 

@@ -18,6 +18,7 @@
 #include "fft_device.hpp"
 #include "gdsp_fft.h"
 #include "launch.hpp"
+#include "api_internal.hpp"
 
 using gdsp::cd;
 
@@ -1001,8 +1002,13 @@ int host_batch(const void *x, size_t in_elem_bytes, double *out, int64_t n, int6
     STCHK(zero_copy_get(&zc));
     memcpy(zc->host, x, in_bytes);
     char *dbase = (char *)zc->dev;
-    STCHK(exec_plan(p, dbase, (cd *)(dbase + kZeroCopyOut), batch, inv, load, s));
-    HIPCHK(hipStreamSynchronize(s));
+    const int st = exec_plan(p, dbase, (cd *)(dbase + kZeroCopyOut), batch, inv, load, s);
+    // drain even on failure: kernels already queued may still touch the
+    // mapped buffer the next call on this thread refills
+    const hipError_t se = hipStreamSynchronize(s);
+    if (st != GDSP_OK) return st;
+    if (se != hipSuccess)
+      return fail(GDSP_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(se));
     memcpy(out, zc->host + kZeroCopyOut, out_bytes);
     return GDSP_OK;
   }
@@ -1010,7 +1016,11 @@ int host_batch(const void *x, size_t in_elem_bytes, double *out, int64_t n, int6
   STCHK(din.alloc(in_bytes, s, SLOT_IN));
   STCHK(dout.alloc(out_bytes, s, SLOT_OUT));
   STCHK(copy_h2d(din.p, x, in_bytes, s));
-  STCHK(exec_plan(p, din.p, (cd *)dout.p, batch, inv, load, s));
+  const int st = exec_plan(p, din.p, (cd *)dout.p, batch, inv, load, s);
+  if (st != GDSP_OK) {
+    (void)hipStreamSynchronize(s);  // queued copies still read the staging halves
+    return st;
+  }
   STCHK(copy_d2h(out, dout.p, out_bytes, s));  // returns after the stream drained
   return GDSP_OK;
 }
@@ -1041,6 +1051,33 @@ int segment_count(int64_t lx, int64_t size, int64_t noverlap, int64_t *count) {
 }
 
 }  // namespace
+
+// Forwarders for the multi-device layer (api_internal.hpp, multi.hip).
+namespace gdsp_api {
+int set_error(int st, const std::string &msg) { return fail(st, msg); }
+hipStream_t stream_for(int dev) { return thread_stream(dev); }
+int scratch(size_t bytes, hipStream_t s, ScratchSlot slot, void **p) {
+  static const Slot map[] = {SLOT_IN, SLOT_AUX, SLOT_AUX2};
+  DevBuf b;
+  STCHK(b.alloc(bytes, s, map[slot]));
+  *p = b.p;
+  return GDSP_OK;
+}
+int h2d(void *dst, const void *src, size_t bytes, hipStream_t s) {
+  return copy_h2d(dst, src, bytes, s);
+}
+int d2h(void *dst, const void *src, size_t bytes, hipStream_t s) {
+  return copy_d2h(dst, src, bytes, s);
+}
+int batch_on_current_device(const void *x, size_t in_elem_bytes, double *out, int64_t n,
+                            int64_t batch, bool inv, int load) {
+  return host_batch(x, in_elem_bytes, out, n, batch, inv, load);
+}
+void hann(int64_t L, double *out) { hann_table(L, out); }
+int segments(int64_t lx, int64_t size, int64_t noverlap, int64_t *count) {
+  return segment_count(lx, size, noverlap, count);
+}
+}  // namespace gdsp_api
 
 // ============================================================================
 // C ABI
@@ -1092,11 +1129,19 @@ int gdsp_ifft_real(const double *x, double *out, int64_t n) {
   return host_batch(c.data(), sizeof(cd), out, n, 1, true, gdsp::LOAD_COMPLEX);
 }
 
+// Large batches are split over the library's device set (gdsp_set_devices;
+// multi.hip): parallelism stays inside the call, as in radix2.go:89-151.
 int gdsp_fft_batch(const double *x, double *out, int64_t n, int64_t batch, int inverse) {
+  if (n > 0 && gdsp_api::multi_wanted((size_t)n * (size_t)batch * sizeof(cd), batch))
+    return gdsp_api::fft_batch_multi(x, sizeof(cd), out, n, batch, inverse != 0,
+                                     gdsp::LOAD_COMPLEX, nullptr, 0);
   return host_batch(x, sizeof(cd), out, n, batch, inverse != 0, gdsp::LOAD_COMPLEX);
 }
 
 int gdsp_fft_real_batch(const double *x, double *out, int64_t n, int64_t batch) {
+  if (n > 0 && gdsp_api::multi_wanted((size_t)n * (size_t)batch * sizeof(double), batch))
+    return gdsp_api::fft_batch_multi(x, sizeof(double), out, n, batch, false, gdsp::LOAD_REAL,
+                                     nullptr, 0);
   return host_batch(x, sizeof(double), out, n, batch, false, gdsp::LOAD_REAL);
 }
 
@@ -1126,7 +1171,10 @@ int gdsp_fft2_device(const void *d_in, void *d_out, int64_t rows, int64_t cols, 
   // fft/fft.go:123-154: column pass (length rows, batch cols), then row pass
   if (rows <= 0) return fail(GDSP_ERR_EMPTY, "empty input array");
   if (cols < 0) return fail(GDSP_ERR_INVALID, "negative size");
-  if (cols == 0) return GDSP_OK;
+  // computeFFT2's row pass calls IFFT on each empty row, which panics
+  // (fft/fft.go:40, :149-151); FFT of an empty row returns it unchanged
+  if (cols == 0)
+    return inverse ? fail(GDSP_ERR_EMPTY, "IFFT of an empty slice (index out of range)") : GDSP_OK;
   hipStream_t s = (hipStream_t)stream;  // NULL = the null stream (HIP convention)
   int dev = 0;
   STCHK(current_device(&dev));
@@ -1257,7 +1305,10 @@ static int fft2_host(const double *x, bool real_in, double *out, int64_t rows, i
                      int inverse) {
   if (rows <= 0) return fail(GDSP_ERR_EMPTY, "empty input array");
   if (cols < 0) return fail(GDSP_ERR_INVALID, "negative size");
-  if (cols == 0) return GDSP_OK;
+  // computeFFT2's row pass calls IFFT on each empty row, which panics
+  // (fft/fft.go:40, :149-151); FFT of an empty row returns it unchanged
+  if (cols == 0)
+    return inverse ? fail(GDSP_ERR_EMPTY, "IFFT of an empty slice (index out of range)") : GDSP_OK;
   int dev = 0;
   STCHK(current_device(&dev));
   hipStream_t s = thread_stream(dev);
@@ -1526,6 +1577,9 @@ int gdsp_pwelch(const double *x, int64_t n, double fs, int64_t nfft, int64_t pad
     hann_table(nfft, hnfft.data());
     win_nfft = hnfft.data();
   }
+  if (nsegs >= 2 && gdsp_api::multi_wanted((size_t)n * sizeof(double), nsegs))
+    return gdsp_api::pwelch_multi(x, n, fs, nfft, pad, noverlap, win_seg, win_nfft, scale_off, pxx,
+                                  freqs, lp_out, nullptr, 0);
   std::vector<double> acc((size_t)flen, 0.0);
   if (nsegs > 0) {
     int dev = 0;

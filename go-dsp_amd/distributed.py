@@ -113,7 +113,7 @@ def pwelch(x_local, Fs: float, o: spectral.PwelchOptions, shard: PwelchShard, gr
         acc = torch.zeros(flen, dtype=torch.float64, device=dev)
         if shard.seg_hi > shard.seg_lo:
             (accumulate or gpu_accumulate)(x_local, shard, win_seg, acc, stream)
-        if dist.is_initialized() and dist.get_world_size(group) > 1:
+        if dist.is_initialized():  # world size 1 included: the same RCCL path
             if acc.is_cuda and dist.get_backend(group) != "nccl":
                 acc = acc.cpu()  # gloo (rehearsal of the N>1 path): reduce a host copy
             dist.all_reduce(acc, group=group)
@@ -164,7 +164,7 @@ def fft2_sharded(x_local, rows_total: int, inverse: bool = False, group=None, st
     ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
     with ctx:
         y = row_fft(x_local.contiguous())
-        if W == 1:
+        if not dist.is_initialized():
             return col_fft(y)
         rows = [shard_range(rows_total, W, q) for q in range(W)]
         cols = [shard_range(C, W, q) for q in range(W)]

@@ -166,3 +166,52 @@ def EnsureRadix2Factors(input_len: int) -> None:
     """fft.EnsureRadix2Factors — fft/radix2.go:35-37: pre-build the device plan
     (twiddle table, and for non-powers of 2 the Bluestein tables)."""
     check(lib().gdsp_ensure_plan(int(input_len)), "EnsureRadix2Factors")
+
+
+# ---- multi-device (include/gdsp_fft.h "multi-device") ---------------------
+# The reference hides its parallelism inside each call (radix2.go:89-151);
+# these select and use the GPUs of the node the same way.
+
+def _dev_array(devices):
+    import ctypes
+    if devices is None:
+        return None, 0
+    ids = [int(d) for d in devices]
+    return (ctypes.c_int * len(ids))(*ids), len(ids)
+
+
+def SetDevices(devices=None) -> None:
+    """Device set of the host-pointer calls (gdsp_set_devices): large
+    FFTBatch / FFTRealBatch / spectral.Pwelch calls split over it. None or []
+    restores the default (every visible device, or GDSP_DEVICES)."""
+    arr, n = _dev_array(devices or [])
+    check(lib().gdsp_set_devices(arr, n), "SetDevices")
+
+
+def Devices() -> list[int]:
+    """The current device set (gdsp_get_devices); [] without a GPU."""
+    import ctypes
+    n = int(lib().gdsp_get_devices(None, 0))
+    arr = (ctypes.c_int * max(n, 1))()
+    n = int(lib().gdsp_get_devices(arr, n))
+    return list(arr[:n])
+
+
+def FFTBatchMulti(x, inverse: bool = False, devices=None) -> np.ndarray:
+    """FFTBatch split over `devices` (None: the device set): contiguous row
+    shards, one per device, no collective (gdsp_fft_batch_multi)."""
+    x = np.ascontiguousarray(np.asarray(x, dtype=np.complex128))
+    if x.ndim != 2:
+        raise ValueError("FFTBatchMulti expects a 2-D (batch, n) array")
+    out = np.empty_like(x)
+    arr, n = _dev_array(devices)
+    check(lib().gdsp_fft_batch_multi(_p(x), _p(out), x.shape[1], x.shape[0], int(inverse),
+                                     arr, n), "FFTBatchMulti")
+    return out
+
+
+def batch_shard(batch: int, ndev: int, i: int) -> tuple[int, int]:
+    """Rows [lo, hi) of shard i of ndev (gdsp_batch_shard; host arithmetic)."""
+    lo, hi = _lib._I64(0), _lib._I64(0)
+    check(lib().gdsp_batch_shard(int(batch), int(ndev), int(i), lo, hi), "batch_shard")
+    return lo.value, hi.value

@@ -273,6 +273,27 @@ inline dsputils::Matrix fftn(const dsputils::Matrix &m, int inverse) {
 inline dsputils::Matrix FFTN(const dsputils::Matrix &m) { return fftn(m, 0); }
 inline dsputils::Matrix IFFTN(const dsputils::Matrix &m) { return fftn(m, 1); }
 
+// Multi-device (gdsp_fft.h "multi-device"): the GPUs large host calls split over.
+inline void SetDevices(const std::vector<int> &devices) {
+  check(gdsp_set_devices(devices.empty() ? nullptr : devices.data(), (int)devices.size()),
+        "SetDevices");
+}
+inline std::vector<int> Devices() {
+  std::vector<int> d((size_t)std::max(gdsp_get_devices(nullptr, 0), 0));
+  d.resize((size_t)gdsp_get_devices(d.data(), (int)d.size()));
+  return d;
+}
+// FFTBatch split over `devices` (empty: the device set), one row shard each.
+inline std::vector<complex> FFTBatchMulti(const std::vector<complex> &x, size_t n,
+                                          bool inverse = false,
+                                          const std::vector<int> &devices = {}) {
+  std::vector<complex> r(x.size());
+  check(gdsp_fft_batch_multi(cp(x), mp(r), (int64_t)n, n ? (int64_t)(x.size() / n) : 0, inverse,
+                             devices.empty() ? nullptr : devices.data(), (int)devices.size()),
+        "FFTBatchMulti");
+  return r;
+}
+
 inline void SetWorkerPoolSize(int n) { gdsp_set_worker_pool_size(n); }  // fft.go:95-101
 inline void EnsureRadix2Factors(int input_len) {                        // radix2.go:35-37
   check(gdsp_ensure_plan(input_len), "EnsureRadix2Factors");
@@ -372,6 +393,30 @@ inline std::pair<std::vector<double>, std::vector<double>> Pwelch(const std::vec
   check(gdsp_pwelch(x.data(), (int64_t)x.size(), Fs, nfft, pad, o->Noverlap, wseg.data(),
                     wnfft.data(), o->Scale_off ? 1 : 0, pxx.data(), freqs.data(), &lpo),
         "Pwelch");
+  pxx.resize((size_t)lpo);
+  freqs.resize((size_t)lpo);
+  return {pxx, freqs};
+}
+
+// Pwelch split over `devices` (empty: the device set): segment shards and one
+// in-process RCCL reduce of the per-bin sums (gdsp_pwelch_multi).
+inline std::pair<std::vector<double>, std::vector<double>> PwelchMulti(
+    const std::vector<double> &x, double Fs, const PwelchOptions *o,
+    const std::vector<int> &devices = {}) {
+  if (x.empty()) return {{}, {}};
+  if (!o) throw Panic(GDSP_ERR_INVALID, "invalid memory address or nil pointer dereference");
+  const int nfft = o->NFFT ? o->NFFT : 256;
+  const int pad = o->Pad ? o->Pad : nfft;
+  const window::Func wf = o->Window ? o->Window : window::Func(window::Hann);
+  const int flen = pad > nfft ? pad : nfft;
+  const auto wseg = wf(flen), wnfft = wf(nfft);
+  const int lp = pad / 2 + 1;
+  std::vector<double> pxx(lp), freqs(lp);
+  int64_t lpo = 0;
+  check(gdsp_pwelch_multi(x.data(), (int64_t)x.size(), Fs, nfft, pad, o->Noverlap, wseg.data(),
+                          wnfft.data(), o->Scale_off ? 1 : 0, pxx.data(), freqs.data(), &lpo,
+                          devices.empty() ? nullptr : devices.data(), (int)devices.size()),
+        "PwelchMulti");
   pxx.resize((size_t)lpo);
   freqs.resize((size_t)lpo);
   return {pxx, freqs};

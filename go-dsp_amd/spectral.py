@@ -84,3 +84,34 @@ def finalize(acc: np.ndarray, nsegs: int, nfft: int, pad: int, win_nfft: np.ndar
                                      float(Fs), int(scale_off), _p(pxx), _p(freqs)),
           "pwelch_finalize")
     return pxx, freqs
+
+
+def PwelchMulti(x, Fs: float, o: Optional[PwelchOptions], devices=None):
+    """spectral.Pwelch split over `devices` (None: the library's device set):
+    segment shards with their halos, per-device accumulation and one
+    in-process RCCL reduce of the per-bin sums (gdsp_pwelch_multi)."""
+    from .fft import _dev_array
+    x = np.ascontiguousarray(np.asarray(x, dtype=np.float64).reshape(-1))
+    if x.size == 0:
+        return np.zeros(0), np.zeros(0)
+    nfft, pad, noverlap, wf, scaling = resolve_options(o)
+    flen = max(pad, nfft)
+    win_seg = np.ascontiguousarray(wf(flen), dtype=np.float64)
+    win_nfft = np.ascontiguousarray(wf(nfft), dtype=np.float64)
+    lp = pad // 2 + 1
+    pxx = np.empty(lp, np.float64)
+    freqs = np.empty(lp, np.float64)
+    lpo = _lib._I64(0)
+    arr, n = _dev_array(devices)
+    check(lib().gdsp_pwelch_multi(_p(x), x.size, float(Fs), nfft, pad, noverlap, _p(win_seg),
+                                  _p(win_nfft), int(not scaling), _p(pxx), _p(freqs), lpo,
+                                  arr, n), "PwelchMulti")
+    return pxx[:lpo.value], freqs[:lpo.value]
+
+
+def pwelch_shard(nsegs: int, nfft: int, noverlap: int, ndev: int, i: int):
+    """(seg_lo, seg_hi, x_lo, x_hi) of device shard i (gdsp_pwelch_shard)."""
+    v = [_lib._I64(0) for _ in range(4)]
+    check(lib().gdsp_pwelch_shard(int(nsegs), int(nfft), int(noverlap), int(ndev), int(i), *v),
+          "pwelch_shard")
+    return tuple(a.value for a in v)

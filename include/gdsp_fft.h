@@ -148,6 +148,48 @@ int gdsp_window_hann(int64_t L, double *out);
 int gdsp_wav_read_floats(const void *in, int64_t count, int audio_format, int bits_per_sample,
                          void *out, int out_f64);
 
+/* ---- multi-device (one node's GPUs inside one call) ------------------------- */
+/* The reference keeps its parallelism inside the call (radix2FFT's goroutine
+ * pool, fft/radix2.go:89-151; Pwelch's one accumulation loop,
+ * spectral/pwelch.go:107-122). These keep that across GPUs: a batched FFT
+ * splits its rows into contiguous shards, one per device, with no
+ * collective; Pwelch splits its segments (each device reads its samples plus
+ * the nfft - stride halo) and combines the per-device accumulators with one
+ * in-process RCCL reduce (sum, float64) before the host finalises Pxx. */
+
+/* Library-wide device set used by gdsp_fft_batch, gdsp_fft_real_batch and
+ * gdsp_pwelch when a call's input is at least GDSP_MULTI_MIN_BYTES (64 MiB by
+ * default) and has at least 2 rows / segments; smaller calls stay on the
+ * calling thread's current device. ndev = 0 restores the default: every
+ * visible device (or the list in GDSP_DEVICES, e.g. "0,1,2,3"). Devices must
+ * be visible and distinct. */
+int gdsp_set_devices(const int *devices, int ndev);
+/* The current device set: writes up to cap ids, returns the set's size (0
+ * without a GPU). */
+int gdsp_get_devices(int *devices, int cap);
+
+/* fft.FFT / fft.IFFT over `batch` rows of n complex128 (as gdsp_fft_batch),
+ * always split over `devices` (NULL or ndev = 0: the library's device set);
+ * at most `batch` devices take part. Host pointers, synchronous. */
+int gdsp_fft_batch_multi(const double *x, double *out, int64_t n, int64_t batch, int inverse,
+                         const int *devices, int ndev);
+
+/* spectral.Pwelch (as gdsp_pwelch), always split over `devices` (NULL or
+ * ndev = 0: the library's device set) with the RCCL reduce of the per-bin
+ * accumulators — also for a single device. */
+int gdsp_pwelch_multi(const double *x, int64_t n, double fs, int64_t nfft, int64_t pad,
+                      int64_t noverlap, const double *win_seg, const double *win_nfft,
+                      int scale_off, double *pxx, double *freqs, int64_t *lp_out,
+                      const int *devices, int ndev);
+
+/* Shard i of ndev, as the calls above split the work: rows [*lo, *hi) of a
+ * batch; and for Pwelch, segments [*seg_lo, *seg_hi) of nsegs and the
+ * samples [*x_lo, *x_hi) they read (empty when the shard has no segment).
+ * Host arithmetic only (no GPU needed). */
+int gdsp_batch_shard(int64_t batch, int ndev, int i, int64_t *lo, int64_t *hi);
+int gdsp_pwelch_shard(int64_t nsegs, int64_t nfft, int64_t noverlap, int ndev, int i,
+                      int64_t *seg_lo, int64_t *seg_hi, int64_t *x_lo, int64_t *x_hi);
+
 /* ---- device-pointer API (stream-ordered; multi-GPU building blocks) ---------- */
 
 typedef struct gdsp_plan gdsp_plan;

@@ -123,6 +123,9 @@ int main(int argc, char **argv) {
       auto res = spectral::Pwelch(x, fs, &o);
       EXPECT(dsputils::PrettyClose(res.first, p), "Pwelch Pxx n=" << n);
       EXPECT(dsputils::PrettyClose(res.second, fr), "Pwelch freqs n=" << n);
+      // the same through the multi-device entry (RCCL reduce over the device set)
+      auto rm = spectral::PwelchMulti(x, fs, &o);
+      EXPECT(dsputils::PrettyClose(rm.first, p), "PwelchMulti Pxx n=" << n);
     } else if (kind == "SEG") {  // TestSegment, spectral_test.go:58-67
       size_t xl, nseg;
       int size, nov;
@@ -200,6 +203,8 @@ int main(int argc, char **argv) {
   auto B = fft::FFTBatch(b, 3000);
   EXPECT(dsputils::ComplexEqual(B[3000], complex(3000, 0)) && std::abs(B[3001]) < 1e-9,
          "FFTBatch Bluestein row 1");
+  auto BM = fft::FFTBatchMulti(b, 3000, false, fft::Devices());
+  EXPECT(BM == B, "FFTBatchMulti equals FFTBatch");
   std::cout << "checks " << checks << " failures " << failures << "\n";
   return failures ? 1 : 0;
 }

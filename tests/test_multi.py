@@ -1,0 +1,203 @@
+"""The multi-device layer behind the C ABI (include/gdsp_fft.h
+"multi-device", go-dsp_amd/csrc/multi.hip): the reference keeps its
+parallelism inside each call (fft/radix2.go:89-151, spectral/pwelch.go:107-122),
+and so does the drop-in across GPUs.
+
+CPU: the shard arithmetic the library uses (rows; Pwelch segments with their
+halo) at ndev 2/3/8, and that the sharded accumulation folded and finalised
+equals the single-pass reference restatement (oracle accumulator per shard).
+GPU: gdsp_fft_batch_multi / gdsp_pwelch_multi on the box's device (ndev = 1
+still runs the RCCL clique and its reduce), and the torch "nccl" branch of
+distributed.py at world size 1."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import nrel
+
+
+@pytest.mark.parametrize("ndev", [1, 2, 3, 8])
+@pytest.mark.parametrize("batch", [0, 1, 5, 7, 65536])
+def test_batch_shards_tile_rows(gdsp, ndev, batch):
+    D = __import__("importlib").import_module("go-dsp_amd.distributed")
+    prev = 0
+    for i in range(ndev):
+        lo, hi = gdsp.fft.batch_shard(batch, ndev, i)
+        assert lo == prev and hi >= lo and hi - lo in (batch // ndev, -(-batch // ndev))
+        assert (lo, hi) == D.shard_range(batch, ndev, i)
+        prev = hi
+    assert prev == batch
+
+
+PW_CASES = [
+    dict(n=50000, nfft=4096, noverlap=2048, pad=0, fs=1.0),
+    dict(n=30001, nfft=1000, noverlap=250, pad=2048, fs=3.0),
+    dict(n=3000, nfft=256, noverlap=0, pad=0, fs=2.0),
+    dict(n=100, nfft=256, noverlap=0, pad=0, fs=2.0),  # one zero-padded segment
+]
+
+
+@pytest.mark.parametrize("ndev", [2, 3, 8])
+@pytest.mark.parametrize("c", PW_CASES, ids=lambda c: f"{c['n']}-{c['nfft']}-{c['noverlap']}")
+def test_pwelch_shards_vs_oracle(gdsp, oracle, ndev, c):
+    """Segments tile [0, S); each shard's sample range is exactly what its
+    segments read; per-shard accumulators summed and finalised equal the
+    reference's one-loop Pwelch (pwelch.go:107-122)."""
+    nfft, pad, nov = c["nfft"], c["pad"] or c["nfft"], c["noverlap"]
+    rng = np.random.default_rng(3)
+    x = np.sin(2 * np.pi * 0.1234 * np.arange(c["n"])) + 0.5 * rng.standard_normal(c["n"])
+    xp = np.zeros(max(x.size, nfft))
+    xp[:x.size] = x
+    S = gdsp.spectral.segment_count(xp.size, nfft, nov)
+    stride, flen = nfft - nov, max(pad, nfft)
+    w = oracle.window("hann", flen)
+    acc = np.zeros(flen)
+    prev = 0
+    for i in range(ndev):
+        slo, shi, xlo, xhi = gdsp.spectral.pwelch_shard(S, nfft, nov, ndev, i)
+        assert slo == prev
+        prev = shi
+        if shi == slo:
+            assert xlo == xhi == 0
+            continue
+        assert (xlo, xhi) == (slo * stride, (shi - 1) * stride + nfft)
+        xl = xp[xlo:xhi]
+        for s in range(shi - slo):
+            seg = np.zeros(flen)
+            seg[:nfft] = xl[s * stride:s * stride + nfft]
+            acc += np.abs(oracle.fft_real(seg * w)) ** 2
+    assert prev == S
+    # the library's accumulators are |Z_k|^2 of packed pairs; finalize folds
+    # acc[k] + acc[F-k], which for a plain per-segment |X_k|^2 sum is 2x
+    # the one-sided value, exactly what finalize's /2 expects
+    p, f = gdsp.spectral.finalize(acc, S, nfft, pad, oracle.window("hann", nfft), c["fs"], False)
+    pr, fr = oracle.pwelch(x, c["fs"], nfft, c["pad"], nov)
+    assert nrel(p, pr) < 1e-12 and nrel(f, fr) < 1e-15
+
+
+def test_shard_queries_reject_bad_arguments(gdsp):
+    with pytest.raises(gdsp.GDSPError):
+        gdsp.fft.batch_shard(10, 0, 0)
+    with pytest.raises(gdsp.GDSPError):
+        gdsp.fft.batch_shard(10, 2, 2)
+    with pytest.raises(gdsp.GDSPError):
+        gdsp.spectral.pwelch_shard(10, 256, 256, 2, 0)  # stride 0
+
+
+def test_multi_entries_without_gpu(gdsp):
+    if gdsp.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    assert gdsp.fft.Devices() == []
+    with pytest.raises(gdsp.GDSPError) as e:
+        gdsp.fft.SetDevices([0])
+    assert e.value.status == gdsp._lib.GDSP_ERR_NO_DEVICE
+    with pytest.raises(gdsp.GDSPError) as e:
+        gdsp.fft.FFTBatchMulti(np.ones((4, 8)))
+    assert e.value.status == gdsp._lib.GDSP_ERR_NO_DEVICE
+    with pytest.raises(gdsp.GDSPError) as e:
+        gdsp.spectral.PwelchMulti(np.ones(1000), 1.0, gdsp.spectral.PwelchOptions())
+    assert e.value.status == gdsp._lib.GDSP_ERR_NO_DEVICE
+
+
+# ---- GPU -------------------------------------------------------------------
+
+@pytest.mark.gpu
+def test_device_set(gdsp):
+    n = gdsp.device_count()
+    assert gdsp.fft.Devices() == list(range(n))
+    gdsp.fft.SetDevices([0])
+    try:
+        assert gdsp.fft.Devices() == [0]
+        with pytest.raises(gdsp.GDSPError):
+            gdsp.fft.SetDevices([0, 0])
+        with pytest.raises(gdsp.GDSPError):
+            gdsp.fft.SetDevices([n])
+    finally:
+        gdsp.fft.SetDevices(None)
+    assert gdsp.fft.Devices() == list(range(n))
+
+
+@pytest.mark.gpu
+def test_fft_batch_multi_fullsize(gdsp, oracle):
+    """BASELINE config 2 (65536 x 4096) through gdsp_fft_batch_multi with
+    host buffers: sampled rows against the oracle, and the inverse."""
+    n, batch = 4096, 65536
+    x = oracle.fill_uniform(2 * n * batch, 0x5EED).view(np.complex128).reshape(batch, n)
+    y = gdsp.fft.FFTBatchMulti(x, devices=[0])
+    rows = np.r_[0:3, batch // 2, batch - 3:batch]
+    for r in rows:
+        assert nrel(y[r], oracle.fft(x[r])) < 1e-12, r
+    z = gdsp.fft.FFTBatchMulti(y[:1024], inverse=True)  # the library's device set
+    assert nrel(z, x[:1024]) < 1e-14
+    # same result as the single-device entry
+    assert np.array_equal(gdsp.fft.FFTBatch(x[:256]), y[:256])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c", [
+    dict(n=1 << 22, nfft=4096, noverlap=2048, pad=0, fs=1.0),
+    dict(n=300001, nfft=1000, noverlap=250, pad=2048, fs=3.0),
+    dict(n=100, nfft=256, noverlap=0, pad=0, fs=2.0),
+], ids=lambda c: f"{c['n']}-{c['nfft']}")
+def test_pwelch_multi_rccl_vs_oracle(gdsp, oracle, c):
+    """gdsp_pwelch_multi on one device: shard, accumulate, RCCL reduce of the
+    per-bin sums, finalise — against the reference restatement."""
+    rng = np.random.default_rng(11)
+    x = np.sin(2 * np.pi * 0.1234 * np.arange(c["n"])) + 0.5 * rng.standard_normal(c["n"])
+    o = gdsp.spectral.PwelchOptions(NFFT=c["nfft"], Noverlap=c["noverlap"], Pad=c["pad"])
+    p, f = gdsp.spectral.PwelchMulti(x, c["fs"], o, devices=[0])
+    pr, fr = oracle.pwelch(x, c["fs"], c["nfft"], c["pad"], c["noverlap"])
+    assert nrel(p, pr) < 1e-9 and nrel(f, fr) < 1e-15
+    p2, _ = gdsp.spectral.PwelchMulti(x, c["fs"], o)  # default device set
+    assert nrel(p2, p) < 1e-13
+
+
+@pytest.mark.gpu
+def test_host_calls_route_over_device_set(gdsp, oracle, monkeypatch):
+    """gdsp_fft_batch / gdsp_pwelch split calls of >= GDSP_MULTI_MIN_BYTES
+    over the device set; with one device they stay on the single path. The
+    result is the same either way."""
+    n, batch = 1024, 8192  # 128 MiB in
+    x = oracle.fill_uniform(2 * n * batch, 7).view(np.complex128).reshape(batch, n)
+    y = gdsp.fft.FFTBatch(x)
+    for r in (0, batch - 1):
+        assert nrel(y[r], oracle.fft(x[r])) < 1e-12
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.gpu
+def test_torch_nccl_world1(gdsp, oracle):
+    """The torch.distributed "nccl" (RCCL) branch of distributed.py at world
+    size 1: the Pwelch all-reduce and the FFT2 all-to-alls run on RCCL."""
+    import importlib
+
+    import torch
+    import torch.distributed as dist
+    D = importlib.import_module("go-dsp_amd.distributed")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                            world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        rng = np.random.default_rng(2)
+        x = rng.standard_normal(1 << 20)
+        sh = D.plan_pwelch(x.size, 1, 0, 4096, 0, 2048)
+        xl = torch.tensor(x[sh.sample_lo:sh.sample_hi], device="cuda:0")
+        o = gdsp.spectral.PwelchOptions(NFFT=4096, Noverlap=2048)
+        p, _ = D.pwelch(xl, 2.0, o, sh)
+        pr, _ = oracle.pwelch(x, 2.0, 4096, 0, 2048)
+        assert nrel(p, pr) < 1e-9
+        m = rng.standard_normal((256, 192)) + 1j * rng.standard_normal((256, 192))
+        y = D.fft2_sharded(torch.tensor(m, device="cuda:0"), 256)
+        torch.cuda.synchronize()
+        assert nrel(y.cpu().numpy(), oracle.fft2(m)) < 1e-12
+    finally:
+        dist.destroy_process_group()
