@@ -3,13 +3,16 @@
 "Gsamples/s + % HBM roofline, batched N=4096 complex128 FFT at 1/2/4/8 GPUs").
 
 A step = one batched transform over one HBM-resident batch of synthetic
-input (configs[1]: N = 4096 complex128 x 65536 rows per GPU). Multi-GPU: one
-process per GPU (torch.distributed.run), each rank transforms its own
-65536-row shard (weak scaling, no data-path collective: the rows are
-independent). value = samples of all ranks / max-over-ranks wall time.
+input (configs[1]: N = 4096 complex128 x 65536 rows). Multi-GPU: one process
+per GPU (torch.distributed.run); the 65536 rows are split over the ranks
+(strong scaling; no data-path collective: the rows are
+independent). value = 2^28 samples / max-over-ranks wall time; at N > 1 a
+weak-scaling figure (65536 rows per rank) is added as "weak_scaling".
 
-Other workloads (--workload): bluestein3000, fft2_8192, pwelch (the other
-BASELINE configs; pwelch uses one RCCL all-reduce of the PSD accumulators).
+The default run also times the other BASELINE configs and nests them under
+"configs": bluestein3000 and chirpz3000 (configs[2]), fft2_8192 (configs[3];
+rows sharded with two RCCL all-to-alls at N > 1) and pwelch (configs[4]; one
+RCCL all-reduce of the PSD accumulators). --workload X runs one alone.
 bluestein3000 is fft.FFT of N = 3000 through the production dispatch (the
 mixed-radix 8*5*5*5*3 kernel); chirpz3000 times the same workload through the
 reference's algorithm (forced Bluestein plan, gdsp_plan_create_chirpz).
@@ -58,104 +61,130 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="radix4096",
-                    choices=["radix4096", "bluestein3000", "chirpz3000", "fft2_8192", "fft2_dist",
-                             "pwelch", "fftn_512", "wav_decode", "fft_2p20"])
-    ap.add_argument("--batch", type=int, default=0, help="rows per GPU (0 = config default)")
+    ap.add_argument("--workload", default="default",
+                    choices=["default"] + WORKLOADS,
+                    help="default: the headline radix4096 line with the other BASELINE "
+                         "configs nested under 'configs'")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="rows in total, split over the ranks (0 = config default 65536)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
-                    help="target CPU seconds for the cpu_baseline sample (0 disables)")
+                    help="target CPU seconds for the headline cpu_baseline sample (0 disables)")
+    ap.add_argument("--config-cpu-seconds", type=float, default=5.0,
+                    help="target CPU seconds for each nested config's cpu_baseline")
     ap.add_argument("--check-rows", type=int, default=8, help="rows checked against the oracle")
     return ap.parse_args()
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+WORKLOADS = ["radix4096", "bluestein3000", "chirpz3000", "fft2_8192", "fft2_dist", "pwelch",
+             "fftn_512", "wav_decode", "fft_2p20"]
+# the BASELINE configs nested in the default line: configs[2] (production
+# dispatch and the reference's chirp-z algorithm), configs[3], configs[4]
+NESTED = ["bluestein3000", "chirpz3000", "fft2_8192", "pwelch"]
+HEADLINE_METRIC = "Gsamples/s + % HBM roofline, batched N=4096 complex128 FFT at 1/2/4/8 GPUs"
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # GDSP_DIST_BACKEND=gloo rehearses the N>1 path with several ranks on one
-    # GPU (RCCL refuses two ranks per device); production runs use nccl=RCCL
-    backend = os.environ.get("GDSP_DIST_BACKEND", "nccl")
-    if world > 1:
-        torch.cuda.set_device(local % torch.cuda.device_count())
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+class Ctx:
+    """Process-wide run context: ranks, device, stream, modules."""
+
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.args = torch, dist, args
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        # GDSP_DIST_BACKEND=gloo rehearses the N>1 path with several ranks on
+        # one GPU (RCCL refuses two ranks per device); production runs use nccl=RCCL
+        self.backend = os.environ.get("GDSP_DIST_BACKEND", "nccl")
+        if self.world > 1:
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            if self.backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group(self.backend)
         else:
-            dist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
-    gdsp = importlib.import_module("go-dsp_amd")
-    D = importlib.import_module("go-dsp_amd.device")
-    stream = torch.cuda.Stream(dev)
+            torch.cuda.set_device(0)
+        self.dev = torch.device("cuda", torch.cuda.current_device())
+        self.gdsp = importlib.import_module("go-dsp_amd")
+        self.D = importlib.import_module("go-dsp_amd.device")
+        self.Dd = importlib.import_module("go-dsp_amd.distributed")
+        self.stream = torch.cuda.Stream(self.dev)
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
 
-    w = args.workload
+
+def setup(w: str, c: Ctx, weak: bool = False) -> dict:
+    """Inputs in HBM and the step of workload w. Batched FFTs are strong
+    scaling: the 65536 rows are split over the ranks (the
+    reference's own benchmark is fixed-work, fft/fft_test.go:262-280);
+    weak=True gives every rank the full 65536 rows instead."""
+    torch, D, Dd, dev, stream, rank, world = c.torch, c.D, c.Dd, c.dev, c.stream, c.rank, c.world
     if w in ("radix4096", "bluestein3000", "chirpz3000"):
         n = 4096 if w == "radix4096" else 3000
         chirpz = w == "chirpz3000"
-        batch = args.batch or 65536
-        x = torch.empty((batch, n), dtype=torch.complex128, device=dev)
+        total = c.args.batch or 65536
+        if weak:
+            lo, hi, total = rank * total, (rank + 1) * total, total * world
+        else:
+            lo, hi = Dd.shard_range(total, world, rank)
+        x = torch.empty((hi - lo, n), dtype=torch.complex128, device=dev)
         y = torch.empty_like(x)
-        D.fill_uniform(x, SEED, offset=rank * batch * n * 2, stream=stream)
+        D.fill_uniform(x, SEED, offset=lo * n * 2, stream=stream)
         kind = D.plan(n, chirpz).kind
 
         def step():
             D.fft_batch(x, y, stream=stream, chirpz=chirpz)
 
-        samples_per_step = batch * n
-        alg_bytes = 32 * samples_per_step
         algo = {1: "Stockham radix-16 (one kernel)", 3: "Bluestein chirp-z (fused, M=8192)",
                 5: "mixed-radix Stockham 8*5*5*5*3 (one kernel)"}.get(kind, str(kind))
-        cfg = {"workload": f"fft.FFT batched complex128 N={n} x {batch} rows per GPU",
-               "n": n, "batch_per_gpu": batch, "parallelism": f"shard{world}",
-               "algorithm": algo}
         kernel = {1: "fft_lds_kernel<12>", 3: "bluestein_kernel<13>",
                   5: "fft_mixed_fixed_kernel<25,15,8>"}.get(kind, str(kind))
-        metric = "Gsamples/s + % HBM roofline, batched N=4096 complex128 FFT at 1/2/4/8 GPUs"
-    elif w == "fft2_8192":
+        return dict(step=step, x=x, y=y, total_samples=total * n, rank_samples=(hi - lo) * n,
+                    alg_bytes=32 * (hi - lo) * n, kernel=kernel, metric=HEADLINE_METRIC,
+                    scaling="weak" if weak else "strong",
+                    cfg={"workload": f"fft.FFT batched complex128 N={n} x {total} rows"
+                                     + (" per GPU" if weak else ", split over the GPUs"),
+                         "n": n, "batch_total": total, "batch_per_gpu": hi - lo,
+                         "parallelism": f"rows{world}", "algorithm": algo})
+    if w == "fft2_8192" and world == 1:
         rows = cols = 8192
         x = torch.empty((rows, cols), dtype=torch.complex128, device=dev)
         y = torch.empty_like(x)
         work = torch.empty_like(x)
-        D.fill_uniform(x, SEED, offset=rank * rows * cols * 2, stream=stream)
+        D.fill_uniform(x, SEED, stream=stream)
 
         def step():
             D.fft2(x, y, work=work, stream=stream)
 
-        samples_per_step = rows * cols
-        alg_bytes = 2 * 2 * 16 * samples_per_step
-        cfg = {"workload": "fft.FFT2 complex128 8192x8192", "rows": rows, "cols": cols,
-               "parallelism": f"replicas{world}"}
-        kernel = "fft2 (all launches)"
-        metric = "Gsamples/s, fft.FFT2 8192x8192 complex128"
-    elif w == "fft2_dist":  # one 8192^2 FFT2 with its rows sharded over the ranks (strong)
-        Dd = importlib.import_module("go-dsp_amd.distributed")
+        return dict(step=step, total_samples=rows * cols, rank_samples=rows * cols,
+                    alg_bytes=2 * 2 * 16 * rows * cols, kernel="fft2 (all launches)",
+                    metric="Gsamples/s, fft.FFT2 8192x8192 complex128", scaling="strong",
+                    cfg={"workload": "fft.FFT2 complex128 8192x8192", "rows": rows,
+                         "cols": cols, "parallelism": "rows1"})
+    if w in ("fft2_8192", "fft2_dist"):
+        # one 8192^2 FFT2 with its rows sharded over the ranks (strong)
         R = C = 8192
         lo, hi = Dd.shard_range(R, world, rank)
         x = torch.empty((hi - lo, C), dtype=torch.complex128, device=dev)
         D.fill_uniform(x, SEED, offset=lo * C * 2, stream=stream)
         result = {}
-        group = None
 
         def step():
-            result["y"] = Dd.fft2_sharded(x, R, group=group, stream=stream)
+            result["y"] = Dd.fft2_sharded(x, R, stream=stream)
 
-        samples_per_step = R * C // world
-        alg_bytes = 2 * 2 * 16 * x.numel()
-        cfg = {"workload": "fft.FFT2 complex128 8192x8192, rows sharded over the ranks "
-                           "(row FFTs, RCCL all-to-all, column FFTs, all-to-all back)",
-               "rows": R, "cols": C, "parallelism": f"rows{world}+alltoall"}
-        kernel = "fft2_sharded (all launches and both all-to-alls)"
-        metric = "Gsamples/s, fft.FFT2 8192x8192 complex128"
-    elif w == "fft_2p20":  # the reference's own BenchmarkFFT (fft/fft_test.go:262-280)
+        return dict(step=step, total_samples=R * C, rank_samples=x.numel(),
+                    alg_bytes=2 * 2 * 16 * x.numel(),
+                    kernel="fft2_sharded (all launches and both all-to-alls)",
+                    metric="Gsamples/s, fft.FFT2 8192x8192 complex128", scaling="strong",
+                    cfg={"workload": "fft.FFT2 complex128 8192x8192, rows sharded over the "
+                                     "ranks (row FFTs, RCCL all-to-all, column FFTs, "
+                                     "all-to-all back)",
+                         "rows": R, "cols": C, "parallelism": f"rows{world}+alltoall"})
+    if w == "fft_2p20":  # the reference's own BenchmarkFFT (fft/fft_test.go:262-280)
         n = 1 << 20
+        c.gdsp.fft.EnsureRadix2Factors(n)  # as BenchmarkFFT does (fft_test.go:273)
         x = torch.empty((1, n), dtype=torch.complex128, device=dev)
         y = torch.empty_like(x)
         D.fill_uniform(x, SEED, offset=rank * n * 2, stream=stream)
@@ -163,14 +192,14 @@ def main():
         def step():
             D.fft_batch(x, y, stream=stream)
 
-        samples_per_step = n
-        alg_bytes = 32 * n
-        cfg = {"workload": "fft.FFT of one N=2^20 complex128 vector (BenchmarkFFT, "
-                           "fft/fft_test.go:262-280), device-resident", "n": n, "batch": 1,
-               "parallelism": f"replicas{world}", "algorithm": "four-step (3 launches)"}
-        kernel = "four-step (colfft tile, row FFTs, transpose)"
-        metric = "Gsamples/s, fft.FFT N=2^20 (BenchmarkFFT)"
-    elif w == "fftn_512":  # fft.FFTN of a 512^3 complex128 Matrix
+        return dict(step=step, x=x, y=y, total_samples=n * world, rank_samples=n,
+                    alg_bytes=32 * n, kernel="four-step (colfft tile, row FFTs, transpose)",
+                    metric="Gsamples/s, fft.FFT N=2^20 (BenchmarkFFT)", scaling="weak",
+                    cfg={"workload": "fft.FFT of one N=2^20 complex128 vector (BenchmarkFFT, "
+                                     "fft/fft_test.go:262-280), device-resident", "n": n,
+                         "batch": 1, "parallelism": f"replicas{world}",
+                         "algorithm": "four-step (3 launches)"})
+    if w == "fftn_512":  # fft.FFTN of a 512^3 complex128 Matrix
         dims = (512, 512, 512)
         x = torch.empty(dims, dtype=torch.complex128, device=dev)
         y = torch.empty_like(x)
@@ -179,13 +208,14 @@ def main():
         def step():
             D.fftn(x, y, stream=stream)
 
-        samples_per_step = x.numel()
-        alg_bytes = 3 * 2 * 16 * x.numel()  # each axis: one read + one write
-        cfg = {"workload": "fft.FFTN complex128 512x512x512 (computeFFTN, fft.go:157-192)",
-               "dims": list(dims), "parallelism": f"replicas{world}"}
-        kernel = "fftn (all launches: rows, then two column-tile axes)"
-        metric = "Gsamples/s, fft.FFTN 512^3 complex128"
-    elif w == "wav_decode":  # wav.ReadFloats -> float64 Pwelch input
+        return dict(step=step, total_samples=x.numel() * world, rank_samples=x.numel(),
+                    alg_bytes=3 * 2 * 16 * x.numel(),  # each axis: one read + one write
+                    kernel="fftn (all launches: rows, then two column-tile axes)",
+                    metric="Gsamples/s, fft.FFTN 512^3 complex128", scaling="weak",
+                    cfg={"workload": "fft.FFTN complex128 512x512x512 (computeFFTN, "
+                                     "fft.go:157-192)", "dims": list(dims),
+                         "parallelism": f"replicas{world}"})
+    if w == "wav_decode":  # wav.ReadFloats -> float64 Pwelch input
         wav = importlib.import_module("go-dsp_amd.wav")
         count = 1 << 30
         raw = torch.empty(2 * count, dtype=torch.uint8, device=dev)
@@ -200,151 +230,181 @@ def main():
         def step():
             wav.device_floats(raw, count, 1, 16, out=y, stream=stream)
 
-        samples_per_step = count
-        alg_bytes = 10 * count  # 2 B PCM16 in, 8 B float64 out
-        cfg = {"workload": "wav.ReadFloats PCM16 -> float64 Pwelch input, 2^30 samples "
-                           "(wav.go:135-161)", "samples": count, "format": "PCM16",
-               "parallelism": f"replicas{world}"}
-        kernel = "wav_decode_vec_kernel<16, f64>"
-        metric = "Gsamples/s, wav.ReadFloats PCM16 2^30 samples"
-    else:  # pwelch: 2^30 samples total, NFFT 4096, 50 % overlap, Hann (strong scaling)
-        Dd = importlib.import_module("go-dsp_amd.distributed")
-        nfft, nov = 4096, 2048
-        total = 1 << 30
-        sh = Dd.plan_pwelch(total, world, rank, nfft, 0, nov)
-        x = torch.empty(sh.sample_hi - sh.sample_lo, dtype=torch.float64, device=dev)
-        D.fill_uniform(x, SEED, offset=sh.sample_lo, stream=stream)
-        opts = gdsp.spectral.PwelchOptions(NFFT=nfft, Noverlap=nov)
-        result = {}
+        return dict(step=step, raw=raw, y=y, total_samples=count * world, rank_samples=count,
+                    alg_bytes=10 * count,  # 2 B PCM16 in, 8 B float64 out
+                    kernel="wav_decode_vec_kernel<16, f64>", dtype="pcm16 -> f64",
+                    metric="Gsamples/s, wav.ReadFloats PCM16 2^30 samples", scaling="weak",
+                    cfg={"workload": "wav.ReadFloats PCM16 -> float64 Pwelch input, 2^30 "
+                                     "samples (wav.go:135-161)", "samples": count,
+                         "format": "PCM16", "parallelism": f"replicas{world}"})
+    # pwelch: 2^30 samples total, NFFT 4096, 50 % overlap, Hann (strong scaling)
+    nfft, nov = 4096, 2048
+    total = 1 << 30
+    sh = Dd.plan_pwelch(total, world, rank, nfft, 0, nov)
+    x = torch.empty(sh.sample_hi - sh.sample_lo, dtype=torch.float64, device=dev)
+    D.fill_uniform(x, SEED, offset=sh.sample_lo, stream=stream)
+    opts = c.gdsp.spectral.PwelchOptions(NFFT=nfft, Noverlap=nov)
+    result = {}
 
-        def step():
-            result["pxx"], _ = Dd.pwelch(x, 1.0, opts, sh, stream=stream)
+    def step():
+        result["pxx"], _ = Dd.pwelch(x, 1.0, opts, sh, stream=stream)
 
-        samples_per_step = total // world  # the stream is split over ranks
-        alg_bytes = 8 * x.numel()
-        cfg = {"workload": "spectral.Pwelch 2^30-sample stream, Hann NFFT 4096, 50% overlap",
-               "segments_total": sh.nsegs_total, "parallelism": f"segments{world}+allreduce"}
-        kernel = "pwelch_half_kernel<12>"
-        metric = "Gsamples/s, spectral.Pwelch 2^30 samples NFFT 4096 50% overlap"
+    return dict(step=step, total_samples=total, rank_samples=total // world,
+                alg_bytes=8 * x.numel(), kernel="pwelch_half_kernel<12>",
+                metric="Gsamples/s, spectral.Pwelch 2^30 samples NFFT 4096 50% overlap",
+                scaling="strong",
+                cfg={"workload": "spectral.Pwelch 2^30-sample stream, Hann NFFT 4096, 50% "
+                                 "overlap", "segments_total": sh.nsegs_total,
+                     "parallelism": f"segments{world}+allreduce"})
+
+
+def measure(wl: dict, c: Ctx) -> dict:
+    """W untimed warm-up steps, then exactly K timed steps between barrier +
+    synchronize; wall time = max over ranks. Per-step HIP events on the
+    stream the kernels run on give the average launch duration."""
+    torch, args = c.torch, c.args
     torch.cuda.synchronize()
     for _ in range(args.warmup):
-        step()
+        wl["step"]()
     torch.cuda.synchronize()
-
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    barrier()
+    c.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        starts[i].record(stream)
-        step()
-        ends[i].record(stream)
+        starts[i].record(c.stream)
+        wl["step"]()
+        ends[i].record(c.stream)
     torch.cuda.synchronize()
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
+    c.barrier()
+    elapsed = time.perf_counter() - t0
+    if c.world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64,
-                         device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                         device=c.dev if c.backend == "nccl" else "cpu")
+        c.dist.all_reduce(t, op=c.dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ev_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
-    avg_launch_s = sum(ev_ms) / len(ev_ms) / 1e3
+    return {"elapsed": elapsed, "avg_launch_s": sum(ev_ms) / len(ev_ms) / 1e3}
 
-    # parity spot check of this run's output (untimed)
-    check = None
-    if rank == 0 and args.check_rows > 0 and w in ("radix4096", "bluestein3000", "chirpz3000"):
-        sys.path.insert(0, os.path.join(REPO, "oracle"))
-        import numpy as np
-        import oracle
-        rows = np.linspace(0, y.shape[0] - 1, args.check_rows).astype(int)
-        xs = x[rows].cpu().numpy()
-        ys = y[rows].cpu().numpy()
+
+def parity(w: str, wl: dict, c: Ctx):
+    """Untimed spot check of this run's output against the oracle (rank 0)."""
+    if c.rank != 0 or c.args.check_rows <= 0:
+        return None
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+    import oracle
+    if w in ("radix4096", "bluestein3000", "chirpz3000"):
+        x, y = wl["x"], wl["y"]
+        rows = np.linspace(0, y.shape[0] - 1, c.args.check_rows).astype(int)
+        xs, ys = x[rows].cpu().numpy(), y[rows].cpu().numpy()
         ref = oracle.fft_rows(xs)
         err = max(float(np.linalg.norm(a - b) / np.linalg.norm(b)) for a, b in zip(ys, ref))
-        check = {"rows": len(rows), "max_nrel_vs_oracle": err}
-    if rank == 0 and args.check_rows > 0 and w == "fft_2p20":
-        sys.path.insert(0, os.path.join(REPO, "oracle"))
-        import numpy as np
-        import oracle
-        ref = oracle.fft(x[0].cpu().numpy())
-        got = y[0].cpu().numpy()
-        check = {"rows": 1, "max_nrel_vs_oracle": float(np.linalg.norm(got - ref) /
+        return {"rows": len(rows), "max_nrel_vs_oracle": err}
+    if w == "fft_2p20":
+        ref = oracle.fft(wl["x"][0].cpu().numpy())
+        got = wl["y"][0].cpu().numpy()
+        return {"rows": 1, "max_nrel_vs_oracle": float(np.linalg.norm(got - ref) /
                                                          np.linalg.norm(ref))}
-    if rank == 0 and args.check_rows > 0 and w == "wav_decode":
-        sys.path.insert(0, os.path.join(REPO, "oracle"))
-        import numpy as np
-        import oracle
+    if w == "wav_decode":
         m = 1 << 20
-        ref = oracle.wav_floats(raw[:2 * m].cpu().numpy().tobytes(), m, 1, 16)
-        got = y[:m].cpu().numpy()
-        check = {"samples": m, "bit_exact": bool(np.array_equal(got, ref.astype(np.float64)))}
+        ref = oracle.wav_floats(wl["raw"][:2 * m].cpu().numpy().tobytes(), m, 1, 16)
+        got = wl["y"][:m].cpu().numpy()
+        return {"samples": m, "bit_exact": bool(np.array_equal(got, ref.astype(np.float64)))}
+    return None
 
-    total_samples = samples_per_step * args.steps * world
-    value = total_samples / elapsed / 1e9
-    achieved = alg_bytes / avg_launch_s / 1e9
+
+def run(w: str, c: Ctx, weak: bool = False) -> dict:
+    """One workload: setup, timed steps, its bench-line fields."""
+    wl = setup(w, c, weak=weak)
+    m = measure(wl, c)
+    check = parity(w, wl, c)
+    elapsed, avg_launch_s, args, world = m["elapsed"], m["avg_launch_s"], c.args, c.world
+    value = wl["total_samples"] * args.steps / elapsed / 1e9
+    achieved = wl["alg_bytes"] / avg_launch_s / 1e9
     # the committed PMC / SQ summaries were taken at the N=1 full-size
     # configuration: scale them to this launch's share of that work (a rank's
     # shard at N>1, or a --batch override)
-    share = alg_bytes / PROFILED_ALG_BYTES[w]
+    share = wl["alg_bytes"] / PROFILED_ALG_BYTES[w]
     traffic = None
     pmc = os.path.join(REPO, "profiles", f"pmc_{w}.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
             t = json.load(f).get("hbm_bytes_per_launch")
         traffic = None if t is None else int(round(t * share))
-
-    fp64 = fp64_info(w, avg_launch_s, share)
-
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(w, args.cpu_seconds)
-    host_api = None
-    if rank == 0 and w == "fft_2p20":
+    out = {
+        "metric": wl["metric"],
+        "value": round(value, 3),
+        "unit": "Gsamples/s",
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "scaling": wl["scaling"],
+        "dtype": wl.get("dtype", "f64 (complex128)"),
+        "config": wl["cfg"],
+        "roofline": {"bound": "hbm", "kernel": wl["kernel"],
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                     "alg_bytes_per_launch": wl["alg_bytes"], "traffic": traffic},
+        "fp64": fp64_info(w, avg_launch_s, share),
+        "cpu_baseline": None,  # filled in by main() after every GPU measurement
+        "parity": check,
+    }
+    if c.rank == 0 and w == "fft_2p20":
         # fft.FFT on a host vector, the way BenchmarkFFT calls it: H2D +
         # transform + D2H through the C ABI's pinned staging (PCIe-inclusive;
         # reported beside value, never as value)
-        xh = x[0].cpu().numpy()
-        gdsp.fft.FFT(xh)
+        xh = wl["x"][0].cpu().numpy()
+        c.gdsp.fft.FFT(xh)
         reps = 20
         t0 = time.perf_counter()
         for _ in range(reps):
-            gdsp.fft.FFT(xh)
+            c.gdsp.fft.FFT(xh)
         dt = (time.perf_counter() - t0) / reps
-        host_api = {"ms_per_call": round(dt * 1e3, 4), "gsamples_s": round(xh.size / dt / 1e9, 4),
-                    "note": "gdsp.fft.FFT on a host numpy vector (C ABI host-pointer path, "
-                            "PCIe-inclusive)"}
+        out["host_api"] = {"ms_per_call": round(dt * 1e3, 4),
+                           "gsamples_s": round(xh.size / dt / 1e9, 4),
+                           "note": "gdsp.fft.FFT on a host numpy vector (C ABI host-pointer "
+                                   "path, PCIe-inclusive)"}
+    del wl
+    c.torch.cuda.empty_cache()
+    return out
 
-    if rank == 0:
-        line = {
-            "metric": metric,
-            "value": round(value, 3),
-            "unit": "Gsamples/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "strong" if w in ("pwelch", "fft2_dist") else "weak",
-            "vs_baseline": None,
-            "dtype": "pcm16 -> f64" if w == "wav_decode" else "f64 (complex128)",
-            "data": "synthetic (splitmix64 uniform[-1,1), generated in HBM)",
-            "config": cfg,
-            "roofline": {"bound": "hbm", "kernel": kernel,
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "avg_launch_ms": round(avg_launch_s * 1e3, 4),
-                         "alg_bytes_per_launch": alg_bytes, "traffic": traffic},
-            "fp64": fp64,
-            "cpu_baseline": cpu,
-            "parity": check,
-        }
-        if host_api is not None:
-            line["host_api"] = host_api
+
+def main():
+    args = parse()
+    c = Ctx(args)
+    w = "radix4096" if args.workload == "default" else args.workload
+    head = run(w, c)
+    line = {"metric": head["metric"], "value": head["value"], "unit": "Gsamples/s",
+            "n_gpus": c.world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": head["ms_per_step"], "higher_is_better": True,
+            "scaling": head["scaling"], "vs_baseline": None, "dtype": head["dtype"],
+            "data": "synthetic (splitmix64 uniform[-1,1), generated in HBM)"}
+    line.update({k: head[k] for k in ("config", "roofline", "fp64", "cpu_baseline", "parity")})
+    if "host_api" in head:
+        line["host_api"] = head["host_api"]
+    if c.world > 1 and w == "radix4096":
+        # secondary: every rank with its own 65536 rows (weak scaling)
+        weak = run(w, c, weak=True)
+        line["weak_scaling"] = {k: weak[k] for k in ("value", "ms_per_step", "config")}
+    if args.workload == "default":
+        line["configs"] = {}
+        for cw in NESTED:
+            r = run(cw, c)
+            r.pop("metric")
+            line["configs"][cw] = r
+    # CPU baselines last, so that no GPU measurement follows seconds of an
+    # idle GPU (rank 0 at N=1 only)
+    if c.rank == 0 and c.world == 1:
+        if args.cpu_seconds > 0:
+            line["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
+        for cw, r in line.get("configs", {}).items():
+            if args.config_cpu_seconds > 0:
+                r["cpu_baseline"] = cpu_baseline(cw, args.config_cpu_seconds)
+    if c.rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    if c.world > 1:
+        c.dist.destroy_process_group()
 
 
 def fp64_info(workload: str, launch_s: float, share: float = 1.0):
