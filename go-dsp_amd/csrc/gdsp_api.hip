@@ -1408,6 +1408,17 @@ int gdsp_plan_destroy(gdsp_plan *) { return GDSP_OK; }
 
 int gdsp_plan_kind(const gdsp_plan *plan) { return plan ? plan->kind : -1; }
 
+int gdsp_plan_info(const gdsp_plan *plan, int64_t *n, int64_t *m, int64_t *n1, int64_t *n2,
+                   int *runtime_compiled) {
+  if (!plan) return fail(GDSP_ERR_INVALID, "NULL plan");
+  if (n) *n = plan->n;
+  if (m) *m = plan->m;
+  if (n1) *n1 = plan->n1;
+  if (n2) *n2 = plan->n2;
+  if (runtime_compiled) *runtime_compiled = (plan->jit || plan->mixcol) ? 1 : 0;
+  return GDSP_OK;
+}
+
 int gdsp_fft_batch_device(const gdsp_plan *plan, const void *d_in, void *d_out, int64_t batch,
                           int inverse, void *stream) {
   if (!plan || batch < 0) return fail(GDSP_ERR_INVALID, "bad argument");

@@ -43,6 +43,12 @@ class Plan:
         else:
             check(lib().gdsp_plan_create(self.n, ctypes.byref(self.handle)), "plan_create")
         self.kind = int(lib().gdsp_plan_kind(self.handle))
+        v = [ctypes.c_int64() for _ in range(4)]
+        rc = ctypes.c_int()
+        check(lib().gdsp_plan_info(self.handle, *v, rc), "plan_info")
+        # chirp-z convolution length; four-step split; runtime-compiled?
+        self.m, self.n1, self.n2 = v[1].value, v[2].value, v[3].value
+        self.runtime_compiled = bool(rc.value)
 
 
 _plans: dict = {}

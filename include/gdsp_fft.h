@@ -210,6 +210,13 @@ int gdsp_plan_create_chirpz(int64_t n, gdsp_plan **plan);
  * n <= 4096 whose prime factors are all <= 13), 6 mixed four-step (such n
  * above 8192 = n1*n2 with one-kernel factors: transposes + row kernels). */
 int gdsp_plan_kind(const gdsp_plan *plan);
+/* Geometry of a plan (any pointer may be NULL): its length n; the chirp-z
+ * convolution length m (kinds 3 and 4; the reference's NextPowerOf2(2n-1),
+ * bluestein.go:70, or a smooth m >= 2n-1 that the composed chirp-z may
+ * choose); the four-step split n = n1*n2 (kinds 2 and 6); and whether a
+ * runtime-compiled specialisation backs it (1) or not (0). 0 where n/a. */
+int gdsp_plan_info(const gdsp_plan *plan, int64_t *n, int64_t *m, int64_t *n1, int64_t *n2,
+                   int *runtime_compiled);
 
 /* Batched C2C on device buffers: d_in/d_out hold batch*n complex128 (may
  * alias only if equal). inverse != 0 → IFFT semantics (1/n scaling). */

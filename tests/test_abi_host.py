@@ -152,3 +152,26 @@ def test_dsputils_segment_reference_table(gdsp, refvec):
     assert list(v[1]) == [4, 5, 6, 7, 8]
     with pytest.raises(gdsp.Panic, match="too many segments"):
         U.Segment(np.arange(3), 4, 0.0)
+
+
+def test_ensure_radix2_factors_without_gpu(gdsp):
+    """fft.EnsureRadix2Factors (radix2.go:35-37) builds a device plan: without a
+    GPU it fails loudly; a negative length is rejected before any device."""
+    with pytest.raises(gdsp.GDSPError) as e:
+        gdsp.fft.EnsureRadix2Factors(-1)
+    assert e.value.status == gdsp._lib.GDSP_ERR_INVALID
+    if gdsp.device_count() == 0:
+        with pytest.raises(gdsp.GDSPError) as e:
+            gdsp.fft.EnsureRadix2Factors(4096)
+        assert e.value.status == gdsp._lib.GDSP_ERR_NO_DEVICE
+
+
+def test_ifft2_of_empty_rows_panics(gdsp):
+    """computeFFT2 on rows x 0: FFT2 returns the empty rows; IFFT2 calls IFFT
+    on an empty row, which panics (fft/fft.go:40, :149-151)."""
+    L = gdsp._lib.lib()
+    buf = np.zeros(2)
+    p = buf.ctypes.data_as(gdsp._lib._P)
+    assert L.gdsp_fft2(p, p, 3, 0, 0) == gdsp._lib.GDSP_OK
+    assert L.gdsp_fft2(p, p, 3, 0, 1) == gdsp._lib.GDSP_ERR_EMPTY
+    assert L.gdsp_fft2_real(p, p, 3, 0, 1) == gdsp._lib.GDSP_ERR_EMPTY

@@ -6,11 +6,13 @@ complex128 result; the reference's known-answer tables with its own
 Float64Equal (1e-8, dsputils/compare.go:94-96) because their constants carry
 8-9 digits. Measured errors are ~1e-15 (powers of 2) and ~1e-13 (Bluestein)."""
 import math
+import os
+import subprocess
 
 import numpy as np
 import pytest
 
-from conftest import cpx, nrel, row_nrel
+from conftest import REPO, cpx, nrel, row_nrel
 
 pytestmark = pytest.mark.gpu
 
@@ -642,3 +644,56 @@ def test_chirpz_primes(gdsp, oracle, n):
     assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL
     xr = x.real.copy()
     assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [4096, 3000, 1 << 20, 8209, 5400])
+def test_ensure_radix2_factors_then_fft(gdsp, oracle, n):
+    """fft.EnsureRadix2Factors (radix2.go:35-37) pre-builds the plan the next
+    fft.FFT uses, as BenchmarkFFT does before timing (fft_test.go:273)."""
+    gdsp.fft.EnsureRadix2Factors(n)
+    gdsp.fft.EnsureRadix2Factors(n)  # idempotent
+    rng = np.random.default_rng(n)
+    x = rng.standard_normal(n) + 1j * rng.standard_normal(n)
+    assert nrel(gdsp.fft.FFT(x), oracle.fft(x)) < (1e-8 if n > 2000000 else 1e-9)
+    assert nrel(gdsp.fft.IFFT(gdsp.fft.FFT(x)), x) < 1e-13
+
+
+@pytest.mark.gpu
+def test_chirpz_convolution_length_selection():
+    """Which convolution length M the composed chirp-z takes (gdsp_plan_info),
+    and that every selectable path agrees with the oracle: by default 8209
+    and 16411 run on a smooth M (<= 0.55 of the power of 2), GDSP_CHIRPZ_POW2=1
+    keeps the reference's NextPowerOf2(2n-1) (bluestein.go:70), and
+    GDSP_BLU_UNFUSED=1 takes the unfused composition."""
+    code = r'''
+import importlib, os, sys
+sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
+import numpy as np, oracle
+g = importlib.import_module("go-dsp_amd")
+D = importlib.import_module("go-dsp_amd.device")
+import torch
+pow2 = os.environ.get("GDSP_CHIRPZ_POW2") == "1"
+rng = np.random.default_rng(8)
+for n in (8209, 16411):
+    p = D.plan(n)
+    assert p.kind == 4, (n, p.kind)
+    ref_m = 1 << (2 * n - 2).bit_length()
+    if pow2:
+        assert p.m == ref_m, (n, p.m)
+    else:
+        assert p.m & (p.m - 1) != 0 and 2 * n - 1 <= p.m <= 0.55 * ref_m, (n, p.m)
+    assert D.plan(n, chirpz=True).m == ref_m
+    x = rng.standard_normal((2, n)) + 1j * rng.standard_normal((2, n))
+    for inv in (False, True):
+        y = g.fft.FFTBatch(x, inverse=inv)
+        ref = oracle.ifft_rows(x) if inv else oracle.fft_rows(x)
+        err = max(np.linalg.norm(a - b) / np.linalg.norm(b) for a, b in zip(y, ref))
+        assert err < 1e-9, (n, inv, err)
+print("ok", os.environ.get("GDSP_CHIRPZ_POW2"), os.environ.get("GDSP_BLU_UNFUSED"))
+'''
+    for extra in ({}, {"GDSP_CHIRPZ_POW2": "1"}, {"GDSP_BLU_UNFUSED": "1"}):
+        env = dict(os.environ, REPO=REPO, **extra)
+        r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300,
+                           env=env)
+        assert r.returncode == 0 and "ok" in r.stdout, (extra, r.stdout + r.stderr[-3000:])
