@@ -38,6 +38,8 @@ SIGNATURES = {
     "gdsp_status_string": (ctypes.c_char_p, [_I]),
     "gdsp_last_error": (ctypes.c_char_p, []),
     "gdsp_version": (ctypes.c_char_p, []),
+    "gdsp_jit_stats": (_I, [ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64),
+                            ctypes.c_char_p, _I64]),
     "gdsp_device_count": (_I, []),
     "gdsp_fft": (_I, [_P, _P, _I64]),
     "gdsp_ifft": (_I, [_P, _P, _I64]),
@@ -151,3 +153,13 @@ def check(status: int, what: str = "") -> None:
 
 def device_count() -> int:
     return int(lib().gdsp_device_count())
+
+
+def jit_stats() -> dict:
+    """gdsp_jit_stats: runtime-compiled modules built / loaded from the cache /
+    failed since process start, and the last failure."""
+    b, c, f = _I64(0), _I64(0), _I64(0)
+    msg = ctypes.create_string_buffer(4096)
+    lib().gdsp_jit_stats(b, c, f, msg, len(msg))
+    return {"built": b.value, "cached": c.value, "failed": f.value,
+            "last_failure": msg.value.decode(errors="replace")}

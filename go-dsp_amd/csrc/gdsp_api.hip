@@ -22,7 +22,7 @@
 
 using gdsp::cd;
 
-#define GDSP_VERSION "gdspfft 0.1.0 (gfx950)"
+#define GDSP_VERSION "gdspfft 0.2.0 (gfx950)"
 
 namespace {
 

@@ -8,21 +8,37 @@
 // last; at most 512 threads per transform where a list allows it, else up to
 // 1024), and the same kernel templates (mixed_fixed.hpp) are compiled for it
 // with hipRTC: the batched transform (forward, inverse, real input) and the
-// fused Pwelch kernel, ~0.5-1 s once per length and process. Any failure
-// (no hipRTC, no headers, a compile error) leaves the plan on the runtime-
-// radix kernel or Bluestein, so this is a speed path only. GDSP_JIT=0
-// disables it; GDSP_JIT_INCLUDE names the header directory (default: the
-// csrc directory beside the library's lib/ directory).
+// fused Pwelch kernel, ~0.3-1.7 s once per length. Any failure (no hipRTC,
+// a compile error) leaves the plan on the runtime-radix kernel or Bluestein,
+// so this is a speed path only; failures are counted and the last one is
+// reported by gdsp_jit_stats. GDSP_JIT=0 disables it.
+//
+// Deployment: the headers the compiler needs are embedded in the library
+// (embed_headers.py at build time), so no source tree has to ship with it
+// (GDSP_JIT_INCLUDE=<dir> compiles against headers on disk instead). Built
+// code objects are kept in an on-disk cache keyed by the embedded headers'
+// hash, the GPU architecture, the compiler options and the kernel names
+// (GDSP_JIT_CACHE=<dir>, default $XDG_CACHE_HOME/gdspfft or
+// ~/.cache/gdspfft; GDSP_JIT_CACHE=off disables it), so a second process
+// creating the same plan loads it instead of compiling.
 #include <dlfcn.h>
+#include <errno.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <string>
 #include <vector>
 
+#include "gdsp_fft.h"
+#include "jit_headers.inc"
 #include "launch.hpp"
 
 namespace gdsp {
@@ -99,15 +115,112 @@ void search(int n, int depth, int maxdepth, Choice &cur, Choice &best) {
   }
 }
 
+// GDSP_JIT_INCLUDE: compile against headers on disk (empty: the embedded ones)
 std::string include_dir() {
-  if (const char *e = getenv("GDSP_JIT_INCLUDE")) return e;
-  Dl_info info;
-  if (dladdr((void *)&jit_radices, &info) && info.dli_fname) {
-    std::string p = info.dli_fname;  // .../go-dsp_amd/lib/libgdspfft.so
-    const size_t s = p.rfind('/');
-    if (s != std::string::npos) return p.substr(0, s) + "/../csrc";
+  const char *e = getenv("GDSP_JIT_INCLUDE");
+  return e ? e : "";
+}
+
+// ---- statistics (gdsp_jit_stats) ----------------------------------------------
+std::atomic<int64_t> g_built{0}, g_cached{0}, g_failed{0};
+std::mutex g_fail_mu;
+std::string g_last_failure;
+
+void record_failure(const std::string &what, const std::string &why) {
+  ++g_failed;
+  std::lock_guard<std::mutex> lk(g_fail_mu);
+  g_last_failure = what + ": " + why;
+}
+
+// ---- on-disk code-object cache -------------------------------------------------
+uint64_t fnv1a(const std::string &s, uint64_t h) {
+  for (unsigned char c : s) h = (h ^ c) * 0x100000001B3ULL;
+  return h;
+}
+
+std::string cache_dir() {
+  const char *e = getenv("GDSP_JIT_CACHE");
+  if (e && (!strcmp(e, "off") || !strcmp(e, "0"))) return "";
+  std::string d;
+  if (e && *e) d = e;
+  else if (const char *x = getenv("XDG_CACHE_HOME")) d = std::string(x) + "/gdspfft";
+  else if (const char *h = getenv("HOME")) d = std::string(h) + "/.cache/gdspfft";
+  else d = "/tmp/gdspfft-" + std::to_string((long)getuid());
+  return d;
+}
+
+bool make_dirs(const std::string &d) {
+  for (size_t p = 1; p <= d.size(); ++p) {
+    if (p == d.size() || d[p] == '/') {
+      const std::string sub = d.substr(0, p);
+      if (mkdir(sub.c_str(), 0755) != 0 && errno != EEXIST) return false;
+    }
   }
-  return "";
+  return true;
+}
+
+// cache file: "GDSPJIT1\n", the lowered (mangled) name of each kernel, then
+// the code object; written to a temporary name and renamed into place
+bool cache_load(const std::string &path, size_t nnames, std::vector<std::string> &lowered,
+                std::vector<char> &code) {
+  FILE *f = fopen(path.c_str(), "rb");
+  if (!f) return false;
+  bool ok = false;
+  char magic[9] = {};
+  if (fread(magic, 1, 9, f) == 9 && !memcmp(magic, "GDSPJIT1\n", 9)) {
+    lowered.clear();
+    ok = true;
+    for (size_t q = 0; ok && q < nnames; ++q) {
+      uint32_t len = 0;
+      ok = fread(&len, 4, 1, f) == 1 && len < 4096;
+      std::string nm(len, '\0');
+      ok = ok && fread(&nm[0], 1, len, f) == len;
+      lowered.push_back(nm);
+    }
+    uint64_t cs = 0;
+    ok = ok && fread(&cs, 8, 1, f) == 1 && cs > 0 && cs < ((uint64_t)1 << 30);
+    if (ok) {
+      code.resize(cs);
+      ok = fread(code.data(), 1, cs, f) == cs;
+    }
+  }
+  fclose(f);
+  return ok;
+}
+
+void cache_store(const std::string &dir, const std::string &path,
+                 const std::vector<std::string> &lowered, const std::vector<char> &code) {
+  if (!make_dirs(dir)) return;
+  const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
+  FILE *f = fopen(tmp.c_str(), "wb");
+  if (!f) return;
+  bool ok = fwrite("GDSPJIT1\n", 1, 9, f) == 9;
+  for (const auto &nm : lowered) {
+    const uint32_t len = (uint32_t)nm.size();
+    ok = ok && fwrite(&len, 4, 1, f) == 1 && fwrite(nm.data(), 1, len, f) == len;
+  }
+  const uint64_t cs = code.size();
+  ok = ok && fwrite(&cs, 8, 1, f) == 1 && fwrite(code.data(), 1, cs, f) == cs;
+  ok = (fclose(f) == 0) && ok;
+  if (!ok || rename(tmp.c_str(), path.c_str()) != 0) unlink(tmp.c_str());
+}
+
+bool load_functions(const std::vector<char> &code, const std::vector<std::string> &lowered,
+                    hipModule_t *mod, std::vector<hipFunction_t> &fs) {
+  *mod = nullptr;
+  if (hipModuleLoadData(mod, code.data()) != hipSuccess) {
+    *mod = nullptr;
+    return false;
+  }
+  fs.assign(lowered.size(), nullptr);
+  for (size_t q = 0; q < lowered.size(); ++q) {
+    if (hipModuleGetFunction(&fs[q], *mod, lowered[q].c_str()) != hipSuccess) {
+      (void)hipModuleUnload(*mod);
+      *mod = nullptr;
+      return false;
+    }
+  }
+  return true;
 }
 
 bool verbose() {
@@ -142,47 +255,78 @@ bool jit_radices(int n, int *rad, int *npass) {
 namespace {
 
 // Compile `names` (kernel template instances of mixed_fixed.hpp) for device
-// dev into one module; fs[q] = the kernel of names[q]. false on any failure.
+// dev into one module; fs[q] = the kernel of names[q]. Loaded from the
+// on-disk cache when an entry for the same headers, architecture, options
+// and names exists. false on any failure (counted, gdsp_jit_stats).
 bool compile_module(int dev, const std::vector<std::string> &names, const std::string &what,
                     hipModule_t *mod, std::vector<hipFunction_t> &fs) {
   hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
+  *mod = nullptr;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) {
+    record_failure(what, "hipGetDeviceProperties failed");
+    return false;
+  }
+  const std::string arch = std::string("--offload-arch=") + prop.gcnArchName;
+  const std::string incdir = include_dir();
+  const std::string inc = "-I" + (incdir.empty() ? std::string(".") : incdir);
+  const char *opts[] = {arch.c_str(), "-O3", "-std=c++17", inc.c_str()};
+  // cache key: everything the code object depends on
+  uint64_t key = fnv1a(gdsp_version(), gdsp_jit_embed::kHash);
+  key = fnv1a(arch + "|" + incdir + "|-O3 -std=c++17", key);
+  for (const auto &nm : names) key = fnv1a(nm + ";", key);
+  const std::string cdir = cache_dir();
+  char hex[17];
+  snprintf(hex, sizeof hex, "%016llx", (unsigned long long)key);
+  const std::string cpath = cdir.empty() ? "" : cdir + "/" + hex + ".co";
+  std::vector<std::string> lowered;
+  std::vector<char> code;
+  if (!cpath.empty() && cache_load(cpath, names.size(), lowered, code) &&
+      load_functions(code, lowered, mod, fs)) {
+    ++g_cached;
+    if (verbose()) fprintf(stderr, "gdsp: hipRTC %s: loaded from %s\n", what.c_str(), cpath.c_str());
+    return true;
+  }
   const char *src = "#include \"mixed_fixed.hpp\"\n";
   hiprtcProgram prog;
-  if (hiprtcCreateProgram(&prog, src, "gdsp_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+  // embedded headers unless GDSP_JIT_INCLUDE points at a directory
+  const int nh = incdir.empty() ? gdsp_jit_embed::kCount : 0;
+  if (hiprtcCreateProgram(&prog, src, "gdsp_jit.hip", nh, nh ? gdsp_jit_embed::kTexts : nullptr,
+                          nh ? gdsp_jit_embed::kNames : nullptr) != HIPRTC_SUCCESS) {
+    record_failure(what, "hiprtcCreateProgram failed");
     return false;
+  }
   for (const auto &nm : names) hiprtcAddNameExpression(prog, nm.c_str());
-  const std::string arch = std::string("--offload-arch=") + prop.gcnArchName;
-  const std::string inc = "-I" + include_dir();
-  const char *opts[] = {arch.c_str(), "-O3", "-std=c++17", inc.c_str()};
   bool ok = false;
-  *mod = nullptr;
+  std::string why;
   const hiprtcResult rc = hiprtcCompileProgram(prog, 4, opts);
   if (rc == HIPRTC_SUCCESS) {
     size_t cs = 0;
     hiprtcGetCodeSize(prog, &cs);
-    std::vector<char> code(cs);
+    code.assign(cs, 0);
     hiprtcGetCode(prog, code.data());
-    fs.assign(names.size(), nullptr);
-    ok = hipModuleLoadData(mod, code.data()) == hipSuccess;
+    lowered.clear();
+    ok = cs > 0;
     for (size_t q = 0; ok && q < names.size(); ++q) {
       const char *low = nullptr;
-      ok = hiprtcGetLoweredName(prog, names[q].c_str(), &low) == HIPRTC_SUCCESS && low &&
-           hipModuleGetFunction(&fs[q], *mod, low) == hipSuccess;
+      ok = hiprtcGetLoweredName(prog, names[q].c_str(), &low) == HIPRTC_SUCCESS && low;
+      if (ok) lowered.push_back(low);
     }
-    if (!ok && *mod) {
-      (void)hipModuleUnload(*mod);
-      *mod = nullptr;
-    }
-  } else if (verbose()) {
+    ok = ok && load_functions(code, lowered, mod, fs);
+    if (!ok) why = "the compiled module did not load";
+    if (ok && !cpath.empty()) cache_store(cdir, cpath, lowered, code);
+  } else {
     size_t ls = 0;
     hiprtcGetProgramLogSize(prog, &ls);
     std::string log(ls, '\0');
     if (ls) hiprtcGetProgramLog(prog, &log[0]);
-    fprintf(stderr, "gdsp: hipRTC %s failed (%s; %s %s):\n%s\n", what.c_str(),
-            hiprtcGetErrorString(rc), arch.c_str(), inc.c_str(), log.c_str());
+    why = std::string(hiprtcGetErrorString(rc)) + ": " + log.substr(0, 2000);
+    if (verbose())
+      fprintf(stderr, "gdsp: hipRTC %s failed (%s; %s %s):\n%s\n", what.c_str(),
+              hiprtcGetErrorString(rc), arch.c_str(), inc.c_str(), log.c_str());
   }
   hiprtcDestroyProgram(&prog);
+  if (ok) ++g_built;
+  else record_failure(what, why);
   if (verbose()) fprintf(stderr, "gdsp: hipRTC %s: %s\n", what.c_str(), ok ? "built" : "not built");
   return ok;
 }
@@ -302,3 +446,17 @@ hipError_t jit_launch_pwelch(const JitSpec *j, const double *x, int64_t nfft, in
 }
 
 }  // namespace gdsp
+
+extern "C" int gdsp_jit_stats(int64_t *built, int64_t *cached, int64_t *failed, char *last_failure,
+                              int64_t cap) {
+  if (built) *built = gdsp::g_built.load();
+  if (cached) *cached = gdsp::g_cached.load();
+  if (failed) *failed = gdsp::g_failed.load();
+  if (last_failure && cap > 0) {
+    std::lock_guard<std::mutex> lk(gdsp::g_fail_mu);
+    const size_t n = std::min<size_t>((size_t)cap - 1, gdsp::g_last_failure.size());
+    memcpy(last_failure, gdsp::g_last_failure.data(), n);
+    last_failure[n] = '\0';
+  }
+  return GDSP_OK;
+}

@@ -51,6 +51,14 @@ const char *gdsp_status_string(int status);
 const char *gdsp_last_error(void);
 /* Library version string. */
 const char *gdsp_version(void);
+/* Runtime compiler (hipRTC specialisations of smooth lengths) since process
+ * start: modules compiled, modules loaded from the on-disk code-object cache
+ * (GDSP_JIT_CACHE), and compilations that failed — each failure leaves its
+ * plan on the slower path it would have replaced, with the same results. The
+ * last failure's description is copied into last_failure (cap bytes, NUL-
+ * terminated; may be NULL). */
+int gdsp_jit_stats(int64_t *built, int64_t *cached, int64_t *failed, char *last_failure,
+                   int64_t cap);
 /* Number of visible HIP devices (0 without a GPU; never initialises a context
  * beyond hipGetDeviceCount). */
 int gdsp_device_count(void);

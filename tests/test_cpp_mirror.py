@@ -168,7 +168,47 @@ for n, kind in ((810, 5), (4320, 3), (390625, 6)):
 print("ok")
 '''
     env = dict(os.environ, GDSP_JIT_INCLUDE="/nonexistent-gdsp-headers", GDSP_JIT_VERBOSE="1",
-               REPO=REPO)
+               GDSP_JIT_CACHE="off", REPO=REPO)
+    code = code.replace('print("ok")', 'print("ok", g._lib.jit_stats())')
     r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
     assert "not built" in r.stderr, r.stderr[-2000:]
+    # the downgrade is reported, not only logged: gdsp_jit_stats
+    stats = eval(r.stdout.split("ok", 1)[1])
+    assert stats["failed"] >= 3 and stats["built"] == 0, stats
+    assert "n = 4320" in stats["last_failure"] or "L = " in stats["last_failure"], stats
+
+
+@pytest.mark.gpu
+def test_runtime_compiler_cache_across_processes(tmp_path):
+    """The hipRTC specialisations compile from headers embedded in the
+    library (no source tree needed) and land in the on-disk code-object cache:
+    a second process creating the same plans loads them and compiles nothing."""
+    code = r'''
+import importlib, os, sys
+sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
+import numpy as np, oracle
+g = importlib.import_module("go-dsp_amd")
+D = importlib.import_module("go-dsp_amd.device")
+import torch
+rng = np.random.default_rng(9)
+for n in (5400, 810):
+    p = D.plan(n)
+    assert p.kind == 5 and p.runtime_compiled, (n, p.kind)
+    x = rng.standard_normal((3, n)) + 1j * rng.standard_normal((3, n))
+    y = g.fft.FFTBatch(x)
+    err = max(np.linalg.norm(a - b) / np.linalg.norm(b) for a, b in zip(y, oracle.fft_rows(x)))
+    assert err < 1e-9, (n, err)
+print("ok", g._lib.jit_stats())
+'''
+    env = dict(os.environ, GDSP_JIT_CACHE=str(tmp_path / "cache"), REPO=REPO)
+    env.pop("GDSP_JIT_INCLUDE", None)
+    runs = []
+    for _ in range(2):
+        r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300,
+                           env=env)
+        assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr[-3000:]
+        runs.append(eval(r.stdout.split("ok", 1)[1]))
+    assert runs[0]["built"] == 2 and runs[0]["cached"] == 0 and runs[0]["failed"] == 0, runs
+    assert runs[1]["built"] == 0 and runs[1]["cached"] == 2 and runs[1]["failed"] == 0, runs
+    assert len(list((tmp_path / "cache").glob("*.co"))) == 2
