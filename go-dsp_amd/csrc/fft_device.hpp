@@ -212,7 +212,8 @@ struct Geo {
   // exchange slot layout: XOR-swizzled (lds_off) when a transform spans at
   // least 32 threads, padded (one slot per 16 doubles) below
   static constexpr bool XOR = T >= 32 && kLdsXor;
-  static constexpr int STRIDE = XOR ? N : N + N / 16;  // doubles per transform
+  // doubles per transform: room for every layout lds_off may use
+  static constexpr int STRIDE = T >= 32 ? N + N / E : N + N / 16;
   static constexpr int LDS_DOUBLES = NPASS > 1 ? TPW * STRIDE : 1;
   __host__ __device__ static constexpr int radix(int p) { return p < NPE ? EMAX : (1 << REM); }
   __host__ __device__ static constexpr int ns(int p) { return p == 0 ? 1 : ns(p - 1) * radix(p - 1); }
@@ -290,14 +291,22 @@ __device__ __forceinline__ void pass_compute(cd (&v)[E], int t, const cd *__rest
 // the pass-0 writes too (stride 34 = 2 mod 16): 33 % of the chirp-z kernel's
 // LDS-array cycles were bank conflicts. It needs no pad slots either.
 
-template <int ILV, int E = 16, bool XOR = false>
+//
+// LINEAR (padE): slot i + i / E. Pass 0's stride-E writes become stride E+1,
+// every other write and every read a contiguous run, and each address is a
+// per-thread base plus a compile-time offset (no VALU per element). At E = 32
+// it is conflict-free too; at E = 16 the 32-lane reads stay 2-way conflicted.
+// The VALU-bound kernels (fused chirp-z, Pwelch) take it: there an address
+// instruction costs what an FP64 one does, while the LDS has slack.
+template <int ILV, int E = 16, bool XOR = false, bool LINEAR = false>
 __device__ __forceinline__ int lds_off(int i) {
   if constexpr (ILV != 0) return i * ILV;
+  else if constexpr (LINEAR && E >= 16) return i + (i >> clog2(E));
   else if constexpr (XOR && kLdsXor) return i ^ ((i >> clog2(E)) & 15);
   else return padi(i);
 }
 
-template <int N, int E, int T, int R, int NS, bool SPLIT, int ILV = 0>
+template <int N, int E, int T, int R, int NS, bool SPLIT, int ILV = 0, bool LINEAR = false>
 __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, double *lim,
                                               bool first) {
   constexpr int B = E / R;
@@ -307,7 +316,7 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
     const int j = t + b * T;
     const int base = (j / NS) * (NS * R) + (j & (NS - 1));
 #pragma unroll
-    for (int r = 0; r < R; ++r) dst[b + r * B] = lds_off<ILV, E, (T >= 32)>(base + r * NS);
+    for (int r = 0; r < R; ++r) dst[b + r * B] = lds_off<ILV, E, (T >= 32), (LINEAR && T >= 32)>(base + r * NS);
   }
   if (!first) __syncthreads();
   if constexpr (SPLIT) {
@@ -315,13 +324,13 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
     for (int k = 0; k < E; ++k) lre[dst[k]] = v[k].x;
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < E; ++k) v[k].x = lre[lds_off<ILV, E, (T >= 32)>(t + k * T)];
+    for (int k = 0; k < E; ++k) v[k].x = lre[lds_off<ILV, E, (T >= 32), (LINEAR && T >= 32)>(t + k * T)];
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < E; ++k) lre[dst[k]] = v[k].y;
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < E; ++k) v[k].y = lre[lds_off<ILV, E, (T >= 32)>(t + k * T)];
+    for (int k = 0; k < E; ++k) v[k].y = lre[lds_off<ILV, E, (T >= 32), (LINEAR && T >= 32)>(t + k * T)];
   } else {
 #pragma unroll
     for (int k = 0; k < E; ++k) {
@@ -331,7 +340,7 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < E; ++k)
-      v[k] = {lre[lds_off<ILV, E, (T >= 32)>(t + k * T)], lim[lds_off<ILV, E, (T >= 32)>(t + k * T)]};
+      v[k] = {lre[lds_off<ILV, E, (T >= 32), (LINEAR && T >= 32)>(t + k * T)], lim[lds_off<ILV, E, (T >= 32), (LINEAR && T >= 32)>(t + k * T)]};
   }
 }
 
@@ -366,7 +375,7 @@ using RegArr = cd[Geo<LOG2N, LOG2E>::E];
 // only the thread index — enough to keep twiddle loads inside a loop, and it
 // leaves an LDS twiddle pointer's address space visible (ds_read, not flat).
 template <int LOG2N, bool SPLIT, int OPAQUE = 0, int LOG2E = 4, int ILV = 0, int P = 0,
-          class TWP = const cd *>
+          class TWP = const cd *, bool LINEAR = false>
 __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw, double *lre,
                                          double *lim, bool first_exchange = true) {
   using G = Geo<LOG2N, LOG2E>;
@@ -381,11 +390,11 @@ __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw,
       // exchange after the previous pass
       constexpr int RP = G::radix(P - 1);
       constexpr int NSP = G::ns(P - 1);
-      pass_exchange<G::N, G::E, G::T, RP, NSP, SPLIT, ILV>(v, t, lre, lim,
-                                                            first_exchange && P == 1);
+      pass_exchange<G::N, G::E, G::T, RP, NSP, SPLIT, ILV, LINEAR>(v, t, lre, lim,
+                                                                    first_exchange && P == 1);
     }
     pass_compute<G::N, G::E, G::T, R, NS>(v, t, tw);
-    fft_regs<LOG2N, SPLIT, 0, LOG2E, ILV, P + 1, TWP>(v, t, tw, lre, lim, first_exchange);
+    fft_regs<LOG2N, SPLIT, 0, LOG2E, ILV, P + 1, TWP, LINEAR>(v, t, tw, lre, lim, first_exchange);
   }
 }
 

@@ -174,10 +174,10 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
       v[k] = cmul(x, chirp[idx]);
     }
   }
-  fft_regs<LOG2M, SPLIT, true, LOG2E>(v, t, twm, lre, lim, true);
+  fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true>(v, t, twm, lre, lim, true);
 #pragma unroll
   for (int k = 0; k < G::E; ++k) v[k] = conjg(cmul(v[k], bhat[t + k * G::T]));
-  fft_regs<LOG2M, SPLIT, true, LOG2E>(v, t, twm, lre, lim, false);
+  fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true>(v, t, twm, lre, lim, false);
   chirp = opaque_ptr(chirp);
   const int to = opaque_int(t);
   if (valid) {
@@ -308,6 +308,14 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_kernel(
 // E = 16 forced to 168 / 128 VGPRs (MINW 3 / 4) spills: 4.85 / 6.07 ms;
 // window re-read from L1/L2 (WMODE 1) with the split exchange 3.48 ms, with
 // a complex (two-buffer) exchange 3.45 ms.
+// Exchange slot layout of the Pwelch kernels: XOR-swizzled (conflict-free);
+// the linear padded layout (fewer address instructions, 2-way conflicted
+// reads at E = 16) measured 3.08-3.09 against 3.03-3.05 ms (GDSP_PW_LINEAR).
+#ifdef GDSP_PW_LINEAR
+constexpr bool kPwLinear = true;
+#else
+constexpr bool kPwLinear = false;
+#endif
 template <int LOG2F, int WMODE = 2, int MINW = 1, int LOG2E = 4, bool SPLIT = true,
           bool PF = false>
 __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_kernel(
@@ -404,9 +412,12 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_ker
 #pragma unroll
     for (int k = 0; k < H; ++k) carry[k] = c2[k];
     if constexpr (PF)
-      fft_regs<LOG2F, SPLIT, 2, LOG2E>(v, opaque_int(t), (const cd *)twl, lre, lim, it == 0);
+      fft_regs<LOG2F, SPLIT, 2, LOG2E, 0, 0, const cd *, kPwLinear>(v, opaque_int(t),
+                                                                    (const cd *)twl, lre, lim,
+                                                                    it == 0);
     else
-      fft_regs<LOG2F, SPLIT, 1, LOG2E>(v, opaque_int(t), tw, lre, lim, it == 0);
+      fft_regs<LOG2F, SPLIT, 1, LOG2E, 0, 0, const cd *, kPwLinear>(v, opaque_int(t), tw, lre,
+                                                                    lim, it == 0);
     if (active) {
 #pragma unroll
       for (int k = 0; k < E; ++k) acc[k] = fma(v[k].y, v[k].y, fma(v[k].x, v[k].x, acc[k]));

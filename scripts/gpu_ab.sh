@@ -11,8 +11,10 @@ fi
 for r in $(seq 1 ${3:-2}); do
 for w in $1; do
   for L in $2; do
-    if [ "$L" = default ]; then unset GDSP_LIB; else export GDSP_LIB=$GRAFT_REPO_ROOT/$L/libgdspfft.so; fi
-    timeout -k 10 300 python bench.py --workload $w --steps 20 --warmup 3 --cpu-seconds 0 > gpurun_out/ab.json 2> gpurun_out/ab.err; rc=$?
+    # "default", a library directory, or env:VAR=value (default library, one switch set)
+    unset GDSP_LIB; EV=""
+    case "$L" in default) ;; env:*) EV="${L#env:}" ;; *) export GDSP_LIB=$GRAFT_REPO_ROOT/$L/libgdspfft.so ;; esac
+    env $EV timeout -k 10 300 python bench.py --workload $w --steps 20 --warmup 3 --cpu-seconds 0 > gpurun_out/ab.json 2> gpurun_out/ab.err; rc=$?
     [ $rc -eq 0 ] || { echo "$w $L rc=$rc"; tail -20 gpurun_out/ab.err; exit $rc; }
     python -c "import json;d=json.load(open('gpurun_out/ab.json'));r=d['roofline'];print('$w','$L',d['ms_per_step'],r['avg_launch_ms'],r['frac'],(d.get('parity') or {}).get('max_nrel_vs_oracle'))"
   done
