@@ -169,7 +169,13 @@ def fft2_sharded(x_local, rows_total: int, inverse: bool = False, group=None, st
         rows = [shard_range(rows_total, W, q) for q in range(W)]
         cols = [shard_range(C, W, q) for q in range(W)]
         c_lo, c_hi = cols[r]
-        send = torch.cat([y[:, a:b].reshape(-1) for a, b in cols])
+        even = C % W == 0
+        if even:
+            # the W column blocks of the local rows, block-major: one copy of
+            # contiguous C/W-element runs (torch.cat of column slices took two)
+            send = y.view(rows_r, W, C // W).transpose(0, 1).contiguous().view(-1)
+        else:
+            send = torch.cat([y[:, a:b].reshape(-1) for a, b in cols])
         blk = torch.empty((rows_total, c_hi - c_lo), dtype=y.dtype, device=y.device)
         _all_to_all_c128(send, blk, [rows_r * (b - a) for a, b in cols],
                          [(b - a) * (c_hi - c_lo) for a, b in rows], group, dist, torch)
@@ -177,6 +183,8 @@ def fft2_sharded(x_local, rows_total: int, inverse: bool = False, group=None, st
         back = torch.empty(rows_r * C, dtype=y.dtype, device=y.device)
         _all_to_all_c128(blk.reshape(-1), back, [(b - a) * (c_hi - c_lo) for a, b in rows],
                          [rows_r * (b - a) for a, b in cols], group, dist, torch)
+        if even:
+            return back.view(W, rows_r, C // W).transpose(0, 1).reshape(rows_r, C)
         pieces, off = [], 0
         for a, b in cols:
             pieces.append(back[off:off + rows_r * (b - a)].view(rows_r, b - a))
