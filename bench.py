@@ -40,14 +40,15 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (tools/fp64peak.hip measures 67.3 FMA-only)
 # kernels whose FP64 work is taken from the committed SQ counter passes
-# (profiles/r01/sq_counters.json: 64 x (2 FMA + ADD + MUL) F64 instructions)
+# (profiles/r02/sq_counters.json: 64 x (2 FMA + ADD + MUL) F64 instructions)
 SQ_KERNELS = {"radix4096": ["fft_lds_kernel<12"], "bluestein3000": ["fft_mixed_fixed_kernel"],
               "chirpz3000": ["bluestein_kernel<13"], "pwelch": ["pwelch_half_kernel<12"],
               "fft2_8192": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"],
               "fft2_dist": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"]}
+SQ_ROUND = "r02"  # the round whose SQ counter passes bench lines quote
 SEED = 0x5EED
 # algorithmic bytes of one launch in the N=1 full-size configuration the
-# committed PMC (profiles/pmc_*.json) and SQ (profiles/r01/sq_counters.json)
+# committed PMC (profiles/pmc_*.json) and SQ (profiles/r02/sq_counters.json)
 # summaries were measured on
 PROFILED_ALG_BYTES = {"radix4096": 32 * 4096 * 65536, "bluestein3000": 32 * 3000 * 65536,
                       "chirpz3000": 32 * 3000 * 65536, "fft2_8192": 4 * 16 * 8192 * 8192,
@@ -412,7 +413,7 @@ def fp64_info(workload: str, launch_s: float, share: float = 1.0):
     over its kernels, times this launch's share of the profiled work)
     against the FP64 vector peak — the second roofline of the compute-heavy
     paths (chirp-z, Pwelch)."""
-    path = os.path.join(REPO, "profiles", "r01", "sq_counters.json")
+    path = os.path.join(REPO, "profiles", SQ_ROUND, "sq_counters.json")
     ks = SQ_KERNELS.get("fft2_8192" if workload == "fft2_dist" else workload)
     if not ks or not os.path.exists(path):
         return None
@@ -428,7 +429,7 @@ def fp64_info(workload: str, launch_s: float, share: float = 1.0):
     tf = flop / launch_s / 1e12
     return {"flop_per_launch": flop, "achieved_tflops": round(tf, 2),
             "peak_tflops": FP64_PEAK_TFLOPS, "frac": round(tf / FP64_PEAK_TFLOPS, 4),
-            "source": "profiles/r01/sq_counters.json (SQ_INSTS_VALU_{FMA,ADD,MUL}_F64)"}
+            "source": f"profiles/{SQ_ROUND}/sq_counters.json (SQ_INSTS_VALU_{{FMA,ADD,MUL}}_F64)"}
 
 
 def cpu_baseline(workload: str, seconds: float):

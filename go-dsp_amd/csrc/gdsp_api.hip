@@ -1445,7 +1445,11 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
     // fused path: packed segment pairs, persistent workers over contiguous
     // pair ranges (the 50 % overlap of consecutive pairs is re-read from L2)
     const int64_t npairs = (nseg + 1) / 2;
-    int64_t target = 2048 * (int64_t)gdsp::pwelch_workers_per_block(p->log2n);
+    static const int64_t wmul = [] {  // workers per workgroup slot (tuning switch)
+      const char *e = getenv("GDSP_PW_WORKERS");
+      return e ? (int64_t)atoll(e) : (int64_t)2048;
+    }();
+    int64_t target = wmul * (int64_t)gdsp::pwelch_workers_per_block(p->log2n);
     if (target > npairs) target = npairs;
     const int64_t ppw = (npairs + target - 1) / target;
     const int64_t nworkers = (npairs + ppw - 1) / ppw;
