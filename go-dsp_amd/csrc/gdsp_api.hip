@@ -321,6 +321,12 @@ struct gdsp_plan {
   gdsp_plan *mplan = nullptr;
   cd *chirp = nullptr;
   cd *bhat = nullptr;
+  // wave-resident chirp-z (fft_wave.hip) for 512 < n <= 4096: Q = M / 2048
+  // waves per transform; bhatw[q 2048 + k] = bhat[Q k + q], wbase[q 65 + j] =
+  // W_M^(q j) (j <= 64); t2048 = T_2048
+  int wq = 0;
+  cd *bhatw = nullptr, *wbase = nullptr;
+  const cd *t2048 = nullptr;
 };
 
 namespace {
@@ -526,6 +532,47 @@ bool mixcol_build(int dev, int64_t n, gdsp_plan *p) {
   return false;
 }
 
+// The wave-resident chirp-z kernel (fft_wave.hip) for 512 < n <= 4096, when
+// GDSP_BLU_WAVE=1. Measured slower than the block-wide bluestein_kernel at
+// every Q (chirp-z 3000: 3.83 against 3.35 ms), so it is opt-in.
+bool wave_chirpz_enabled() {
+  static const bool on = [] {
+    const char *e = getenv("GDSP_BLU_WAVE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+// Plan tables of the wave-resident chirp-z kernel (see gdsp_plan::wq): bhat
+// permuted per wave, and the DIF/DIT twiddle bases W_M^(q j), j <= 64.
+int build_wave_tables(int dev, gdsp_plan *p) {
+  const int64_t n = p->n, M = p->m;
+  const int Q = gdsp::bluestein_wave_q(n, M);
+  if (!Q) return GDSP_OK;
+  gdsp_plan *p2048 = nullptr;
+  STCHK(get_plan_locked(dev, 2048, &p2048));
+  hipStream_t s = thread_stream(dev);
+  std::vector<cd> bh((size_t)M), bw((size_t)M), wb((size_t)(Q * 65));
+  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipMemcpy(bh.data(), p->bhat, (size_t)M * sizeof(cd), hipMemcpyDeviceToHost));
+  const long double tau = 2.0L * 3.141592653589793238462643383279502884L;
+  for (int q = 0; q < Q; ++q) {
+    for (int64_t k = 0; k < 2048; ++k) bw[(size_t)(q * 2048 + k)] = bh[(size_t)(Q * k + q)];
+    for (int j = 0; j <= 64; ++j) {
+      const long double a = -tau * (long double)(q * j) / (long double)M;
+      wb[(size_t)(q * 65 + j)] = {(double)cosl(a), (double)sinl(a)};
+    }
+  }
+  HIPCHK(hipMalloc((void **)&p->bhatw, bw.size() * sizeof(cd)));
+  HIPCHK(hipMalloc((void **)&p->wbase, wb.size() * sizeof(cd)));
+  STCHK(copy_h2d(p->bhatw, bw.data(), bw.size() * sizeof(cd), s));
+  STCHK(copy_h2d(p->wbase, wb.data(), wb.size() * sizeof(cd), s));
+  HIPCHK(hipStreamSynchronize(s));
+  p->t2048 = p2048->tw;
+  p->wq = Q;
+  return GDSP_OK;
+}
+
 int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   p->device = dev;
   p->n = n;
@@ -646,6 +693,8 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
     if (e != hipSuccess) st = fail(GDSP_ERR_HIP, hipGetErrorString(e));
   }
   (void)hipFree(db);
+  if (st == GDSP_OK && wave_chirpz_enabled() && gdsp::bluestein_wave_q(n, p->m))
+    st = build_wave_tables(dev, p);
   return st;
 }
 
@@ -967,6 +1016,11 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
         STCHK(tmp.alloc((size_t)batch * (size_t)p->n * sizeof(cd), s, SLOT_REAL));
         HIPCHK(gdsp::launch_real_to_complex((const double *)in, (cd *)tmp.p, batch * p->n, s));
         src = (const cd *)tmp.p;
+      }
+      if (p->kind == KIND_BLUESTEIN && p->wq) {
+        HIPCHK(gdsp::launch_bluestein_wave(p->wq, inv, src, out, p->n, batch, p->t2048, p->wbase,
+                                           p->bhatw, p->chirp, scale, s));
+        return GDSP_OK;
       }
       if (p->kind == KIND_BLUESTEIN) {
         HIPCHK(gdsp::launch_bluestein(p->log2m, inv, src, out, p->n, batch, p->mplan->tw, p->chirp,
@@ -1407,6 +1461,7 @@ int gdsp_plan_create_chirpz(int64_t n, gdsp_plan **plan) {
 int gdsp_plan_destroy(gdsp_plan *) { return GDSP_OK; }
 
 int gdsp_plan_kind(const gdsp_plan *plan) { return plan ? plan->kind : -1; }
+int gdsp_plan_wave_q(const gdsp_plan *plan) { return plan ? plan->wq : 0; }
 
 int gdsp_plan_info(const gdsp_plan *plan, int64_t *n, int64_t *m, int64_t *n1, int64_t *n2,
                    int *runtime_compiled) {

@@ -67,6 +67,13 @@ hipError_t launch_fft_mixed(const MixedDesc &d, bool inv, int load, const void *
 hipError_t launch_bluestein(int log2m, bool inv, const cd *in, cd *out, int64_t n,
                             int64_t batch, const cd *twm, const cd *chirp, const cd *bhat,
                             double scale, hipStream_t s);
+// wave-resident chirp-z (fft_wave.hip): waves per transform Q = M / 2048 for
+// 512 < n <= 1024 Q, 2n - 1 <= M (0: not this kernel's case)
+int bluestein_wave_q(int64_t n, int64_t m);
+// wbase[q 65 + j] = W_M^(q j) (j <= 64), bhatw[q 2048 + k] = bhat[Q k + q]
+hipError_t launch_bluestein_wave(int q, bool inv, const cd *in, cd *out, int64_t n, int64_t batch,
+                                 const cd *t2048, const cd *wbase, const cd *bhatw, const cd *chirp,
+                                 double scale, hipStream_t s);
 hipError_t launch_global_pass(int radix, bool conj_in, int load, bool conj_scale_out,
                               const void *in, cd *out, const cd *tw, int log2n, int log2ns,
                               int64_t batch, double scale, hipStream_t s);

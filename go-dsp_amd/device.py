@@ -49,6 +49,8 @@ class Plan:
         # chirp-z convolution length; four-step split; runtime-compiled?
         self.m, self.n1, self.n2 = v[1].value, v[2].value, v[3].value
         self.runtime_compiled = bool(rc.value)
+        # waves per transform of the wave-resident chirp-z kernel (0: another kernel)
+        self.wave_q = int(lib().gdsp_plan_wave_q(self.handle))
 
 
 _plans: dict = {}

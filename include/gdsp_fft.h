@@ -225,6 +225,10 @@ int gdsp_plan_kind(const gdsp_plan *plan);
  * runtime-compiled specialisation backs it (1) or not (0). 0 where n/a. */
 int gdsp_plan_info(const gdsp_plan *plan, int64_t *n, int64_t *m, int64_t *n1, int64_t *n2,
                    int *runtime_compiled);
+/* Waves per transform of the wave-resident chirp-z kernel (fft_wave.hip:
+ * one 64-lane wavefront per 2048-point sub-transform, M = 2048 * waves) that a
+ * kind-3 plan with 512 < n <= 4096 runs, or 0 for any other kernel. */
+int gdsp_plan_wave_q(const gdsp_plan *plan);
 
 /* Batched C2C on device buffers: d_in/d_out hold batch*n complex128 (may
  * alias only if equal). inverse != 0 → IFFT semantics (1/n scaling). */

@@ -646,6 +646,52 @@ def test_chirpz_primes(gdsp, oracle, n):
     assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
 
 
+# the wave-resident chirp-z kernel (fft_wave.hip, opt-in: GDSP_BLU_WAVE=1):
+# Q = M/2048 waves per transform, Q = 1 (n <= 1024), 2, 4; the edges of each
+# range, primes, and batches that leave the last workgroup partly empty (2 or
+# 4 transforms per workgroup at Q = 2, 1). Its exchanges are a wave-local LDS
+# transpose and a v_permlane32_swap (no workgroup barrier inside a transform).
+WAVE_N = [513, 700, 1009, 1023, 1024, 1025, 1500, 2039, 2047, 2048, 2049, 2053, 3000, 3072,
+          3073, 4093, 4095, 4096]
+
+
+def test_chirpz_wave_kernel():
+    code = r'''
+import importlib, os, sys
+sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
+import numpy as np, oracle, torch
+D = importlib.import_module("go-dsp_amd.device")
+def row_nrel(a, b):
+    return max(np.linalg.norm(x - y) / np.linalg.norm(y) for x, y in zip(a, b))
+for n in [int(v) for v in os.environ["WAVE_N"].split()]:
+    p = D.plan(n, chirpz=True)
+    m = 1 << (2 * n - 2).bit_length()  # bluestein.go:70
+    assert p.kind == 3 and p.m == m and p.wave_q == m // 2048, (n, p.kind, p.m, p.wave_q)
+    rng = np.random.default_rng(9000 + n)
+    for batch in (1, 5):
+        x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
+        xt = torch.from_numpy(x).cuda()
+        e = row_nrel(D.fft_batch(xt, chirpz=True).cpu().numpy(), oracle.fft_rows(x))
+        ei = row_nrel(D.fft_batch(xt, inverse=True, chirpz=True).cpu().numpy(), oracle.ifft_rows(x))
+        assert e < 1e-9 and ei < 1e-9, (n, batch, e, ei)
+    # the default plan of the same length takes the wave kernel too when it is chirp-z
+    if D.plan(n).kind == 3:
+        assert D.plan(n).wave_q == m // 2048, n
+print("ok")
+'''
+    env = dict(os.environ, REPO=REPO, GDSP_BLU_WAVE="1", WAVE_N=" ".join(map(str, WAVE_N)))
+    r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_chirpz_block_kernel_default(gdsp):
+    """Without GDSP_BLU_WAVE=1 the fused chirp-z plans run the block-wide
+    bluestein_kernel (the faster of the two, DESIGN.md §3)."""
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    for n in (1009, 3000):
+        assert D.plan(n, chirpz=True).wave_q == 0
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [4096, 3000, 1 << 20, 8209, 5400])
 def test_ensure_radix2_factors_then_fft(gdsp, oracle, n):

@@ -46,13 +46,16 @@ def collect(w):
 
 def main(tag, workloads):
     res = {w: collect(w) for w in workloads}
+    if tag == "-":  # print only (experiments)
+        merged = None
     dst = os.path.join(REPO, "profiles", tag)
-    os.makedirs(dst, exist_ok=True)
-    path = os.path.join(dst, "sq_counters.json")
-    merged = json.load(open(path)) if os.path.exists(path) else {}
-    merged.update(res)  # the workloads re-measured replace their entries
-    with open(path, "w") as f:
-        json.dump(merged, f, indent=1, sort_keys=True)
+    if tag != "-":
+        os.makedirs(dst, exist_ok=True)
+        path = os.path.join(dst, "sq_counters.json")
+        merged = json.load(open(path)) if os.path.exists(path) else {}
+        merged.update(res)  # the workloads re-measured replace their entries
+        with open(path, "w") as f:
+            json.dump(merged, f, indent=1, sort_keys=True)
     for w, ks in res.items():
         print("==", w)
         for k, m in ks.items():
@@ -62,7 +65,8 @@ def main(tag, workloads):
                   f"bankconf={m['lds_bank_conflict_per_active']:.3f} f64flop={m['f64_flop']:.3e} "
                   f"insts valu={m.get('SQ_INSTS_VALU',0):.3e} lds={m.get('SQ_INSTS_LDS',0):.3e} "
                   f"salu={m.get('SQ_INSTS_SALU',0):.3e} vmem={m.get('SQ_INSTS_VMEM',0):.3e} "
-                  f"grbm={m.get('GRBM_GUI_ACTIVE',0):.3e}")
+                  f"grbm={m.get('GRBM_GUI_ACTIVE',0):.3e} waves={m.get('SQ_WAVES',0):.3e} "
+                  f"wavecyc={m.get('SQ_WAVE_CYCLES',0):.3e} busy={m.get('SQ_BUSY_CYCLES',0):.3e}")
 
 
 if __name__ == "__main__":
