@@ -926,9 +926,18 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
     GDSP_PWH(5) GDSP_PWH(6) GDSP_PWH(7) GDSP_PWH(8) GDSP_PWH(9) GDSP_PWH(10) GDSP_PWH(11)
     // F = 4096 (the BASELINE configuration): twiddle bases in LDS and the
     // next pair prefetched (3.16 -> 3.11 ms; 244 VGPRs, still 2 waves/SIMD)
-    case 12:
+    case 12: {
+      // the wavefront-shuffle variant (pwelch_shfl.hip): one exchange in LDS,
+      // the other inside the wave (GDSP_PW_SHFL=0 restores the two-exchange one)
+      static const int shfl = [] {
+        const char *e = getenv("GDSP_PW_SHFL");
+        return e ? atoi(e) : 0;
+      }();
+      if (shfl)
+        return launch_pwelch4096_shfl(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
       return launch_pwh_t<12, 2, 1, 4, true, true>(x, seg_begin, seg_end, ppw, nworkers, win, tw,
                                                    partial, s);
+    }
     GDSP_PWH(13)
 #undef GDSP_PWH
     // F = 16384: the exchange buffer alone takes 136 KiB, so the window is

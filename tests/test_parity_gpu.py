@@ -684,6 +684,31 @@ print("ok")
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 
 
+def test_pwelch_shuffle_kernel():
+    """The NFFT 4096 / 50 % Pwelch kernel with the in-wave second exchange
+    (pwelch_shfl.hip, opt-in GDSP_PW_SHFL=1: DPP row shifts and
+    v_permlane16/32_swap) against the oracle: even and odd segment counts,
+    a one-pair call, and Hann / Hamming windows."""
+    code = r'''
+import importlib, os, sys
+sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
+import numpy as np, oracle
+g = importlib.import_module("go-dsp_amd")
+for n, win in ((40960, "hann"), (38913, "hann"), (6144, "hann"), (100000, "hamming"), (8192, "hann")):
+    x = np.random.default_rng(n).standard_normal(n)
+    w = getattr(g.window, win.capitalize())
+    o = g.spectral.PwelchOptions(NFFT=4096, Noverlap=2048, Window=w)
+    p, f = g.spectral.Pwelch(x, 2.0, o)
+    pr, fr = oracle.pwelch(x, 2.0, nfft=4096, noverlap=2048, window_kind=win)
+    e = np.linalg.norm(p - pr) / np.linalg.norm(pr)
+    assert e < 1e-9, (n, win, e)
+print("ok")
+'''
+    env = dict(os.environ, REPO=REPO, GDSP_PW_SHFL="1")
+    r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
 def test_chirpz_block_kernel_default(gdsp):
     """Without GDSP_BLU_WAVE=1 the fused chirp-z plans run the block-wide
     bluestein_kernel (the faster of the two, DESIGN.md §3)."""
