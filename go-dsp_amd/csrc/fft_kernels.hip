@@ -628,13 +628,16 @@ __global__ __launch_bounds__(256) void transpose_kernel(const cd *__restrict__ i
 //   mode 1: out[b*M + k] = conj(v * bhat[k])          (between the two FFTs)
 //   mode 2: out[b*n + k] = conj(v) * chirp[k], k < n   (the result; an
 //           inverse conjugates and scales it)
-// Tiles as transpose_kernel<32, 64>.
+// Tiles of TR x TC as transpose_kernel; TR follows the row count (the
+// four-step's column length, as short as 4 for a single-radix column split),
+// so the load lanes of a tile are not mostly past the last row.
+template <int TR, int TC>
 __global__ __launch_bounds__(256) void transpose_blu_kernel(const cd *__restrict__ in,
                                                             cd *__restrict__ out, int64_t rows,
                                                             int64_t cols, int64_t batch, int mode,
                                                             int64_t n, const cd *__restrict__ tab,
                                                             int inv, double scale) {
-  constexpr int TR = 32, TC = 64, LY = 256 / TC, SY = 256 / TR;
+  constexpr int LY = 256 / TC, SY = 256 / TR;
   __shared__ cd tile[TR][TC + 1];
   const int64_t M = rows * cols;
   const int64_t tiles_c = (cols + TC - 1) / TC, tiles_r = (rows + TR - 1) / TR;
@@ -1111,11 +1114,18 @@ hipError_t launch_transpose_blu(const cd *in, cd *out, int64_t rows, int64_t col
                                 hipStream_t s) {
   if (batch < 1 || batch > 65535 || (mode != 1 && mode != 2)) return hipErrorInvalidValue;
   if (mode == 2 && n > rows * cols) return hipErrorInvalidValue;
-  const int64_t tiles = ((rows + 31) / 32) * ((cols + 63) / 64) * batch;
   const int64_t cap = 256 * 32;
-  const unsigned nb = (unsigned)(tiles < cap ? tiles : cap);
-  hipLaunchKernelGGL(transpose_blu_kernel, dim3(nb), dim3(256), 0, s, in, out, rows, cols, batch,
-                     mode, n, tab, (int)inv, scale);
+#define GDSP_TBLU(TR, TC)                                                                    \
+  do {                                                                                       \
+    const int64_t tiles = ((rows + TR - 1) / TR) * ((cols + TC - 1) / TC) * batch;          \
+    const unsigned nb = (unsigned)(tiles < cap ? tiles : cap);                               \
+    hipLaunchKernelGGL((transpose_blu_kernel<TR, TC>), dim3(nb), dim3(256), 0, s, in, out,   \
+                       rows, cols, batch, mode, n, tab, (int)inv, scale);                    \
+  } while (0)
+  if (rows <= 8) GDSP_TBLU(8, 256);
+  else if (rows <= 16) GDSP_TBLU(16, 128);
+  else GDSP_TBLU(32, 64);
+#undef GDSP_TBLU
   return hipGetLastError();
 }
 
