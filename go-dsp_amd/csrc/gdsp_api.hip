@@ -327,6 +327,9 @@ struct gdsp_plan {
   int wq = 0;
   cd *bhatw = nullptr, *wbase = nullptr;
   const cd *t2048 = nullptr;
+  // shuffle chirp-z (bluestein_shfl.hip) for M = 8192: bhat in the kernel's
+  // register order, bhats[r 256 + t] = bhat[bluestein_shfl_bin(t, r)]
+  cd *bhats = nullptr;
 };
 
 namespace {
@@ -573,6 +576,29 @@ int build_wave_tables(int dev, gdsp_plan *p) {
   return GDSP_OK;
 }
 
+// The M = 8192 chirp-z kernel whose FFTs keep one exchange in the wave
+// (bluestein_shfl.hip), when GDSP_BLU_SHFL=1.
+bool shfl_chirpz_enabled() {
+  static const bool on = [] {
+    const char *e = getenv("GDSP_BLU_SHFL");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+int build_shfl_tables(gdsp_plan *p) {
+  hipStream_t s = thread_stream(p->device);
+  std::vector<cd> bh((size_t)p->m), bs((size_t)p->m);
+  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipMemcpy(bh.data(), p->bhat, (size_t)p->m * sizeof(cd), hipMemcpyDeviceToHost));
+  for (int r = 0; r < 32; ++r)
+    for (int t = 0; t < 256; ++t) bs[(size_t)(r * 256 + t)] = bh[(size_t)gdsp::bluestein_shfl_bin(t, r)];
+  HIPCHK(hipMalloc((void **)&p->bhats, bs.size() * sizeof(cd)));
+  STCHK(copy_h2d(p->bhats, bs.data(), bs.size() * sizeof(cd), s));
+  HIPCHK(hipStreamSynchronize(s));
+  return GDSP_OK;
+}
+
 int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   p->device = dev;
   p->n = n;
@@ -695,6 +721,9 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   (void)hipFree(db);
   if (st == GDSP_OK && wave_chirpz_enabled() && gdsp::bluestein_wave_q(n, p->m))
     st = build_wave_tables(dev, p);
+  if (st == GDSP_OK && !p->wq && shfl_chirpz_enabled() && p->kind == KIND_BLUESTEIN &&
+      p->m == 8192 && 2 * n <= p->m)
+    st = build_shfl_tables(p);
   return st;
 }
 
@@ -1020,6 +1049,11 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
       if (p->kind == KIND_BLUESTEIN && p->wq) {
         HIPCHK(gdsp::launch_bluestein_wave(p->wq, inv, src, out, p->n, batch, p->t2048, p->wbase,
                                            p->bhatw, p->chirp, scale, s));
+        return GDSP_OK;
+      }
+      if (p->kind == KIND_BLUESTEIN && p->bhats) {
+        HIPCHK(gdsp::launch_bluestein_shfl(inv, src, out, p->n, batch, p->mplan->tw, p->chirp,
+                                           p->bhats, scale, s));
         return GDSP_OK;
       }
       if (p->kind == KIND_BLUESTEIN) {
@@ -1462,6 +1496,8 @@ int gdsp_plan_destroy(gdsp_plan *) { return GDSP_OK; }
 
 int gdsp_plan_kind(const gdsp_plan *plan) { return plan ? plan->kind : -1; }
 int gdsp_plan_wave_q(const gdsp_plan *plan) { return plan ? plan->wq : 0; }
+
+int gdsp_plan_shfl(const gdsp_plan *plan) { return plan && plan->bhats ? 1 : 0; }
 
 int gdsp_plan_info(const gdsp_plan *plan, int64_t *n, int64_t *m, int64_t *n1, int64_t *n2,
                    int *runtime_compiled) {

@@ -74,6 +74,12 @@ int bluestein_wave_q(int64_t n, int64_t m);
 hipError_t launch_bluestein_wave(int q, bool inv, const cd *in, cd *out, int64_t n, int64_t batch,
                                  const cd *t2048, const cd *wbase, const cd *bhatw, const cd *chirp,
                                  double scale, hipStream_t s);
+// M = 8192 chirp-z with in-wave exchanges (bluestein_shfl.hip), 2049 <= n <=
+// 4096: bhatp[r 256 + t] = bhat[bluestein_shfl_bin(t, r)], twm = T_8192
+int bluestein_shfl_bin(int t, int r);
+hipError_t launch_bluestein_shfl(bool inv, const cd *in, cd *out, int64_t n, int64_t batch,
+                                 const cd *twm, const cd *chirp, const cd *bhatp, double scale,
+                                 hipStream_t s);
 hipError_t launch_global_pass(int radix, bool conj_in, int load, bool conj_scale_out,
                               const void *in, cd *out, const cd *tw, int log2n, int log2ns,
                               int64_t batch, double scale, hipStream_t s);

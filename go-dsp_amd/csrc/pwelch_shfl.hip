@@ -23,6 +23,7 @@
 // Four workgroup barriers per pair instead of eight.
 #include "fft_device.hpp"
 #include "launch.hpp"
+#include "shfl.hpp"
 
 namespace gdsp {
 
@@ -62,123 +63,35 @@ __device__ __forceinline__ void twiddle16(cd (&u)[16], cd w) {
   }
 }
 
-__device__ __forceinline__ unsigned lo32(double d) {
-  return (unsigned)__builtin_bit_cast(unsigned long long, d);
-}
-__device__ __forceinline__ unsigned hi32(double d) {
-  return (unsigned)(__builtin_bit_cast(unsigned long long, d) >> 32);
-}
-__device__ __forceinline__ double mk64(unsigned lo, unsigned hi) {
-  return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
-}
-
-// Swap lane bit log2(S) (S = 4: bit 2, S = 8: bit 3) with a register bit:
-// x holds the register-bit-0 element, y the register-bit-1 one. New x = y from
-// lane l - S on the lanes with the bit set (row_shr, banks of those lanes
-// only), new y = x from lane l + S on the others (row_shl); the lanes a bank
-// mask leaves out keep their value, so no select is needed.
-template <int S>
-__device__ __forceinline__ void dpp_swap(double &x, double &y) {
-  constexpr int SHR = 0x110 + S, SHL = 0x100 + S;
-#ifdef GDSP_PS_SEL
-  const bool sel = (__lane_id() & S) != 0;
-  const unsigned xl0 = lo32(x), xh0 = hi32(x), yl0 = lo32(y), yh0 = hi32(y);
-  const unsigned a = __builtin_amdgcn_update_dpp(0u, yl0, SHR, 0xF, 0xF, true);
-  const unsigned b = __builtin_amdgcn_update_dpp(0u, yh0, SHR, 0xF, 0xF, true);
-  const unsigned c = __builtin_amdgcn_update_dpp(0u, xl0, SHL, 0xF, 0xF, true);
-  const unsigned d = __builtin_amdgcn_update_dpp(0u, xh0, SHL, 0xF, 0xF, true);
-  x = mk64(sel ? a : xl0, sel ? b : xh0);
-  y = mk64(sel ? yl0 : c, sel ? yh0 : d);
-  return;
-#endif
-  constexpr int BSET = S == 4 ? 0xA : 0xC, BCLR = S == 4 ? 0x5 : 0x3;
-  const unsigned xl = lo32(x), xh = hi32(x), yl = lo32(y), yh = hi32(y);
-  const unsigned nxl = __builtin_amdgcn_update_dpp(xl, yl, SHR, 0xF, BSET, false);
-  const unsigned nxh = __builtin_amdgcn_update_dpp(xh, yh, SHR, 0xF, BSET, false);
-  const unsigned nyl = __builtin_amdgcn_update_dpp(yl, xl, SHL, 0xF, BCLR, false);
-  const unsigned nyh = __builtin_amdgcn_update_dpp(yh, xh, SHL, 0xF, BCLR, false);
-  x = mk64(nxl, nxh);
-  y = mk64(nyl, nyh);
-}
-
-// lane bit 4 (ROW16) or 5 <-> register bit: v_permlane16_swap / 32_swap
-template <bool ROW16>
-__device__ __forceinline__ void perm_swap(double &x, double &y) {
-  const unsigned xl = lo32(x), xh = hi32(x), yl = lo32(y), yh = hi32(y);
-  if constexpr (ROW16) {
-    const auto l = __builtin_amdgcn_permlane16_swap(xl, yl, false, false);
-    const auto h = __builtin_amdgcn_permlane16_swap(xh, yh, false, false);
-    x = mk64(l[0], h[0]);
-    y = mk64(l[1], h[1]);
-  } else {
-    const auto l = __builtin_amdgcn_permlane32_swap(xl, yl, false, false);
-    const auto h = __builtin_amdgcn_permlane32_swap(xh, yh, false, false);
-    x = mk64(l[0], h[0]);
-    y = mk64(l[1], h[1]);
-  }
-}
-
-// reference form of one lane-bit <-> register-bit swap through ds_bpermute
-// (experiments: GDSP_PS_BPERM / GDSP_PS_BPERM_HI)
-template <int S>
-__device__ __forceinline__ void bperm_swap(double &x, double &y) {
-  const int l = __lane_id();
-  const bool sel = (l & S) != 0;
-  const double yo = __shfl(y, l ^ S), xo = __shfl(x, l ^ S);
-  const double nx = sel ? yo : x, ny = sel ? y : xo;
-  x = nx;
-  y = ny;
-}
-
 // register bits 0-3 <-> lane bits 2-5 (exchange 2): afterwards register r
 // holds D0 = r and lane bits 2-5 hold the former register index
 __device__ __forceinline__ void swap_reg_lane(cd (&v)[16]) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     if (!(r & 1)) {
-#ifdef GDSP_PS_BPERM
-      bperm_swap<4>(v[r].x, v[r | 1].x);
-      bperm_swap<4>(v[r].y, v[r | 1].y);
-#else
       dpp_swap<4>(v[r].x, v[r | 1].x);
       dpp_swap<4>(v[r].y, v[r | 1].y);
-#endif
     }
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     if (!(r & 2)) {
-#ifdef GDSP_PS_BPERM
-      bperm_swap<8>(v[r].x, v[r | 2].x);
-      bperm_swap<8>(v[r].y, v[r | 2].y);
-#else
       dpp_swap<8>(v[r].x, v[r | 2].x);
       dpp_swap<8>(v[r].y, v[r | 2].y);
-#endif
     }
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     if (!(r & 4)) {
-#ifdef GDSP_PS_BPERM_HI
-      bperm_swap<16>(v[r].x, v[r | 4].x);
-      bperm_swap<16>(v[r].y, v[r | 4].y);
-#else
       perm_swap<true>(v[r].x, v[r | 4].x);
       perm_swap<true>(v[r].y, v[r | 4].y);
-#endif
     }
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     if (!(r & 8)) {
-#ifdef GDSP_PS_BPERM_HI
-      bperm_swap<32>(v[r].x, v[r | 8].x);
-      bperm_swap<32>(v[r].y, v[r | 8].y);
-#else
       perm_swap<false>(v[r].x, v[r | 8].x);
       perm_swap<false>(v[r].y, v[r | 8].y);
-#endif
     }
   }
 }

@@ -51,6 +51,8 @@ class Plan:
         self.runtime_compiled = bool(rc.value)
         # waves per transform of the wave-resident chirp-z kernel (0: another kernel)
         self.wave_q = int(lib().gdsp_plan_wave_q(self.handle))
+        # 1: the M = 8192 chirp-z kernel with in-wave exchanges (GDSP_BLU_SHFL=1)
+        self.shfl = int(lib().gdsp_plan_shfl(self.handle))
 
 
 _plans: dict = {}

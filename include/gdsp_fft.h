@@ -229,6 +229,10 @@ int gdsp_plan_info(const gdsp_plan *plan, int64_t *n, int64_t *m, int64_t *n1, i
  * one 64-lane wavefront per 2048-point sub-transform, M = 2048 * waves) that a
  * kind-3 plan with 512 < n <= 4096 runs, or 0 for any other kernel. */
 int gdsp_plan_wave_q(const gdsp_plan *plan);
+/* 1 when a kind-3 plan (M = 8192, 2049 <= n <= 4096) runs the chirp-z kernel
+ * whose FFTs keep one of their two exchanges inside the wavefront
+ * (bluestein_shfl.hip, opt-in GDSP_BLU_SHFL=1), else 0. */
+int gdsp_plan_shfl(const gdsp_plan *plan);
 
 /* Batched C2C on device buffers: d_in/d_out hold batch*n complex128 (may
  * alias only if equal). inverse != 0 → IFFT semantics (1/n scaling). */

@@ -684,6 +684,37 @@ print("ok")
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 
 
+SHFL_N = [2049, 2500, 3000, 3001, 4095, 4096]
+
+
+def test_chirpz_shuffle_kernel():
+    """The M = 8192 chirp-z kernel whose FFTs keep one exchange inside the
+    wave (bluestein_shfl.hip, opt-in GDSP_BLU_SHFL=1) against the oracle:
+    forward and inverse, batch 1 and a ragged 7, over 2049 <= n <= 4096."""
+    code = r'''
+import importlib, os, sys
+sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
+import numpy as np, oracle, torch
+D = importlib.import_module("go-dsp_amd.device")
+def row_nrel(a, b):
+    return max(np.linalg.norm(x - y) / np.linalg.norm(y) for x, y in zip(a, b))
+for n in [int(v) for v in os.environ["SHFL_N"].split()]:
+    p = D.plan(n, chirpz=True)
+    assert p.kind == 3 and p.m == 8192 and p.shfl == 1, (n, p.kind, p.m, p.shfl)
+    rng = np.random.default_rng(7000 + n)
+    for batch in (1, 7):
+        x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
+        xt = torch.from_numpy(x).cuda()
+        e = row_nrel(D.fft_batch(xt, chirpz=True).cpu().numpy(), oracle.fft_rows(x))
+        ei = row_nrel(D.fft_batch(xt, inverse=True, chirpz=True).cpu().numpy(), oracle.ifft_rows(x))
+        assert e < 1e-9 and ei < 1e-9, (n, batch, e, ei)
+print("ok")
+'''
+    env = dict(os.environ, REPO=REPO, GDSP_BLU_SHFL="1", SHFL_N=" ".join(map(str, SHFL_N)))
+    r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
 def test_pwelch_shuffle_kernel():
     """The NFFT 4096 / 50 % Pwelch kernel with the in-wave second exchange
     (pwelch_shfl.hip, opt-in GDSP_PW_SHFL=1: DPP row shifts and

@@ -15,7 +15,7 @@ defs = [a for a in sys.argv[2:] if a.startswith("-D")]
 inc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "include")
 cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-I" + inc,
        "--cuda-device-only", "-c", src, "-o", "/dev/null",
-       "-Rpass-analysis=kernel-resource-usage"] + defs
+       "-Rpass-analysis=kernel-resource-usage"] + defs + os.environ.get("RESUSAGE_FLAGS", "").split()
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 rows, cur = [], None
 for line in out.splitlines():
