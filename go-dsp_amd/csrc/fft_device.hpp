@@ -186,6 +186,29 @@ struct Dft<32> {
   __device__ __forceinline__ static void run(cd (&a)[32]) { dft_split<8, 4>(a); }
 };
 
+// DFT_R of an input whose upper half is zero (a[R/2 ..] = 0, as in the first
+// pass of a chirp-z FFT, where n <= M/2): X[2m] = DFT_{R/2}(a)[m] and
+// X[2m+1] = DFT_{R/2}(a_j W_R^j)[m], one radix-2 stage fewer than Dft<R>
+// (compile-time zeros do not fold away: x + 0.0 is not x for x = -0.0).
+template <int R>
+__device__ __forceinline__ void dft_half_in(cd (&a)[R]) {
+  static_assert(R >= 4 && R <= 32, "rot32 covers W_R for R <= 32");
+  constexpr int H = R / 2;
+  cd e[H], o[H];
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+    e[j] = a[j];
+    o[j] = rot32(a[j], j * (32 / R));
+  }
+  Dft<H>::run(e);
+  Dft<H>::run(o);
+#pragma unroll
+  for (int m = 0; m < H; ++m) {
+    a[2 * m] = e[m];
+    a[2 * m + 1] = o[m];
+  }
+}
+
 // XOR-swizzled exchange slots (lds_off); -DGDSP_LDS_PAD16 restores the padded layout
 #ifndef GDSP_LDS_PAD16
 constexpr bool kLdsXor = true;
@@ -237,7 +260,9 @@ __device__ __forceinline__ int padi(int i) { return i + (i >> 4); }
 // Twiddle + DFT of one Stockham pass on the thread's registers. v[b + r*B]
 // holds input r of butterfly j = t + b*T. tw: forward table T_N[k] =
 // exp(-2 pi i k/N).
-template <int N, int E, int T, int R, int NS>
+// HALF_IN: the upper half of every butterfly's inputs is zero (first pass,
+// NS = 1, of a transform whose input fills at most half the points)
+template <int N, int E, int T, int R, int NS, bool HALF_IN = false>
 __device__ __forceinline__ void pass_compute(cd (&v)[E], int t, const cd *__restrict__ tw) {
   constexpr int B = E / R;
 #pragma unroll
@@ -267,7 +292,8 @@ __device__ __forceinline__ void pass_compute(cd (&v)[E], int t, const cd *__rest
         }
       }
     }
-    Dft<R>::run(u);
+    if constexpr (HALF_IN && NS == 1 && R >= 4) dft_half_in<R>(u);
+    else Dft<R>::run(u);
 #pragma unroll
     for (int r = 0; r < R; ++r) v[b + r * B] = u[r];
   }
@@ -374,8 +400,10 @@ using RegArr = cd[Geo<LOG2N, LOG2E>::E];
 // address or twiddle value survives from one call to the next); 2 launder
 // only the thread index — enough to keep twiddle loads inside a loop, and it
 // leaves an LDS twiddle pointer's address space visible (ds_read, not flat).
+// HALF_IN: elements t + k T with k >= E/2 are zero on entry (pass 0 prunes
+// one radix-2 stage; pass_compute)
 template <int LOG2N, bool SPLIT, int OPAQUE = 0, int LOG2E = 4, int ILV = 0, int P = 0,
-          class TWP = const cd *, bool LINEAR = false>
+          class TWP = const cd *, bool LINEAR = false, bool HALF_IN = false>
 __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw, double *lre,
                                          double *lim, bool first_exchange = true) {
   using G = Geo<LOG2N, LOG2E>;
@@ -393,7 +421,7 @@ __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw,
       pass_exchange<G::N, G::E, G::T, RP, NSP, SPLIT, ILV, LINEAR>(v, t, lre, lim,
                                                                     first_exchange && P == 1);
     }
-    pass_compute<G::N, G::E, G::T, R, NS>(v, t, tw);
+    pass_compute<G::N, G::E, G::T, R, NS, HALF_IN && P == 0>(v, t, tw);
     fft_regs<LOG2N, SPLIT, 0, LOG2E, ILV, P + 1, TWP, LINEAR>(v, t, tw, lre, lim, first_exchange);
   }
 }

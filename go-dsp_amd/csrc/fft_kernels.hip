@@ -162,19 +162,28 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
   const bool valid = g < batch;
   double *lre = lds + slot * G::STRIDE;
   double *lim = SPLIT ? lre : lds + G::LDS_DOUBLES + slot * G::STRIDE;
+  // n <= M/2 (M is a power of 2 >= 2n - 1): registers k >= E/2 hold no input
+  // and no output, so the first pass of FFT 1 and the last of FFT 2 are pruned
+#ifndef GDSP_BLU_NOPRUNE
+  constexpr int KH = G::E > 1 ? G::E / 2 : G::E;
+  constexpr bool HALF = G::E >= 4;
+#else
+  constexpr int KH = G::E;
+  constexpr bool HALF = false;
+#endif
   cd v[G::E];
   const cd *src = in + g * n;
 #pragma unroll
   for (int k = 0; k < G::E; ++k) {
     const int idx = t + k * G::T;
     v[k] = {0.0, 0.0};
-    if (valid && idx < n) {
+    if (k < KH && valid && idx < n) {
       cd x = ld_nt(&src[idx]);
       if constexpr (INV) x.y = -x.y;
       v[k] = cmul(x, chirp[idx]);
     }
   }
-  fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true>(v, t, twm, lre, lim, true);
+  fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, HALF>(v, t, twm, lre, lim, true);
 #pragma unroll
   for (int k = 0; k < G::E; ++k) v[k] = conjg(cmul(v[k], bhat[t + k * G::T]));
   fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true>(v, t, twm, lre, lim, false);
@@ -183,7 +192,7 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
   if (valid) {
     cd *dst = out + g * n;
 #pragma unroll
-    for (int k = 0; k < G::E; ++k) {
+    for (int k = 0; k < KH; ++k) {
       const int idx = to + k * G::T;
       if (idx < n) {
         cd y = cmul(conjg(v[k]), chirp[idx]);
