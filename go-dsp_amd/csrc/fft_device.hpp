@@ -262,12 +262,33 @@ __device__ __forceinline__ int padi(int i) { return i + (i >> 4); }
 // exp(-2 pi i k/N).
 // HALF_IN: the upper half of every butterfly's inputs is zero (first pass,
 // NS = 1, of a transform whose input fills at most half the points)
-template <int N, int E, int T, int R, int NS, bool HALF_IN = false>
-__device__ __forceinline__ void pass_compute(cd (&v)[E], int t, const cd *__restrict__ tw) {
+// Epilogue of a transform's last pass (EPI::on): butterfly b's outputs k =
+// b + r B go through epi.apply(v, k, u, f) with f = epi.load(k) loaded before
+// the butterfly's twiddles and DFT, so the load's L2 latency hides behind that
+// arithmetic instead of stalling after the pass (outputs with !epi.want(k)
+// are neither loaded nor applied). The chirp-z kernel fuses its bhat step and
+// its output postmultiply this way.
+struct NoEpi {
+  static constexpr bool on = false;
+  __device__ static constexpr bool want(int) { return false; }
+  __device__ cd load(int) const { return {0.0, 0.0}; }
+  template <int E>
+  __device__ void apply(cd (&)[E], int, cd, cd) const {}
+};
+
+template <int N, int E, int T, int R, int NS, bool HALF_IN = false, class EPI = NoEpi>
+__device__ __forceinline__ void pass_compute(cd (&v)[E], int t, const cd *__restrict__ tw,
+                                             const EPI &epi = EPI()) {
   constexpr int B = E / R;
 #pragma unroll
   for (int b = 0; b < B; ++b) {
     const int j = t + b * T;
+    cd mf[EPI::on ? R : 1];
+    if constexpr (EPI::on) {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (EPI::want(b + r * B)) mf[r] = epi.load(b + r * B);
+    }
     cd u[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) u[r] = v[b + r * B];
@@ -294,8 +315,14 @@ __device__ __forceinline__ void pass_compute(cd (&v)[E], int t, const cd *__rest
     }
     if constexpr (HALF_IN && NS == 1 && R >= 4) dft_half_in<R>(u);
     else Dft<R>::run(u);
+    if constexpr (EPI::on) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[b + r * B] = u[r];
+      for (int r = 0; r < R; ++r)
+        if (EPI::want(b + r * B)) epi.apply(v, b + r * B, u[r], mf[r]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[b + r * B] = u[r];
+    }
   }
 }
 
@@ -402,10 +429,12 @@ using RegArr = cd[Geo<LOG2N, LOG2E>::E];
 // leaves an LDS twiddle pointer's address space visible (ds_read, not flat).
 // HALF_IN: elements t + k T with k >= E/2 are zero on entry (pass 0 prunes
 // one radix-2 stage; pass_compute)
+// EPI: the last pass's epilogue (pass_compute)
 template <int LOG2N, bool SPLIT, int OPAQUE = 0, int LOG2E = 4, int ILV = 0, int P = 0,
-          class TWP = const cd *, bool LINEAR = false, bool HALF_IN = false>
+          class TWP = const cd *, bool LINEAR = false, bool HALF_IN = false, class EPI = NoEpi>
 __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw, double *lre,
-                                         double *lim, bool first_exchange = true) {
+                                         double *lim, bool first_exchange = true,
+                                         const EPI &epi = EPI()) {
   using G = Geo<LOG2N, LOG2E>;
   if constexpr (OPAQUE && P == 0 && G::NPASS > 1) {
     t = opaque_int(t);
@@ -421,8 +450,12 @@ __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw,
       pass_exchange<G::N, G::E, G::T, RP, NSP, SPLIT, ILV, LINEAR>(v, t, lre, lim,
                                                                     first_exchange && P == 1);
     }
-    pass_compute<G::N, G::E, G::T, R, NS, HALF_IN && P == 0>(v, t, tw);
-    fft_regs<LOG2N, SPLIT, 0, LOG2E, ILV, P + 1, TWP, LINEAR>(v, t, tw, lre, lim, first_exchange);
+    if constexpr (P == G::NPASS - 1)
+      pass_compute<G::N, G::E, G::T, R, NS, HALF_IN && P == 0, EPI>(v, t, tw, epi);
+    else
+      pass_compute<G::N, G::E, G::T, R, NS, HALF_IN && P == 0>(v, t, tw);
+    fft_regs<LOG2N, SPLIT, 0, LOG2E, ILV, P + 1, TWP, LINEAR, false, EPI>(v, t, tw, lre, lim,
+                                                                         first_exchange, epi);
   }
 }
 

@@ -143,6 +143,66 @@ fft_lds_kernel(const void *__restrict__ in, cd *__restrict__ out, int64_t batch,
 }
 
 // ----------------------------------------------------------------------------
+// Epilogues of the chirp-z kernel's two FFTs (fft_regs EPI): FFT 1 ends with
+// v = conj(A * bhat), FFT 2 with the postmultiply and the store of the first
+// n outputs; both load their factors ahead of each butterfly's arithmetic.
+template <int T>
+struct BhatEpi {
+  const cd *m;  // bhat + t
+  static constexpr bool on = true;
+  __device__ static constexpr bool want(int) { return true; }
+  __device__ cd load(int k) const { return m[k * T]; }
+  template <int E>
+  __device__ void apply(cd (&v)[E], int k, cd u, cd f) const { v[k] = conjg(cmul(u, f)); }
+};
+template <int T, int KH, bool INV>
+struct ChirpOutEpi {
+  const cd *chirp;
+  cd *dst;  // the transform's output row, or null (a padding slot)
+  int t;
+  int64_t n;
+  double scale;
+  static constexpr bool on = true;
+  __device__ static constexpr bool want(int k) { return k < KH; }
+  __device__ cd load(int k) const {
+    const int idx = t + k * T;
+    return idx < n ? chirp[idx] : cd{0.0, 0.0};
+  }
+  template <int E>
+  __device__ void apply(cd (&)[E], int k, cd u, cd f) const {
+    const int idx = t + k * T;
+    if (dst && idx < n) {
+      cd y = cmul(conjg(u), f);
+      if constexpr (INV) y = {y.x * scale, -y.y * scale};
+      st_nt(&dst[idx], y);
+    }
+  }
+};
+
+// Which chirp-z steps ride in an FFT's last pass (EPI): 2 both the bhat step
+// and the output postmultiply, 1 the bhat step only, 0 neither. Chosen per M
+// by occupancy and measurement (forced chirp-z, ms per 2^27 samples, 2 runs
+// each, both / bhat only / neither): M = 2^4 (n 5, 7) 4.62, 5.43 / — / 4.80,
+// 6.50; 2^5 (13) 4.33 / — / 4.10; 2^6 (29) 2.64 / — / 2.58; 2^7 (n 37) 1.76-1.86 / 1.86-1.93 /
+// 2.04-2.11; 2^8 (101) 1.38-1.40 / 1.75-1.78 / 1.73-1.78; 2^10 (509, the
+// fused steps cost a wave per SIMD) 1.68 / 1.71-1.72 / 1.46; 2^11 (1021) 1.57
+// / 1.72 / 1.74; 2^12 (1201, 2039; both: 2 waves per SIMD, else 3) 2.65 /
+// 2.23 / 2.24-2.27 and 1.83 / 1.76 / 1.77; 2^13 (3000, 4093) 2.16-2.18 /
+// 2.17-2.19 / 2.24 and 1.83 / 1.91 / 1.98; 2^14 (8191) 2.35 / 2.27-2.28 / 2.26.
+// GDSP_BLU_NOEPI / GDSP_BLU_OUT_AFTER force 0 / at most 1 (experiments).
+__host__ __device__ constexpr int blu_epi_mode(int log2m) {
+#if defined(GDSP_BLU_NOEPI)
+  return 0 * log2m;
+#else
+  const int m = (log2m == 5 || log2m == 6 || log2m == 10) ? 0 : (log2m == 12 || log2m == 14) ? 1 : 2;
+#if defined(GDSP_BLU_OUT_AFTER)
+  return m < 1 ? m : 1;
+#else
+  return m;
+#endif
+#endif
+}
+
 // Fused Bluestein (chirp-z) for non-power-of-2 n with M = NextPowerOf2(2n-1):
 //   a = x * conj(w) (zero-padded to M), A = FFT_M(a), C = A * bhat,
 //   r = IFFT_M(C) = conj(FFT_M(conj(C))) (1/M folded into bhat),
@@ -183,21 +243,37 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
       v[k] = cmul(x, chirp[idx]);
     }
   }
-  fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, HALF>(v, t, twm, lre, lim, true);
+  constexpr int EPI = blu_epi_mode(LOG2M);
+  if constexpr (EPI >= 1) {
+    // x bhat, conj: fused into FFT 1's last pass, each butterfly's factors
+    // loaded ahead of its arithmetic
+    fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, HALF, BhatEpi<G::T>>(
+        v, t, twm, lre, lim, true, BhatEpi<G::T>{bhat + t});
+  } else {
+    fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, HALF>(v, t, twm, lre, lim, true);
 #pragma unroll
-  for (int k = 0; k < G::E; ++k) v[k] = conjg(cmul(v[k], bhat[t + k * G::T]));
-  fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true>(v, t, twm, lre, lim, false);
-  chirp = opaque_ptr(chirp);
-  const int to = opaque_int(t);
-  if (valid) {
-    cd *dst = out + g * n;
+    for (int k = 0; k < G::E; ++k) v[k] = conjg(cmul(v[k], bhat[t + k * G::T]));
+  }
+  if constexpr (EPI == 2) {
+    // postmultiply and store: fused into FFT 2's last pass the same way
+    const ChirpOutEpi<G::T, KH, INV> oe{opaque_ptr(chirp), valid ? out + g * n : nullptr,
+                                        opaque_int(t), n, scale};
+    fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, false,
+             ChirpOutEpi<G::T, KH, INV>>(v, t, twm, lre, lim, false, oe);
+  } else {
+    fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true>(v, t, twm, lre, lim, false);
+    chirp = opaque_ptr(chirp);
+    const int to = opaque_int(t);
+    if (valid) {
+      cd *dst = out + g * n;
 #pragma unroll
-    for (int k = 0; k < KH; ++k) {
-      const int idx = to + k * G::T;
-      if (idx < n) {
-        cd y = cmul(conjg(v[k]), chirp[idx]);
-        if constexpr (INV) y = {y.x * scale, -y.y * scale};
-        st_nt(&dst[idx], y);
+      for (int k = 0; k < KH; ++k) {
+        const int idx = to + k * G::T;
+        if (idx < n) {
+          cd y = cmul(conjg(v[k]), chirp[idx]);
+          if constexpr (INV) y = {y.x * scale, -y.y * scale};
+          st_nt(&dst[idx], y);
+        }
       }
     }
   }
