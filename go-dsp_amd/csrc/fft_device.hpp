@@ -276,9 +276,18 @@ struct NoEpi {
   __device__ void apply(cd (&)[E], int, cd, cd) const {}
 };
 
-template <int N, int E, int T, int R, int NS, bool HALF_IN = false, class EPI = NoEpi>
+// Twiddle base of butterfly j in pass (R, NS): W_{NS R}^(j % NS)
+template <int N, int R, int NS>
+__device__ __forceinline__ cd pass_base(const cd *__restrict__ tw, int j) {
+  return tw[(j & (NS - 1)) * (N / (NS * R))];
+}
+
+// WPRE: the butterflies' twiddle bases come in wpre[b] (loaded by the caller
+// a pass ahead: fft_regs PREW) instead of being read here
+template <int N, int E, int T, int R, int NS, bool HALF_IN = false, class EPI = NoEpi,
+          bool WPRE = false>
 __device__ __forceinline__ void pass_compute(cd (&v)[E], int t, const cd *__restrict__ tw,
-                                             const EPI &epi = EPI()) {
+                                             const EPI &epi = EPI(), const cd *wpre = nullptr) {
   constexpr int B = E / R;
 #pragma unroll
   for (int b = 0; b < B; ++b) {
@@ -295,7 +304,9 @@ __device__ __forceinline__ void pass_compute(cd (&v)[E], int t, const cd *__rest
     if constexpr (NS > 1) {
       // W_{NS*R}^{(j%NS)*r}: one table read, powers by two interleaved
       // recurrences (odd and even exponents) to keep the product depth ~R/2
-      const cd w = tw[(j & (NS - 1)) * (N / (NS * R))];
+      cd w;
+      if constexpr (WPRE) w = wpre[b];
+      else w = pass_base<N, R, NS>(tw, j);
       u[1] = cmul(u[1], w);
       if constexpr (R > 2) {
         const cd w2 = cmul(w, w);
@@ -430,11 +441,16 @@ using RegArr = cd[Geo<LOG2N, LOG2E>::E];
 // HALF_IN: elements t + k T with k >= E/2 are zero on entry (pass 0 prunes
 // one radix-2 stage; pass_compute)
 // EPI: the last pass's epilogue (pass_compute)
+// PREW: each pass's twiddle bases are read before the previous pass's
+// arithmetic and exchange (wpre carries them down), so their L1/L2 or LDS
+// latency hides behind that work instead of opening the pass; only for
+// passes with at most PREW bases per thread (0: off)
 template <int LOG2N, bool SPLIT, int OPAQUE = 0, int LOG2E = 4, int ILV = 0, int P = 0,
-          class TWP = const cd *, bool LINEAR = false, bool HALF_IN = false, class EPI = NoEpi>
+          class TWP = const cd *, bool LINEAR = false, bool HALF_IN = false, class EPI = NoEpi,
+          int PREW = 0>
 __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw, double *lre,
                                          double *lim, bool first_exchange = true,
-                                         const EPI &epi = EPI()) {
+                                         const EPI &epi = EPI(), const cd *wpre = nullptr) {
   using G = Geo<LOG2N, LOG2E>;
   if constexpr (OPAQUE && P == 0 && G::NPASS > 1) {
     t = opaque_int(t);
@@ -450,12 +466,23 @@ __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw,
       pass_exchange<G::N, G::E, G::T, RP, NSP, SPLIT, ILV, LINEAR>(v, t, lre, lim,
                                                                     first_exchange && P == 1);
     }
+    // PREW: the next pass's bases, read now
+    constexpr int PN = P + 1 < G::NPASS ? P + 1 : P;
+    constexpr int RN = G::radix(PN), NSN = G::ns(PN), BN = G::E / RN;
+    constexpr bool PRE_NEXT = PREW >= BN && P + 1 < G::NPASS && NSN > 1;
+    cd wn[PRE_NEXT ? BN : 1];
+    if constexpr (PRE_NEXT) {
+#pragma unroll
+      for (int b = 0; b < BN; ++b) wn[b] = pass_base<G::N, RN, NSN>(tw, t + b * G::T);
+    }
+    constexpr bool USE_PRE = PREW >= G::E / R && P > 0 && NS > 1;
     if constexpr (P == G::NPASS - 1)
-      pass_compute<G::N, G::E, G::T, R, NS, HALF_IN && P == 0, EPI>(v, t, tw, epi);
+      pass_compute<G::N, G::E, G::T, R, NS, HALF_IN && P == 0, EPI, USE_PRE>(v, t, tw, epi, wpre);
     else
-      pass_compute<G::N, G::E, G::T, R, NS, HALF_IN && P == 0>(v, t, tw);
-    fft_regs<LOG2N, SPLIT, 0, LOG2E, ILV, P + 1, TWP, LINEAR, false, EPI>(v, t, tw, lre, lim,
-                                                                         first_exchange, epi);
+      pass_compute<G::N, G::E, G::T, R, NS, HALF_IN && P == 0, NoEpi, USE_PRE>(v, t, tw, NoEpi(),
+                                                                                wpre);
+    fft_regs<LOG2N, SPLIT, 0, LOG2E, ILV, P + 1, TWP, LINEAR, false, EPI, PREW>(
+        v, t, tw, lre, lim, first_exchange, epi, PRE_NEXT ? wn : nullptr);
   }
 }
 

@@ -190,6 +190,15 @@ struct ChirpOutEpi {
 // 2.23 / 2.24-2.27 and 1.83 / 1.76 / 1.77; 2^13 (3000, 4093) 2.16-2.18 /
 // 2.17-2.19 / 2.24 and 1.83 / 1.91 / 1.98; 2^14 (8191) 2.35 / 2.27-2.28 / 2.26.
 // GDSP_BLU_NOEPI / GDSP_BLU_OUT_AFTER force 0 / at most 1 (experiments).
+// Twiddle-base prefetch (fft_regs PREW) for passes with one base per thread;
+// not at M = 2^10, where it costs that kernel a wave per SIMD
+#ifndef GDSP_NO_PREW
+constexpr int kPwPrew = 1;
+__host__ __device__ constexpr int blu_prew(int log2m) { return log2m == 10 ? 0 : 1; }
+#else
+constexpr int kPwPrew = 0;
+__host__ __device__ constexpr int blu_prew(int) { return 0; }
+#endif
 __host__ __device__ constexpr int blu_epi_mode(int log2m) {
 #if defined(GDSP_BLU_NOEPI)
   return 0 * log2m;
@@ -247,10 +256,11 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
   if constexpr (EPI >= 1) {
     // x bhat, conj: fused into FFT 1's last pass, each butterfly's factors
     // loaded ahead of its arithmetic
-    fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, HALF, BhatEpi<G::T>>(
+    fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, HALF, BhatEpi<G::T>, blu_prew(LOG2M)>(
         v, t, twm, lre, lim, true, BhatEpi<G::T>{bhat + t});
   } else {
-    fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, HALF>(v, t, twm, lre, lim, true);
+    fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, HALF, NoEpi, blu_prew(LOG2M)>(
+        v, t, twm, lre, lim, true);
 #pragma unroll
     for (int k = 0; k < G::E; ++k) v[k] = conjg(cmul(v[k], bhat[t + k * G::T]));
   }
@@ -259,9 +269,10 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
     const ChirpOutEpi<G::T, KH, INV> oe{opaque_ptr(chirp), valid ? out + g * n : nullptr,
                                         opaque_int(t), n, scale};
     fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, false,
-             ChirpOutEpi<G::T, KH, INV>>(v, t, twm, lre, lim, false, oe);
+             ChirpOutEpi<G::T, KH, INV>, blu_prew(LOG2M)>(v, t, twm, lre, lim, false, oe);
   } else {
-    fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true>(v, t, twm, lre, lim, false);
+    fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, false, NoEpi, blu_prew(LOG2M)>(
+        v, t, twm, lre, lim, false);
     chirp = opaque_ptr(chirp);
     const int to = opaque_int(t);
     if (valid) {
@@ -497,9 +508,8 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_ker
 #pragma unroll
     for (int k = 0; k < H; ++k) carry[k] = c2[k];
     if constexpr (PF)
-      fft_regs<LOG2F, SPLIT, 2, LOG2E, 0, 0, const cd *, kPwLinear>(v, opaque_int(t),
-                                                                    (const cd *)twl, lre, lim,
-                                                                    it == 0);
+      fft_regs<LOG2F, SPLIT, 2, LOG2E, 0, 0, const cd *, kPwLinear, false, NoEpi, kPwPrew>(
+          v, opaque_int(t), (const cd *)twl, lre, lim, it == 0);
     else
       fft_regs<LOG2F, SPLIT, 1, LOG2E, 0, 0, const cd *, kPwLinear>(v, opaque_int(t), tw, lre,
                                                                     lim, it == 0);
