@@ -278,8 +278,11 @@ def measure(wl: dict, c: Ctx) -> dict:
         wl["step"]()
         ends[i].record(c.stream)
     torch.cuda.synchronize()
-    c.barrier()
+    # each rank's clock stops when its own GPU work is done; the closing
+    # barrier's latency (an RCCL round trip at N > 1) is not step time, and
+    # the max over ranks below is the slowest rank's finish
     elapsed = time.perf_counter() - t0
+    c.barrier()
     if c.world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64,
                          device=c.dev if c.backend == "nccl" else "cpu")
