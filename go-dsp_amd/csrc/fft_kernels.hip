@@ -199,11 +199,15 @@ __host__ __device__ constexpr int blu_prew(int log2m) { return log2m == 10 ? 0 :
 constexpr int kPwPrew = 0;
 __host__ __device__ constexpr int blu_prew(int) { return 0; }
 #endif
-__host__ __device__ constexpr int blu_epi_mode(int log2m) {
+__host__ __device__ constexpr int blu_epi_mode(int log2m, int log2e) {
 #if defined(GDSP_BLU_NOEPI)
-  return 0 * log2m;
+  return 0 * log2m * log2e;
 #else
-  const int m = (log2m == 5 || log2m == 6 || log2m == 10) ? 0 : (log2m == 12 || log2m == 14) ? 1 : 2;
+  // (the 16-points-per-thread kernels of M = 2^13 / 2^14, GDSP_BLU_E16=1: none;
+  // with both chirpz3000 took 4.86 against 3.40 ms)
+  const int m = (log2m == 5 || log2m == 6 || log2m == 10 || (log2m >= 13 && log2e == 4))   ? 0
+                : (log2m == 12 || log2m == 14) ? 1
+                                               : 2;
 #if defined(GDSP_BLU_OUT_AFTER)
   return m < 1 ? m : 1;
 #else
@@ -252,7 +256,7 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
       v[k] = cmul(x, chirp[idx]);
     }
   }
-  constexpr int EPI = blu_epi_mode(LOG2M);
+  constexpr int EPI = blu_epi_mode(LOG2M, LOG2E);
   if constexpr (EPI >= 1) {
     // x bhat, conj: fused into FFT 1's last pass, each butterfly's factors
     // loaded ahead of its arithmetic
