@@ -221,11 +221,18 @@ __host__ __device__ constexpr int blu_epi_mode(int log2m, int log2e) {
 //   r = IFFT_M(C) = conj(FFT_M(conj(C))) (1/M folded into bhat),
 //   X = r * conj(w), first n.  chirp[k] = conj(w_k) = exp(-i pi k^2/n).
 // Inverse (fft.IFFT of non-power-of-2 length): conj in, conj + 1/n out.
-template <int LOG2M, bool INV, bool SPLIT, int LOG2E = 4>
+//
+// PARTS (n > M/2, where bluestein.go:70's M would exceed one kernel): the
+// outputs are split into parts of kpart, part blockIdx.y computing
+// X[k0 + k], k < kpart, k0 = blockIdx.y * kpart, by its own circular
+// convolution c_p[m mod M] = w_(k0 + m), m in [-(n-1), kpart-1], which does not
+// wrap as long as n + kpart - 1 <= M (bhat + blockIdx.y * M holds FFT_M(c_p)/M).
+// The input then fills more than half of M, so only the output side is pruned.
+template <int LOG2M, bool INV, bool SPLIT, int LOG2E = 4, bool PARTS = false>
 __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
     const cd *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
     const cd *__restrict__ twm, const cd *__restrict__ chirp, const cd *__restrict__ bhat,
-    double scale) {
+    double scale, int64_t kpart) {
   using G = Geo<LOG2M, LOG2E>;
   __shared__ double lds[(SPLIT ? 1 : 2) * G::LDS_DOUBLES];
   const int lt = threadIdx.x;
@@ -239,18 +246,30 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
   // and no output, so the first pass of FFT 1 and the last of FFT 2 are pruned
 #ifndef GDSP_BLU_NOPRUNE
   constexpr int KH = G::E > 1 ? G::E / 2 : G::E;
-  constexpr bool HALF = G::E >= 4;
+  constexpr bool HALF = G::E >= 4 && !PARTS;
 #else
   constexpr int KH = G::E;
   constexpr bool HALF = false;
 #endif
+  constexpr int KIN = PARTS ? G::E : KH;
+  // this block's outputs: X[k0 + k], k < nout
+  int64_t nout = n;
+  const cd *ochirp = chirp;
+  cd *orow = valid ? out + g * n : nullptr;
+  if constexpr (PARTS) {
+    const int64_t k0 = (int64_t)blockIdx.y * kpart;
+    nout = n - k0 < kpart ? n - k0 : kpart;
+    ochirp += k0;
+    if (orow) orow += k0;
+    bhat += (int64_t)blockIdx.y * G::N;
+  }
   cd v[G::E];
   const cd *src = in + g * n;
 #pragma unroll
   for (int k = 0; k < G::E; ++k) {
     const int idx = t + k * G::T;
     v[k] = {0.0, 0.0};
-    if (k < KH && valid && idx < n) {
+    if (k < KIN && valid && idx < n) {
       cd x = ld_nt(&src[idx]);
       if constexpr (INV) x.y = -x.y;
       v[k] = cmul(x, chirp[idx]);
@@ -270,22 +289,21 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
   }
   if constexpr (EPI == 2) {
     // postmultiply and store: fused into FFT 2's last pass the same way
-    const ChirpOutEpi<G::T, KH, INV> oe{opaque_ptr(chirp), valid ? out + g * n : nullptr,
-                                        opaque_int(t), n, scale};
+    const ChirpOutEpi<G::T, KH, INV> oe{opaque_ptr(ochirp), orow, opaque_int(t), nout, scale};
     fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, false,
              ChirpOutEpi<G::T, KH, INV>, blu_prew(LOG2M)>(v, t, twm, lre, lim, false, oe);
   } else {
     fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, false, NoEpi, blu_prew(LOG2M)>(
         v, t, twm, lre, lim, false);
-    chirp = opaque_ptr(chirp);
+    ochirp = opaque_ptr(ochirp);
     const int to = opaque_int(t);
-    if (valid) {
-      cd *dst = out + g * n;
+    if (orow) {
+      cd *dst = orow;
 #pragma unroll
       for (int k = 0; k < KH; ++k) {
         const int idx = to + k * G::T;
-        if (idx < n) {
-          cd y = cmul(conjg(v[k]), chirp[idx]);
+        if (idx < nout) {
+          cd y = cmul(conjg(v[k]), ochirp[idx]);
           if constexpr (INV) y = {y.x * scale, -y.y * scale};
           st_nt(&dst[idx], y);
         }
@@ -923,14 +941,34 @@ static hipError_t launch_blu_t(const cd *in, cd *out, int64_t n, int64_t batch, 
       using G5 = Geo<LOG2M, 5>;
       const int64_t nb5 = (batch + G5::TPW - 1) / G5::TPW;
       hipLaunchKernelGGL((bluestein_kernel<LOG2M, INV, true, 5>), dim3((unsigned)nb5),
-                         dim3(G5::WG), 0, s, in, out, n, batch, twm, chirp, bhat, scale);
+                         dim3(G5::WG), 0, s, in, out, n, batch, twm, chirp, bhat, scale,
+                         (int64_t)0);
       return hipGetLastError();
     }
   }
   using G = Geo<LOG2M>;
   const int64_t nblk = (batch + G::TPW - 1) / G::TPW;
   hipLaunchKernelGGL((bluestein_kernel<LOG2M, INV, true>), dim3((unsigned)nblk), dim3(G::WG), 0,
-                     s, in, out, n, batch, twm, chirp, bhat, scale);
+                     s, in, out, n, batch, twm, chirp, bhat, scale, (int64_t)0);
+  return hipGetLastError();
+}
+
+// Output-split chirp-z on M = 16384 (bluestein_kernel PARTS): `parts` launches'
+// worth of blocks in one grid (blockIdx.y = part), bhat holding parts * M.
+hipError_t launch_bluestein_parts(bool inv, const cd *in, cd *out, int64_t n, int64_t batch,
+                                  int parts, int64_t kpart, const cd *twm, const cd *chirp,
+                                  const cd *bhat, double scale, hipStream_t s) {
+  using G = Geo<14, 5>;
+  if (parts < 1 || parts > 65535 || kpart < 1 || kpart > G::N / 2 || n + kpart - 1 > G::N ||
+      kpart * parts < n)
+    return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((batch + G::TPW - 1) / G::TPW), (unsigned)parts);
+  if (inv)
+    hipLaunchKernelGGL((bluestein_kernel<14, true, true, 5, true>), grid, dim3(G::WG), 0, s, in,
+                       out, n, batch, twm, chirp, bhat, scale, kpart);
+  else
+    hipLaunchKernelGGL((bluestein_kernel<14, false, true, 5, true>), grid, dim3(G::WG), 0, s, in,
+                       out, n, batch, twm, chirp, bhat, scale, kpart);
   return hipGetLastError();
 }
 

@@ -330,6 +330,11 @@ struct gdsp_plan {
   // shuffle chirp-z (bluestein_shfl.hip) for M = 8192: bhat in the kernel's
   // register order, bhats[r 256 + t] = bhat[bluestein_shfl_bin(t, r)]
   cd *bhats = nullptr;
+  // output-split chirp-z (bluestein_kernel PARTS): n in (8192, 16384] whose
+  // NextPowerOf2(2n-1) = 32768 exceeds one kernel runs as `parts` fused
+  // convolutions of M = 16384, each giving kpart outputs; bhat holds parts * M
+  int parts = 1;
+  int64_t kpart = 0;
 };
 
 namespace {
@@ -666,6 +671,26 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   p->m = next_pow2_ref(2 * n - 1);
   p->log2m = ilog2(p->m);
   p->kind = p->log2m <= gdsp::kMaxLdsLog2 ? KIND_BLUESTEIN : KIND_BLUESTEIN_COMPOSED;
+  if (p->kind == KIND_BLUESTEIN_COMPOSED && !chirpz && !p->mplan) {
+    // Output-split chirp-z: X[k0 + k] for k < kpart needs a circular
+    // convolution of length >= n + kpart - 1 only (bluestein.go:70 sizes it for
+    // all n outputs, 2n - 1), so P parts of kpart = ceil(n/P) run on the
+    // one-kernel M = 16384 wherever n + kpart - 1 <= 16384 with P <= 8
+    // (n <= 14563); the composed chirp-z over 32768 moves ~8 HBM passes of M
+    // per transform. GDSP_BLU_NOPARTS=1 keeps the composed path.
+    const int64_t mk = (int64_t)1 << gdsp::kMaxLdsLog2;
+    for (int parts = 2; parts <= 8 && !getenv("GDSP_BLU_NOPARTS"); ++parts) {
+      const int64_t kp = (n + parts - 1) / parts;
+      if (n + kp - 1 <= mk) {
+        p->m = mk;
+        p->log2m = gdsp::kMaxLdsLog2;
+        p->kind = KIND_BLUESTEIN;
+        p->parts = parts;
+        p->kpart = kp;
+        break;
+      }
+    }
+  }
   if (p->kind == KIND_BLUESTEIN_COMPOSED && !chirpz && !getenv("GDSP_CHIRPZ_POW2")) {
     // The composed chirp-z is HBM-bound, so its cost follows M: take the
     // smallest M >= 2n - 1 with a three-pass split (power-of-2 or
@@ -689,7 +714,8 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
     }
   }
   if (!p->mplan) STCHK(get_plan_locked(dev, p->m, &p->mplan));
-  std::vector<cd> w((size_t)n), chirp((size_t)n), b((size_t)p->m, cd{0.0, 0.0});
+  std::vector<cd> w((size_t)n), chirp((size_t)n),
+      b((size_t)p->m * (size_t)p->parts, cd{0.0, 0.0});
   for (int64_t k = 0; k < n; ++k) {
     double sn = 0.0, cs = 1.0;
     if (k != 0) {
@@ -700,21 +726,35 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
     w[(size_t)k] = {cs, sn};
     chirp[(size_t)k] = {cs, -sn};
   }
-  for (int64_t i = 0; i < n; ++i) {  // bluestein.go:78-85
-    b[(size_t)i] = w[(size_t)i];
-    if (i != 0) b[(size_t)(p->m - i)] = w[(size_t)i];
+  if (p->parts == 1) {
+    for (int64_t i = 0; i < n; ++i) {  // bluestein.go:78-85
+      b[(size_t)i] = w[(size_t)i];
+      if (i != 0) b[(size_t)(p->m - i)] = w[(size_t)i];
+    }
+  } else {
+    // part q: c[j mod M] = w_(k0 + j), j in [-(n-1), kpart-1], k0 = q kpart
+    // (w_(-i) = w_i; indices k0 + j >= n feed no wanted output)
+    for (int q = 0; q < p->parts; ++q) {
+      cd *c = b.data() + (size_t)q * (size_t)p->m;
+      const int64_t k0 = q * p->kpart;
+      for (int64_t j = -(n - 1); j < p->kpart; ++j) {
+        const int64_t i = k0 + j < 0 ? -(k0 + j) : k0 + j;
+        if (i < n) c[(size_t)(j < 0 ? p->m + j : j)] = w[(size_t)i];
+      }
+    }
   }
+  const size_t nb = (size_t)p->m * (size_t)p->parts;
   HIPCHK(hipMalloc((void **)&p->chirp, (size_t)n * sizeof(cd)));
   hipStream_t s = thread_stream(dev);
   STCHK(copy_h2d(p->chirp, chirp.data(), (size_t)n * sizeof(cd), s));
-  HIPCHK(hipMalloc((void **)&p->bhat, (size_t)p->m * sizeof(cd)));
+  HIPCHK(hipMalloc((void **)&p->bhat, nb * sizeof(cd)));
   cd *db = nullptr;
-  HIPCHK(hipMalloc((void **)&db, (size_t)p->m * sizeof(cd)));
-  STCHK(copy_h2d(db, b.data(), (size_t)p->m * sizeof(cd), s));
+  HIPCHK(hipMalloc((void **)&db, nb * sizeof(cd)));
+  STCHK(copy_h2d(db, b.data(), nb * sizeof(cd), s));
   // FFT_M(b) on the device with the engine itself, then fold the IFFT's 1/M
-  int st = exec_plan(p->mplan, db, p->bhat, 1, false, gdsp::LOAD_COMPLEX, s);
+  int st = exec_plan(p->mplan, db, p->bhat, p->parts, false, gdsp::LOAD_COMPLEX, s);
   if (st == GDSP_OK) {
-    hipError_t e = gdsp::launch_scale(p->bhat, p->m, 1.0 / (double)p->m, s);
+    hipError_t e = gdsp::launch_scale(p->bhat, (int64_t)nb, 1.0 / (double)p->m, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) st = fail(GDSP_ERR_HIP, hipGetErrorString(e));
   }
@@ -1056,6 +1096,11 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
                                            p->bhats, scale, s));
         return GDSP_OK;
       }
+      if (p->kind == KIND_BLUESTEIN && p->parts > 1) {
+        HIPCHK(gdsp::launch_bluestein_parts(inv, src, out, p->n, batch, p->parts, p->kpart,
+                                            p->mplan->tw, p->chirp, p->bhat, scale, s));
+        return GDSP_OK;
+      }
       if (p->kind == KIND_BLUESTEIN) {
         HIPCHK(gdsp::launch_bluestein(p->log2m, inv, src, out, p->n, batch, p->mplan->tw, p->chirp,
                                       p->bhat, scale, s));
@@ -1281,7 +1326,9 @@ int gdsp_fft2_device(const void *d_in, void *d_out, int64_t rows, int64_t cols, 
     // row pass (contiguous rows, any length) -> work; column pass on
     // row-segment tiles: one kernel for rows <= 512, otherwise the four-step
     // split rows = R1*R2 (A in place on work, B from work into out)
-    STCHK(exec_plan(pc, d_in, work, rows, inv, gdsp::LOAD_COMPLEX, s));
+    static const bool oop_env = getenv("GDSP_FFT2_OOP") != nullptr;
+    const bool oop = oop_env && d_in != d_out && lr > gdsp::kColMaxLog2;
+    if (!oop) STCHK(exec_plan(pc, d_in, work, rows, inv, gdsp::LOAD_COMPLEX, s));
     const double sc = 1.0 / (double)rows;
     if (lr <= gdsp::kColMaxLog2) {
       HIPCHK(gdsp::launch_colfft(lr, inv, 0, inv, work, (cd *)d_out, cols, 1, 0, 1, 0, 1,
@@ -1292,8 +1339,16 @@ int gdsp_fft2_device(const void *d_in, void *d_out, int64_t rows, int64_t cols, 
       STCHK(get_plan((int64_t)1 << l1, &p1));
       STCHK(get_plan((int64_t)1 << l2, &p2));
       const int64_t R1 = (int64_t)1 << l1, R2 = (int64_t)1 << l2;
-      HIPCHK(gdsp::launch_colfft(l1, inv, 1, false, work, work, cols, R2, 1, R2, 1, R2, p1->tw,
-                                 pr->tw, lr, 1.0, 1, 0, s));
+      if (oop) {
+        // experiment: every pass out of place (rows -> out, A out -> work, B
+        // work -> out)
+        STCHK(exec_plan(pc, d_in, (cd *)d_out, rows, inv, gdsp::LOAD_COMPLEX, s));
+        HIPCHK(gdsp::launch_colfft(l1, inv, 1, false, (cd *)d_out, work, cols, R2, 1, R2, 1, R2,
+                                   p1->tw, pr->tw, lr, 1.0, 1, 0, s));
+      } else {
+        HIPCHK(gdsp::launch_colfft(l1, inv, 1, false, work, work, cols, R2, 1, R2, 1, R2, p1->tw,
+                                   pr->tw, lr, 1.0, 1, 0, s));
+      }
       HIPCHK(gdsp::launch_colfft(l2, false, 0, inv, work, (cd *)d_out, cols, R1, R2, 1, 1, R1,
                                  p2->tw, nullptr, lr, sc, 1, 0, s));
     }
@@ -1498,6 +1553,7 @@ int gdsp_plan_kind(const gdsp_plan *plan) { return plan ? plan->kind : -1; }
 int gdsp_plan_wave_q(const gdsp_plan *plan) { return plan ? plan->wq : 0; }
 
 int gdsp_plan_shfl(const gdsp_plan *plan) { return plan && plan->bhats ? 1 : 0; }
+int gdsp_plan_parts(const gdsp_plan *plan) { return plan ? plan->parts : 0; }
 
 int gdsp_plan_info(const gdsp_plan *plan, int64_t *n, int64_t *m, int64_t *n1, int64_t *n2,
                    int *runtime_compiled) {

@@ -53,6 +53,8 @@ class Plan:
         self.wave_q = int(lib().gdsp_plan_wave_q(self.handle))
         # 1: the M = 8192 chirp-z kernel with in-wave exchanges (GDSP_BLU_SHFL=1)
         self.shfl = int(lib().gdsp_plan_shfl(self.handle))
+        # output parts of the chirp-z kernel (> 1: n in (8192, 14563] on M = 16384)
+        self.parts = int(lib().gdsp_plan_parts(self.handle))
 
 
 _plans: dict = {}

@@ -233,6 +233,11 @@ int gdsp_plan_wave_q(const gdsp_plan *plan);
  * whose FFTs keep one of their two exchanges inside the wavefront
  * (bluestein_shfl.hip, opt-in GDSP_BLU_SHFL=1), else 0. */
 int gdsp_plan_shfl(const gdsp_plan *plan);
+/* Output parts of a kind-3 plan: 1 for the one-convolution chirp-z of
+ * bluestein.go:68-94; P > 1 when n in (8192, 14563] (NextPowerOf2(2n-1) =
+ * 32768, beyond one kernel) runs as P fused convolutions of M = 16384, each
+ * giving ceil(n/P) of the outputs (GDSP_BLU_NOPARTS=1: composed chirp-z). */
+int gdsp_plan_parts(const gdsp_plan *plan);
 
 /* Batched C2C on device buffers: d_in/d_out hold batch*n complex128 (may
  * alias only if equal). inverse != 0 → IFFT semantics (1/n scaling). */

@@ -293,7 +293,9 @@ def test_plan_kinds(gdsp):
     assert D.plan(44100).kind == 6  # 25 x 1764: mixed four-step (single-radix columns)
     assert D.plan(5000).kind == 5  # a compiled specialisation above 4096 (25*25*8)
     assert D.plan(5400).kind == 5  # smooth, no compiled specialisation: hipRTC-compiled one
-    assert D.plan(8209).kind == 4  # prime, M = 32768: composed Bluestein
+    # prime, NextPowerOf2(2n-1) = 32768: output-split chirp-z, 2 parts on M = 16384
+    assert D.plan(8209).kind == 3 and D.plan(8209).parts == 2 and D.plan(8209).m == 16384
+    assert D.plan(16411).kind == 4  # prime beyond the parts' reach: composed Bluestein
     assert D.plan(8191 * 64).kind == 6  # power-of-2 columns, fused chirp-z rows of 8191
     assert D.plan(3000, chirpz=True).kind == 3
     assert D.plan(10000, chirpz=True).kind == 4
@@ -766,9 +768,10 @@ def test_ensure_radix2_factors_then_fft(gdsp, oracle, n):
 def test_chirpz_convolution_length_selection():
     """Which convolution length M the composed chirp-z takes (gdsp_plan_info),
     and that every selectable path agrees with the oracle: by default 8209
-    and 16411 run on a smooth M (<= 0.55 of the power of 2), GDSP_CHIRPZ_POW2=1
-    keeps the reference's NextPowerOf2(2n-1) (bluestein.go:70), and
-    GDSP_BLU_UNFUSED=1 takes the unfused composition."""
+    runs as the output-split chirp-z (2 parts on M = 16384) and 16411 on a
+    smooth M (<= 0.55 of the power of 2); GDSP_BLU_NOPARTS=1 puts 8209 on the
+    smooth M too, GDSP_CHIRPZ_POW2=1 keeps the reference's NextPowerOf2(2n-1)
+    (bluestein.go:70), and GDSP_BLU_UNFUSED=1 takes the unfused composition."""
     code = r'''
 import importlib, os, sys
 sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
@@ -777,12 +780,18 @@ g = importlib.import_module("go-dsp_amd")
 D = importlib.import_module("go-dsp_amd.device")
 import torch
 pow2 = os.environ.get("GDSP_CHIRPZ_POW2") == "1"
+parts = os.environ.get("GDSP_BLU_NOPARTS") != "1"
 rng = np.random.default_rng(8)
 for n in (8209, 16411):
     p = D.plan(n)
-    assert p.kind == 4, (n, p.kind)
     ref_m = 1 << (2 * n - 2).bit_length()
-    if pow2:
+    if parts and n == 8209:
+        assert (p.kind, p.parts, p.m) == (3, 2, 16384), (n, p.kind, p.parts, p.m)
+    else:
+        assert p.kind == 4 and p.parts == 1, (n, p.kind, p.parts)
+    if p.kind == 3:
+        pass
+    elif pow2:
         assert p.m == ref_m, (n, p.m)
     else:
         assert p.m & (p.m - 1) != 0 and 2 * n - 1 <= p.m <= 0.55 * ref_m, (n, p.m)
@@ -795,8 +804,41 @@ for n in (8209, 16411):
         assert err < 1e-9, (n, inv, err)
 print("ok", os.environ.get("GDSP_CHIRPZ_POW2"), os.environ.get("GDSP_BLU_UNFUSED"))
 '''
-    for extra in ({}, {"GDSP_CHIRPZ_POW2": "1"}, {"GDSP_BLU_UNFUSED": "1"}):
+    for extra in ({}, {"GDSP_BLU_NOPARTS": "1"},
+                  {"GDSP_CHIRPZ_POW2": "1", "GDSP_BLU_NOPARTS": "1"},
+                  {"GDSP_BLU_UNFUSED": "1", "GDSP_BLU_NOPARTS": "1"}):
         env = dict(os.environ, REPO=REPO, **extra)
         r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300,
                            env=env)
         assert r.returncode == 0 and "ok" in r.stdout, (extra, r.stdout + r.stderr[-3000:])
+
+
+# primes whose NextPowerOf2(2n-1) is 32768: 2 parts (8209, 10007, 10909), 3
+# (11003, 12281), 4 (12289), 6 (13999), 8 (14563, the largest length with P <= 8)
+PARTS = [(8209, 2), (10007, 2), (10909, 2), (11003, 3), (12281, 3), (12289, 4), (13999, 6),
+         (14563, 8)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,parts", PARTS)
+def test_chirpz_output_parts_vs_oracle(gdsp, oracle, n, parts):
+    """Output-split chirp-z (bluestein_kernel PARTS): X[k0 + k], k < ceil(n/P),
+    from P fused circular convolutions of M = 16384 >= n + ceil(n/P) - 1, for
+    lengths whose reference M = NextPowerOf2(2n-1) = 32768 exceeds one kernel
+    (bluestein.go:68-94). Forward, inverse and real input against the oracle
+    (which runs the reference's M = 32768), batch 3 so row offsets are covered."""
+    import torch
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    p = D.plan(n)
+    assert (p.kind, p.parts, p.m) == (3, parts, 16384), (n, p.kind, p.parts, p.m)
+    rng = np.random.default_rng(n)
+    x = rng.uniform(-1, 1, (3, n)) + 1j * rng.uniform(-1, 1, (3, n))
+    xt = torch.from_numpy(x).cuda()
+    assert row_nrel(D.fft_batch(xt).cpu().numpy(), oracle.fft_rows(x)) < TOL
+    assert row_nrel(D.fft_batch(xt, inverse=True).cpu().numpy(), oracle.ifft_rows(x)) < TOL
+    xr = rng.uniform(-1, 1, (2, n))
+    assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
+    # an output tail the last part leaves partly empty, and the forced
+    # chirp-z plan (reference M, composed) agreeing with it
+    yc = D.fft_batch(xt[:1], chirpz=True).cpu().numpy()
+    assert row_nrel(D.fft_batch(xt[:1]).cpu().numpy(), yc) < TOL
