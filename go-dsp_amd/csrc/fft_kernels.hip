@@ -953,23 +953,35 @@ static hipError_t launch_blu_t(const cd *in, cd *out, int64_t n, int64_t batch, 
   return hipGetLastError();
 }
 
-// Output-split chirp-z on M = 16384 (bluestein_kernel PARTS): `parts` launches'
-// worth of blocks in one grid (blockIdx.y = part), bhat holding parts * M.
-hipError_t launch_bluestein_parts(bool inv, const cd *in, cd *out, int64_t n, int64_t batch,
-                                  int parts, int64_t kpart, const cd *twm, const cd *chirp,
-                                  const cd *bhat, double scale, hipStream_t s) {
-  using G = Geo<14, 5>;
+// Output-split chirp-z on M = 8192 / 16384 (bluestein_kernel PARTS): `parts`
+// launches' worth of blocks in one grid (blockIdx.y = part), bhat holding
+// parts * M.
+template <int LOG2M>
+static hipError_t launch_blu_parts_t(bool inv, const cd *in, cd *out, int64_t n, int64_t batch,
+                                     int parts, int64_t kpart, const cd *twm, const cd *chirp,
+                                     const cd *bhat, double scale, hipStream_t s) {
+  using G = Geo<LOG2M, 5>;
   if (parts < 1 || parts > 65535 || kpart < 1 || kpart > G::N / 2 || n + kpart - 1 > G::N ||
       kpart * parts < n)
     return hipErrorInvalidValue;
   const dim3 grid((unsigned)((batch + G::TPW - 1) / G::TPW), (unsigned)parts);
   if (inv)
-    hipLaunchKernelGGL((bluestein_kernel<14, true, true, 5, true>), grid, dim3(G::WG), 0, s, in,
-                       out, n, batch, twm, chirp, bhat, scale, kpart);
+    hipLaunchKernelGGL((bluestein_kernel<LOG2M, true, true, 5, true>), grid, dim3(G::WG), 0, s,
+                       in, out, n, batch, twm, chirp, bhat, scale, kpart);
   else
-    hipLaunchKernelGGL((bluestein_kernel<14, false, true, 5, true>), grid, dim3(G::WG), 0, s, in,
-                       out, n, batch, twm, chirp, bhat, scale, kpart);
+    hipLaunchKernelGGL((bluestein_kernel<LOG2M, false, true, 5, true>), grid, dim3(G::WG), 0, s,
+                       in, out, n, batch, twm, chirp, bhat, scale, kpart);
   return hipGetLastError();
+}
+
+hipError_t launch_bluestein_parts(int log2m, bool inv, const cd *in, cd *out, int64_t n,
+                                  int64_t batch, int parts, int64_t kpart, const cd *twm,
+                                  const cd *chirp, const cd *bhat, double scale, hipStream_t s) {
+  if (log2m == 13)
+    return launch_blu_parts_t<13>(inv, in, out, n, batch, parts, kpart, twm, chirp, bhat, scale, s);
+  if (log2m == 14)
+    return launch_blu_parts_t<14>(inv, in, out, n, batch, parts, kpart, twm, chirp, bhat, scale, s);
+  return hipErrorInvalidValue;
 }
 
 #define GDSP_BLU_CASE(L)                                                                     \

@@ -466,8 +466,28 @@ int build_mixed(int dev, int64_t n, const std::vector<int> &rad, gdsp_plan *p) {
 // kernel (M = NextPowerOf2(2m - 1) <= 16384), so a length with a large prime
 // factor but a smooth cofactor (8191 * 64) still gets a three-pass four-step
 // instead of the composed chirp-z over 2n-point rows.
+// Output parts of the split chirp-z for n (see gdsp_plan::parts): the fewest
+// P <= 8 with n + ceil(n/P) - 1 <= 16384 where NextPowerOf2(2n-1) exceeds
+// one kernel, else 0 (composed chirp-z). P = 8 (n <= 14563) measured 10.8
+// against 11.5 ms for the composed chirp-z per 2^27 samples, P = 2 4x faster.
+int chirpz_parts(int64_t n) {
+  static const bool off = getenv("GDSP_BLU_NOPARTS") != nullptr;
+  const int64_t mk = (int64_t)1 << gdsp::kMaxLdsLog2;
+  if (off || next_pow2_ref(2 * n - 1) <= mk) return 0;
+  for (int parts = 2; parts <= 8; ++parts)
+    if (n + (n + parts - 1) / parts - 1 <= mk) return parts;
+  return 0;
+}
+
 bool one_kernel_len(int64_t m) {
   if (m < 2) return false;
+  if (chirpz_parts(m)) {
+    // only a prime builds as the output-split chirp-z plan: a composite in
+    // (8192, 14563] has a four-step split, which build_plan takes first
+    bool prime = true;
+    for (int64_t d = 2; d * d <= m && prime; ++d) prime = m % d != 0;
+    if (prime) return true;
+  }
   if (is_pow2(m)) return ilog2(m) <= gdsp::kMaxLdsLog2;
   std::vector<int> rad;
   if (mixed_radices(m, rad)) return true;
@@ -678,18 +698,23 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
     // one-kernel M = 16384 wherever n + kpart - 1 <= 16384 with P <= 8
     // (n <= 14563); the composed chirp-z over 32768 moves ~8 HBM passes of M
     // per transform. GDSP_BLU_NOPARTS=1 keeps the composed path.
-    const int64_t mk = (int64_t)1 << gdsp::kMaxLdsLog2;
-    for (int parts = 2; parts <= 8 && !getenv("GDSP_BLU_NOPARTS"); ++parts) {
-      const int64_t kp = (n + parts - 1) / parts;
-      if (n + kp - 1 <= mk) {
-        p->m = mk;
-        p->log2m = gdsp::kMaxLdsLog2;
-        p->kind = KIND_BLUESTEIN;
-        p->parts = parts;
-        p->kpart = kp;
-        break;
-      }
+    if (const int parts = chirpz_parts(n)) {
+      p->m = (int64_t)1 << gdsp::kMaxLdsLog2;
+      p->log2m = gdsp::kMaxLdsLog2;
+      p->kind = KIND_BLUESTEIN;
+      p->parts = parts;
+      p->kpart = (n + parts - 1) / parts;
     }
+  }
+  static const bool parts13 = getenv("GDSP_BLU_PARTS13") != nullptr;
+  if (parts13 && p->kind == KIND_BLUESTEIN && p->log2m == 14 && !chirpz &&
+      n + (n + 1) / 2 - 1 <= 8192) {
+    // experiment: n in (4096, 5461] as 2 parts on M = 8192 instead of one
+    // convolution of 16384
+    p->m = 8192;
+    p->log2m = 13;
+    p->parts = 2;
+    p->kpart = (n + 1) / 2;
   }
   if (p->kind == KIND_BLUESTEIN_COMPOSED && !chirpz && !getenv("GDSP_CHIRPZ_POW2")) {
     // The composed chirp-z is HBM-bound, so its cost follows M: take the
@@ -1097,8 +1122,9 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
         return GDSP_OK;
       }
       if (p->kind == KIND_BLUESTEIN && p->parts > 1) {
-        HIPCHK(gdsp::launch_bluestein_parts(inv, src, out, p->n, batch, p->parts, p->kpart,
-                                            p->mplan->tw, p->chirp, p->bhat, scale, s));
+        HIPCHK(gdsp::launch_bluestein_parts(p->log2m, inv, src, out, p->n, batch, p->parts,
+                                            p->kpart, p->mplan->tw, p->chirp, p->bhat, scale,
+                                            s));
         return GDSP_OK;
       }
       if (p->kind == KIND_BLUESTEIN) {
@@ -1326,9 +1352,7 @@ int gdsp_fft2_device(const void *d_in, void *d_out, int64_t rows, int64_t cols, 
     // row pass (contiguous rows, any length) -> work; column pass on
     // row-segment tiles: one kernel for rows <= 512, otherwise the four-step
     // split rows = R1*R2 (A in place on work, B from work into out)
-    static const bool oop_env = getenv("GDSP_FFT2_OOP") != nullptr;
-    const bool oop = oop_env && d_in != d_out && lr > gdsp::kColMaxLog2;
-    if (!oop) STCHK(exec_plan(pc, d_in, work, rows, inv, gdsp::LOAD_COMPLEX, s));
+    STCHK(exec_plan(pc, d_in, work, rows, inv, gdsp::LOAD_COMPLEX, s));
     const double sc = 1.0 / (double)rows;
     if (lr <= gdsp::kColMaxLog2) {
       HIPCHK(gdsp::launch_colfft(lr, inv, 0, inv, work, (cd *)d_out, cols, 1, 0, 1, 0, 1,
@@ -1339,16 +1363,8 @@ int gdsp_fft2_device(const void *d_in, void *d_out, int64_t rows, int64_t cols, 
       STCHK(get_plan((int64_t)1 << l1, &p1));
       STCHK(get_plan((int64_t)1 << l2, &p2));
       const int64_t R1 = (int64_t)1 << l1, R2 = (int64_t)1 << l2;
-      if (oop) {
-        // experiment: every pass out of place (rows -> out, A out -> work, B
-        // work -> out)
-        STCHK(exec_plan(pc, d_in, (cd *)d_out, rows, inv, gdsp::LOAD_COMPLEX, s));
-        HIPCHK(gdsp::launch_colfft(l1, inv, 1, false, (cd *)d_out, work, cols, R2, 1, R2, 1, R2,
-                                   p1->tw, pr->tw, lr, 1.0, 1, 0, s));
-      } else {
-        HIPCHK(gdsp::launch_colfft(l1, inv, 1, false, work, work, cols, R2, 1, R2, 1, R2, p1->tw,
-                                   pr->tw, lr, 1.0, 1, 0, s));
-      }
+      HIPCHK(gdsp::launch_colfft(l1, inv, 1, false, work, work, cols, R2, 1, R2, 1, R2, p1->tw,
+                                 pr->tw, lr, 1.0, 1, 0, s));
       HIPCHK(gdsp::launch_colfft(l2, false, 0, inv, work, (cd *)d_out, cols, R1, R2, 1, 1, R1,
                                  p2->tw, nullptr, lr, sc, 1, 0, s));
     }

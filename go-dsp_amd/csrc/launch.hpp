@@ -67,11 +67,11 @@ hipError_t launch_fft_mixed(const MixedDesc &d, bool inv, int load, const void *
 hipError_t launch_bluestein(int log2m, bool inv, const cd *in, cd *out, int64_t n,
                             int64_t batch, const cd *twm, const cd *chirp, const cd *bhat,
                             double scale, hipStream_t s);
-// output-split chirp-z on M = 16384 for n in (8192, 16384]: parts * kpart >= n
-// outputs, n + kpart - 1 <= 16384, bhat = parts tables of 16384, twm = T_16384
-hipError_t launch_bluestein_parts(bool inv, const cd *in, cd *out, int64_t n, int64_t batch,
-                                  int parts, int64_t kpart, const cd *twm, const cd *chirp,
-                                  const cd *bhat, double scale, hipStream_t s);
+// output-split chirp-z on M = 2^log2m (13 or 14): parts * kpart >= n outputs,
+// n + kpart - 1 <= M, bhat = parts tables of M, twm = T_M
+hipError_t launch_bluestein_parts(int log2m, bool inv, const cd *in, cd *out, int64_t n,
+                                  int64_t batch, int parts, int64_t kpart, const cd *twm,
+                                  const cd *chirp, const cd *bhat, double scale, hipStream_t s);
 // wave-resident chirp-z (fft_wave.hip): waves per transform Q = M / 2048 for
 // 512 < n <= 1024 Q, 2n - 1 <= M (0: not this kernel's case)
 int bluestein_wave_q(int64_t n, int64_t m);

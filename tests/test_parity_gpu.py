@@ -296,6 +296,9 @@ def test_plan_kinds(gdsp):
     # prime, NextPowerOf2(2n-1) = 32768: output-split chirp-z, 2 parts on M = 16384
     assert D.plan(8209).kind == 3 and D.plan(8209).parts == 2 and D.plan(8209).m == 16384
     assert D.plan(16411).kind == 4  # prime beyond the parts' reach: composed Bluestein
+    # four-step rows on the output-split chirp-z (power-of-2 / single-radix columns)
+    assert (D.plan(64 * 8209).kind, D.plan(64 * 8209).n2) == (6, 8209)
+    assert (D.plan(2 * 10007).kind, D.plan(2 * 10007).n2) == (6, 10007)
     assert D.plan(8191 * 64).kind == 6  # power-of-2 columns, fused chirp-z rows of 8191
     assert D.plan(3000, chirpz=True).kind == 3
     assert D.plan(10000, chirpz=True).kind == 4
@@ -365,7 +368,9 @@ MIXED4 = [4100, 5000, 6000, 8190, 10000, 44100, 48000, 3 << 16, 8209, 100000, 10
           1114112,
           # rows through the fused chirp-z kernel: 64 x 8191, 100 x 4099,
           # 143 x 1009, 91 x 7919
-          524224, 409900, 144287, 720629]
+          524224, 409900, 144287, 720629,
+          # rows through the output-split chirp-z: 64 x 8209, 2 x 10007, 3 x 12289
+          525376, 20014, 36867]
 
 
 @pytest.mark.parametrize("n", MIXED4)
