@@ -706,16 +706,6 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
       p->kpart = (n + parts - 1) / parts;
     }
   }
-  static const bool parts13 = getenv("GDSP_BLU_PARTS13") != nullptr;
-  if (parts13 && p->kind == KIND_BLUESTEIN && p->log2m == 14 && !chirpz &&
-      n + (n + 1) / 2 - 1 <= 8192) {
-    // experiment: n in (4096, 5461] as 2 parts on M = 8192 instead of one
-    // convolution of 16384
-    p->m = 8192;
-    p->log2m = 13;
-    p->parts = 2;
-    p->kpart = (n + 1) / 2;
-  }
   if (p->kind == KIND_BLUESTEIN_COMPOSED && !chirpz && !getenv("GDSP_CHIRPZ_POW2")) {
     // The composed chirp-z is HBM-bound, so its cost follows M: take the
     // smallest M >= 2n - 1 with a three-pass split (power-of-2 or
