@@ -103,7 +103,7 @@ bool lds_split_default() {
 enum Slot {
   SLOT_IN = 0, SLOT_OUT, SLOT_AUX, SLOT_AUX2, SLOT_GLOBAL, SLOT_GLOBAL_IN, SLOT_REAL,
   SLOT_BLU, SLOT_FFT2, SLOT_PW_PART, SLOT_PW_RED, SLOT_PW_BUF, SLOT_FS0, SLOT_FS1, SLOT_FS2,
-  SLOT_FS3, SLOT_FFTN, SLOT_MX0, SLOT_MX1, SLOT_COUNT
+  SLOT_FS3, SLOT_FFTN, SLOT_MX0, SLOT_MX1, SLOT_PARTS, SLOT_COUNT
 };
 
 struct Workspace {
@@ -1112,6 +1112,16 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
         return GDSP_OK;
       }
       if (p->kind == KIND_BLUESTEIN && p->parts > 1) {
+        // the parts of a row run in different workgroups, so a part may
+        // write the row before another has read it: in place (the four-step
+        // rows, or a caller's in == out) goes through a copy of the input
+        DevBuf cp;
+        if ((const void *)src == (const void *)out) {
+          const size_t bytes = (size_t)batch * (size_t)p->n * sizeof(cd);
+          STCHK(cp.alloc(bytes, s, SLOT_PARTS));
+          HIPCHK(hipMemcpyAsync(cp.p, src, bytes, hipMemcpyDeviceToDevice, s));
+          src = (const cd *)cp.p;
+        }
         HIPCHK(gdsp::launch_bluestein_parts(p->log2m, inv, src, out, p->n, batch, p->parts,
                                             p->kpart, p->mplan->tw, p->chirp, p->bhat, scale,
                                             s));
