@@ -547,92 +547,6 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_ker
   }
 }
 
-// Register-lean half-overlap Pwelch for a third wave per SIMD (experiment,
-// GDSP_PW_LEAN=1): the per-bin sums leave the registers for a folded LDS
-// accumulator S[j] += |Z_j|^2 + |Z_(F-j)|^2, j <= F/2 (two phases per pair so
-// every slot has one writer at a time: deterministic), the window is re-read
-// from L1/L2 and the twiddle bases from the global table, no next-pair
-// prefetch. LDS: exchange (F + F/16 doubles) + F/2 + 1 sums = 50 KiB at F =
-// 4096, three workgroups per CU; __launch_bounds__ min 3 waves per SIMD.
-// The worker's partial is written unfolded-compatible for the finalise, which
-// adds acc[k] + acc[F-k] for 0 < k < F/2: S[j] at j, zero above F/2 (bins 0
-// and F/2 have no partner bin, so S holds them once, as acc does).
-#ifndef GDSP_LEAN_OPQ
-#define GDSP_LEAN_OPQ 1
-#endif
-#ifndef GDSP_LEAN_LIN
-#define GDSP_LEAN_LIN kPwLinear
-#endif
-template <int LOG2F>
-__global__ __launch_bounds__((Geo<LOG2F>::WG), 3) void pwelch_half_lean_kernel(
-    const double *__restrict__ x, int64_t seg_begin, int64_t seg_end, int64_t pairs_per_worker,
-    const double *__restrict__ win, const cd *__restrict__ tw, double *__restrict__ partial) {
-  using G = Geo<LOG2F>;
-  static_assert(G::TPW == 1, "one pair per workgroup");
-  constexpr int E = G::E, H = E / 2, F = G::N;
-  constexpr int64_t STRIDE = F / 2;
-  __shared__ double lds[G::LDS_DOUBLES + F / 2 + 1];
-  double *lre = lds, *S = lds + G::LDS_DOUBLES;
-  const int t = threadIdx.x;
-  const int64_t worker = blockIdx.x;
-  const int64_t npairs = (seg_end - seg_begin + 1) / 2;
-  for (int i = t; i <= F / 2; i += G::WG) S[i] = 0.0;
-  const int64_t p0 = worker * pairs_per_worker;
-  double carry[H];
-  {
-    const int64_t s0 = seg_begin + 2 * (p0 < npairs ? p0 : 0);
-    const double *b = x + s0 * STRIDE + t;
-#pragma unroll
-    for (int k = 0; k < H; ++k) carry[k] = (p0 < npairs) ? b[k * G::T] : 0.0;
-  }
-  __syncthreads();
-  for (int64_t it = 0; it < pairs_per_worker; ++it) {
-    const int64_t p = p0 + it;
-    const bool active = p < npairs;  // uniform: one worker per workgroup
-    const int64_t s0 = seg_begin + 2 * p;
-    const bool has1 = active && (s0 + 1 < seg_end);
-    const double *b = opaque_ptr(x) + s0 * STRIDE + t;
-    const double *w = opaque_ptr(win) + t;
-    cd v[E];
-#pragma unroll
-    for (int k = 0; k < H; ++k) {
-      const double a2 = active ? b[(H + k) * G::T] : 0.0;
-      const double c2 = has1 ? b[(E + k) * G::T] : 0.0;
-      const double wl = w[k * G::T], wh = w[(H + k) * G::T];
-#ifdef GDSP_LEAN_NOCARRY
-      // re-read the carried half from L2 instead of holding it across the FFT
-      const double a1 = active ? b[k * G::T] : 0.0;
-#else
-      const double a1 = carry[k];
-      carry[k] = c2;
-#endif
-      v[k] = {a1 * wl, has1 ? a2 * wl : 0.0};
-      v[H + k] = {a2 * wh, c2 * wh};
-    }
-    fft_regs<LOG2F, true, GDSP_LEAN_OPQ, 4, 0, 0, const cd *, GDSP_LEAN_LIN>(v, opaque_int(t), tw, lre, lre,
-                                                              it == 0);
-    if (active) {
-#pragma unroll
-      for (int k = 0; k < E; ++k) {
-        const int bin = t + k * G::T;
-        if (bin <= F / 2) S[bin] = fma(v[k].y, v[k].y, fma(v[k].x, v[k].x, S[bin]));
-      }
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < E; ++k) {
-        const int bin = t + k * G::T;
-        if (bin > F / 2) S[F - bin] = fma(v[k].y, v[k].y, fma(v[k].x, v[k].x, S[F - bin]));
-      }
-    }
-  }
-  __syncthreads();
-  if (p0 < npairs) {
-    double *dst = partial + worker * F;
-    for (int i = t; i < F; i += G::WG)
-      dst[i] = i > F / 2 ? 0.0 : S[i];
-  }
-}
-
 // Deterministic two-level reduction of the per-worker partial spectra:
 // level 1 sums fixed chunks of workers per bin (grid: bins x chunks), level 2
 // sums the chunk results in chunk order and adds into acc.
@@ -1173,12 +1087,6 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
       }();
       if (shfl)
         return launch_pwelch4096_shfl(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
-      static const bool lean = getenv("GDSP_PW_LEAN") != nullptr;
-      if (lean) {
-        hipLaunchKernelGGL((pwelch_half_lean_kernel<12>), dim3((unsigned)nworkers),
-                           dim3(Geo<12>::WG), 0, s, x, seg_begin, seg_end, ppw, win, tw, partial);
-        return hipGetLastError();
-      }
       return launch_pwh_t<12, 2, 1, 4, true, true>(x, seg_begin, seg_end, ppw, nworkers, win, tw,
                                                    partial, s);
     }
