@@ -170,7 +170,9 @@ def test_convolve(gdsp, oracle, n):
 
 @pytest.mark.parametrize("shape", [(1, 1), (1, 8), (8, 1), (2, 3), (3, 5), (16, 16), (64, 32),
                                    (6, 10), (100, 7), (128, 256), (512, 300), (1024, 1024),
-                                   (16, 1000), (2048, 48), (4096, 33), (65536, 8), (32, 5)])
+                                   (16, 1000), (2048, 48), (4096, 33), (65536, 8), (32, 5),
+                                   # a dimension on the output-split chirp-z (in-place rows)
+                                   (3, 8209), (8209, 2)])
 def test_fft2_vs_oracle(gdsp, oracle, shape):
     rng = np.random.default_rng(shape[0] * 1000 + shape[1])
     x = rng.uniform(-1, 1, shape) + 1j * rng.uniform(-1, 1, shape)
@@ -431,7 +433,7 @@ def test_TestFFTN(gdsp, refvec):
 
 @pytest.mark.parametrize("dims", [[2, 2, 3], [5], [16, 16], [3, 5, 7], [64, 1, 32], [32, 16, 8, 4],
                                   [1024, 16], [2048, 9], [7, 100, 3], [4, 4096], [2, 3, 3000],
-                                  [600, 20], [2, 1, 1, 2]])
+                                  [600, 20], [2, 1, 1, 2], [8209, 2], [2, 3, 8209]])
 def test_fftn_vs_oracle(gdsp, oracle, dims):
     rng = np.random.default_rng(sum(dims))
     n = int(np.prod(dims))
