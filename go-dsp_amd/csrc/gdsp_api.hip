@@ -852,19 +852,28 @@ int exec_global(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool
 int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv,
                     int load, hipStream_t s, int depth);
 
+void fourstep_split(int ln, int *lr, int *lc);
+
 int exec_fourstep(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
                   hipStream_t s, int depth) {
   const int ln = p->log2n;
   int lr, lc;
-  if (ln - 13 >= gdsp::kColMinLog2 && ln - 13 <= gdsp::kColMaxLog2) {
-    lc = 13;
-    lr = ln - 13;
-  } else if (ln - 13 < gdsp::kColMinLog2) {
-    lr = gdsp::kColMinLog2;
-    lc = ln - lr;
-  } else {
-    lr = gdsp::kColMaxLog2;
-    lc = ln - lr;  // rows longer than 8192 recurse
+  fourstep_split(ln, &lr, &lc);
+  // Few transforms: rows of 8192 leave the row pass at <= 256 workgroups, and
+  // rows of 4096 (twice the rows, the column DFT twice as long) measured
+  // 5-20 % faster per call at batch * 2^(ln-13) <= 256 (2^17..2^21 at batch 1:
+  // 2^20 0.0275 -> 0.026 ms, 2^18 0.022 -> 0.0177; scripts/dev/fs_split_ab.py,
+  // profiles/r02/fs_split.jsonl); larger batches keep 8192.
+  if (lc == 13 && lr + 1 <= gdsp::kColMaxLog2 && (batch << lr) <= 256) {
+    lc = 12;
+    lr += 1;
+  }
+  if (const char *e = getenv("GDSP_FS_LC")) {  // experiment: force the row length
+    const int f = atoi(e);
+    if (f >= 4 && f <= 13 && ln - f >= gdsp::kColMinLog2 && ln - f <= gdsp::kColMaxLog2) {
+      lc = f;
+      lr = ln - f;
+    }
   }
   if (depth >= 4) return fail(GDSP_ERR_UNSUPPORTED, "transform too long");
   gdsp_plan *pr = nullptr, *pcol = nullptr;

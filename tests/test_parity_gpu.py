@@ -124,6 +124,20 @@ def test_fft_sizes_vs_oracle(gdsp, oracle, n):
     assert nrel(gdsp.fft.FFT(x[0]), ref[0]) < TOL
 
 
+@pytest.mark.parametrize("log2n,batch", [(17, 1), (17, 16), (17, 17), (18, 3), (19, 4),
+                                          (19, 5), (20, 1), (20, 2), (20, 3), (21, 1)])
+def test_fourstep_split_by_batch(gdsp, oracle, log2n, batch):
+    # exec_fourstep takes rows of 4096 when batch * 2^(log2n-13) <= 256 and of
+    # 8192 above: both sides of the boundary, forward / inverse / real input
+    n = 1 << log2n
+    rng = np.random.default_rng(log2n * 100 + batch)
+    x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
+    assert row_nrel(gdsp.fft.FFTBatch(x), oracle.fft_rows(x)) < TOL
+    assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL
+    xr = x.real.copy()
+    assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
+
+
 @pytest.mark.parametrize("n", [2, 4, 8, 16, 32, 64, 128, 256])
 def test_short_rows_many_blocks(gdsp, oracle, n):
     # short transforms stage whole workgroup chunks through LDS: several
