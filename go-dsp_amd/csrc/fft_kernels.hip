@@ -228,6 +228,12 @@ __host__ __device__ constexpr int blu_epi_mode(int log2m, int log2e) {
 // convolution c_p[m mod M] = w_(k0 + m), m in [-(n-1), kpart-1], which does not
 // wrap as long as n + kpart - 1 <= M (bhat + blockIdx.y * M holds FFT_M(c_p)/M).
 // The input then fills more than half of M, so only the output side is pruned.
+// Rows ahead a chirp-z block touches for its successor on the XCD (0: off).
+// chirpz3000 2.95-2.99 -> 2.80-2.83 ms at 8-32, 2.84-2.85 at 48, 2.94-3.03 at
+// 64-128 (scripts/dev/blu_pf_ab.sh)
+#ifndef GDSP_BLU_PF
+#define GDSP_BLU_PF 16
+#endif
 template <int LOG2M, bool INV, bool SPLIT, int LOG2E = 4, bool PARTS = false>
 __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
     const cd *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
@@ -265,6 +271,22 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
   }
   cd v[G::E];
   const cd *src = in + g * n;
+#if GDSP_BLU_PF > 0
+  // touch every 128-B line of the row the block GDSP_BLU_PF places later on
+  // this XCD will take (xcd_remap keeps an XCD's rows contiguous), so that
+  // block's row loads hit L2 / MALL instead of waiting on HBM
+  double pf0 = 0.0, pf1 = 0.0;
+  if constexpr (!PARTS && G::TPW == 1) {
+    const int64_t gp = g + GDSP_BLU_PF;
+    if (valid && gp < batch) {
+      const char *prow = reinterpret_cast<const char *>(in + gp * n);
+      const int lines = (int)((n * 16 + 127) >> 7);
+      if (lt < lines) pf0 = *reinterpret_cast<const double *>(prow + ((int64_t)lt << 7));
+      if (lt + G::WG < lines)
+        pf1 = *reinterpret_cast<const double *>(prow + ((int64_t)(lt + G::WG) << 7));
+    }
+  }
+#endif
 #pragma unroll
   for (int k = 0; k < G::E; ++k) {
     const int idx = t + k * G::T;
@@ -275,6 +297,11 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
       v[k] = cmul(x, chirp[idx]);
     }
   }
+#if GDSP_BLU_PF > 0
+  // the prefetches were issued before the row loads the premultiply waited
+  // for (loads return in order), so consuming them here costs no wait
+  asm volatile("" ::"v"(pf0), "v"(pf1));
+#endif
   constexpr int EPI = blu_epi_mode(LOG2M, LOG2E);
   if constexpr (EPI >= 1) {
     // x bhat, conj: fused into FFT 1's last pass, each butterfly's factors
