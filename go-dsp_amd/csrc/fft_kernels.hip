@@ -234,6 +234,9 @@ __host__ __device__ constexpr int blu_epi_mode(int log2m, int log2e) {
 #ifndef GDSP_BLU_PF
 #define GDSP_BLU_PF 16
 #endif
+#ifndef GDSP_BLU_PF_ALL
+#define GDSP_BLU_PF_ALL 0
+#endif
 template <int LOG2M, bool INV, bool SPLIT, int LOG2E = 4, bool PARTS = false>
 __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
     const cd *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
@@ -276,14 +279,16 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
   // this XCD will take (xcd_remap keeps an XCD's rows contiguous), so that
   // block's row loads hit L2 / MALL instead of waiting on HBM
   double pf0 = 0.0, pf1 = 0.0;
-  if constexpr (!PARTS && G::TPW == 1) {
-    const int64_t gp = g + GDSP_BLU_PF;
+  // (n <= M/2 = T*E/2, so a row is at most T*E/16 lines: two per thread of
+  // the transform's T up to E = 32)
+  if constexpr (!PARTS && (G::TPW == 1 || GDSP_BLU_PF_ALL)) {
+    const int64_t gp = g + (int64_t)GDSP_BLU_PF * G::TPW;
     if (valid && gp < batch) {
       const char *prow = reinterpret_cast<const char *>(in + gp * n);
       const int lines = (int)((n * 16 + 127) >> 7);
-      if (lt < lines) pf0 = *reinterpret_cast<const double *>(prow + ((int64_t)lt << 7));
-      if (lt + G::WG < lines)
-        pf1 = *reinterpret_cast<const double *>(prow + ((int64_t)(lt + G::WG) << 7));
+      if (t < lines) pf0 = *reinterpret_cast<const double *>(prow + ((int64_t)t << 7));
+      if (t + G::T < lines)
+        pf1 = *reinterpret_cast<const double *>(prow + ((int64_t)(t + G::T) << 7));
     }
   }
 #endif
