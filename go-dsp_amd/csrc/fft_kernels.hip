@@ -229,13 +229,12 @@ __host__ __device__ constexpr int blu_epi_mode(int log2m, int log2e) {
 // wrap as long as n + kpart - 1 <= M (bhat + blockIdx.y * M holds FFT_M(c_p)/M).
 // The input then fills more than half of M, so only the output side is pruned.
 // Rows ahead a chirp-z block touches for its successor on the XCD (0: off).
-// chirpz3000 2.95-2.99 -> 2.80-2.83 ms at 8-32, 2.84-2.85 at 48, 2.94-3.03 at
-// 64-128 (scripts/dev/blu_pf_ab.sh)
+// chirpz3000 2.95-3.05 -> 2.80-2.89 ms at 8-32, 2.84-2.85 at 48, 2.94-3.03 at
+// 64-128 (scripts/dev/blu_pf_ab.sh); blocks of several transforms (M <= 2048)
+// touch the same slot's row GDSP_BLU_PF blocks on: primes 13..1021 10-22 %
+// faster (scripts/dev/blu_pfall_ab.sh)
 #ifndef GDSP_BLU_PF
 #define GDSP_BLU_PF 16
-#endif
-#ifndef GDSP_BLU_PF_ALL
-#define GDSP_BLU_PF_ALL 0
 #endif
 template <int LOG2M, bool INV, bool SPLIT, int LOG2E = 4, bool PARTS = false>
 __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
@@ -281,7 +280,7 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
   double pf0 = 0.0, pf1 = 0.0;
   // (n <= M/2 = T*E/2, so a row is at most T*E/16 lines: two per thread of
   // the transform's T up to E = 32)
-  if constexpr (!PARTS && (G::TPW == 1 || GDSP_BLU_PF_ALL)) {
+  if constexpr (!PARTS) {
     const int64_t gp = g + (int64_t)GDSP_BLU_PF * G::TPW;
     if (valid && gp < batch) {
       const char *prow = reinterpret_cast<const char *>(in + gp * n);
