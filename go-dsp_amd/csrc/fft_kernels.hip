@@ -236,6 +236,9 @@ __host__ __device__ constexpr int blu_epi_mode(int log2m, int log2e) {
 #ifndef GDSP_BLU_PF
 #define GDSP_BLU_PF 16
 #endif
+#ifndef GDSP_BLU_PF_SHIFT
+#define GDSP_BLU_PF_SHIFT 7  // touch granularity: one load per 2^SHIFT bytes
+#endif
 template <int LOG2M, bool INV, bool SPLIT, int LOG2E = 4, bool PARTS = false>
 __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
     const cd *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
@@ -277,17 +280,21 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
   // touch every 128-B line of the row the block GDSP_BLU_PF places later on
   // this XCD will take (xcd_remap keeps an XCD's rows contiguous), so that
   // block's row loads hit L2 / MALL instead of waiting on HBM
-  double pf0 = 0.0, pf1 = 0.0;
-  // (n <= M/2 = T*E/2, so a row is at most T*E/16 lines: two per thread of
-  // the transform's T up to E = 32)
+  // (n <= M/2 = T*E/2, so a row is at most T*E*16/2^SH pieces of 2^SH bytes:
+  // E*8/2^SH per thread of the transform's T)
+  constexpr int SH = GDSP_BLU_PF_SHIFT, NPF = (G::E * 8 >> SH) > 0 ? (G::E * 8 >> SH) : 1;
+  double pf[NPF];
+#pragma unroll
+  for (int k = 0; k < NPF; ++k) pf[k] = 0.0;
   if constexpr (!PARTS) {
     const int64_t gp = g + (int64_t)GDSP_BLU_PF * G::TPW;
     if (valid && gp < batch) {
       const char *prow = reinterpret_cast<const char *>(in + gp * n);
-      const int lines = (int)((n * 16 + 127) >> 7);
-      if (t < lines) pf0 = *reinterpret_cast<const double *>(prow + ((int64_t)t << 7));
-      if (t + G::T < lines)
-        pf1 = *reinterpret_cast<const double *>(prow + ((int64_t)(t + G::T) << 7));
+      const int pieces = (int)((n * 16 + (1 << SH) - 1) >> SH);
+#pragma unroll
+      for (int k = 0; k < NPF; ++k)
+        if (t + k * G::T < pieces)
+          pf[k] = *reinterpret_cast<const double *>(prow + ((int64_t)(t + k * G::T) << SH));
     }
   }
 #endif
@@ -304,7 +311,8 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
 #if GDSP_BLU_PF > 0
   // the prefetches were issued before the row loads the premultiply waited
   // for (loads return in order), so consuming them here costs no wait
-  asm volatile("" ::"v"(pf0), "v"(pf1));
+#pragma unroll
+  for (int k = 0; k < NPF; ++k) asm volatile("" ::"v"(pf[k]));
 #endif
   constexpr int EPI = blu_epi_mode(LOG2M, LOG2E);
   if constexpr (EPI >= 1) {
