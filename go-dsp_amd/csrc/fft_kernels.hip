@@ -223,10 +223,10 @@ __host__ __device__ constexpr int blu_epi_mode(int log2m, int log2e) {
 // Inverse (fft.IFFT of non-power-of-2 length): conj in, conj + 1/n out.
 //
 // PARTS (n > M/2, where bluestein.go:70's M would exceed one kernel): the
-// outputs are split into parts of kpart, part blockIdx.y computing
-// X[k0 + k], k < kpart, k0 = blockIdx.y * kpart, by its own circular
+// outputs are split into nparts parts of kpart, part p computing
+// X[k0 + k], k < kpart, k0 = p * kpart, by its own circular
 // convolution c_p[m mod M] = w_(k0 + m), m in [-(n-1), kpart-1], which does not
-// wrap as long as n + kpart - 1 <= M (bhat + blockIdx.y * M holds FFT_M(c_p)/M).
+// wrap as long as n + kpart - 1 <= M (bhat + p * M holds FFT_M(c_p)/M).
 // The input then fills more than half of M, so only the output side is pruned.
 // Rows ahead a chirp-z block touches for its successor on the XCD (0: off).
 // chirpz3000 2.95-3.05 -> 2.80-2.89 ms at 8-32, 2.84-2.85 at 48, 2.94-3.03 at
@@ -236,6 +236,9 @@ __host__ __device__ constexpr int blu_epi_mode(int log2m, int log2e) {
 #ifndef GDSP_BLU_PF
 #define GDSP_BLU_PF 16
 #endif
+#ifndef GDSP_BLU_PARTS_YMAJOR
+#define GDSP_BLU_PARTS_YMAJOR 0
+#endif
 #ifndef GDSP_BLU_PF_SHIFT
 #define GDSP_BLU_PF_SHIFT 7  // touch granularity: one load per 2^SHIFT bytes
 #endif
@@ -243,13 +246,27 @@ template <int LOG2M, bool INV, bool SPLIT, int LOG2E = 4, bool PARTS = false>
 __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
     const cd *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
     const cd *__restrict__ twm, const cd *__restrict__ chirp, const cd *__restrict__ bhat,
-    double scale, int64_t kpart) {
+    double scale, int64_t kpart, int nparts) {
   using G = Geo<LOG2M, LOG2E>;
   __shared__ double lds[(SPLIT ? 1 : 2) * G::LDS_DOUBLES];
   const int lt = threadIdx.x;
   const int slot = lt / G::T;
   const int t = lt & (G::T - 1);
-  const int64_t g = xcd_remap(blockIdx.x, gridDim.x) * G::TPW + slot;
+  // PARTS: the parts of a row are adjacent block indices (after the XCD
+  // remap, so on one XCD at about the same time), and its 2nd..nth reads of
+  // the row hit L2 instead of HBM (GDSP_BLU_PARTS_YMAJOR=1: part = blockIdx.y)
+  int64_t gb = xcd_remap(blockIdx.x, gridDim.x);
+  int part = 0;
+  if constexpr (PARTS) {
+#if GDSP_BLU_PARTS_YMAJOR
+    part = (int)blockIdx.y;
+#else
+    const int64_t q = gb / nparts;
+    part = (int)(gb - q * nparts);
+    gb = q;
+#endif
+  }
+  const int64_t g = gb * G::TPW + slot;
   const bool valid = g < batch;
   double *lre = lds + slot * G::STRIDE;
   double *lim = SPLIT ? lre : lds + G::LDS_DOUBLES + slot * G::STRIDE;
@@ -268,11 +285,11 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
   const cd *ochirp = chirp;
   cd *orow = valid ? out + g * n : nullptr;
   if constexpr (PARTS) {
-    const int64_t k0 = (int64_t)blockIdx.y * kpart;
+    const int64_t k0 = (int64_t)part * kpart;
     nout = n - k0 < kpart ? n - k0 : kpart;
     ochirp += k0;
     if (orow) orow += k0;
-    bhat += (int64_t)blockIdx.y * G::N;
+    bhat += (int64_t)part * G::N;
   }
   cd v[G::E];
   const cd *src = in + g * n;
@@ -981,19 +998,19 @@ static hipError_t launch_blu_t(const cd *in, cd *out, int64_t n, int64_t batch, 
       const int64_t nb5 = (batch + G5::TPW - 1) / G5::TPW;
       hipLaunchKernelGGL((bluestein_kernel<LOG2M, INV, true, 5>), dim3((unsigned)nb5),
                          dim3(G5::WG), 0, s, in, out, n, batch, twm, chirp, bhat, scale,
-                         (int64_t)0);
+                         (int64_t)0, 1);
       return hipGetLastError();
     }
   }
   using G = Geo<LOG2M>;
   const int64_t nblk = (batch + G::TPW - 1) / G::TPW;
   hipLaunchKernelGGL((bluestein_kernel<LOG2M, INV, true>), dim3((unsigned)nblk), dim3(G::WG), 0,
-                     s, in, out, n, batch, twm, chirp, bhat, scale, (int64_t)0);
+                     s, in, out, n, batch, twm, chirp, bhat, scale, (int64_t)0, 1);
   return hipGetLastError();
 }
 
 // Output-split chirp-z on M = 8192 / 16384 (bluestein_kernel PARTS): `parts`
-// launches' worth of blocks in one grid (blockIdx.y = part), bhat holding
+// launches' worth of blocks in one grid (the parts of a row adjacent), bhat holding
 // parts * M.
 template <int LOG2M>
 static hipError_t launch_blu_parts_t(bool inv, const cd *in, cd *out, int64_t n, int64_t batch,
@@ -1003,13 +1020,19 @@ static hipError_t launch_blu_parts_t(bool inv, const cd *in, cd *out, int64_t n,
   if (parts < 1 || parts > 65535 || kpart < 1 || kpart > G::N / 2 || n + kpart - 1 > G::N ||
       kpart * parts < n)
     return hipErrorInvalidValue;
+#if GDSP_BLU_PARTS_YMAJOR
   const dim3 grid((unsigned)((batch + G::TPW - 1) / G::TPW), (unsigned)parts);
+#else
+  const int64_t nb = (batch + G::TPW - 1) / G::TPW * parts;
+  if (nb > 0x7fffffff) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)nb);
+#endif
   if (inv)
     hipLaunchKernelGGL((bluestein_kernel<LOG2M, true, true, 5, true>), grid, dim3(G::WG), 0, s,
-                       in, out, n, batch, twm, chirp, bhat, scale, kpart);
+                       in, out, n, batch, twm, chirp, bhat, scale, kpart, parts);
   else
     hipLaunchKernelGGL((bluestein_kernel<LOG2M, false, true, 5, true>), grid, dim3(G::WG), 0, s,
-                       in, out, n, batch, twm, chirp, bhat, scale, kpart);
+                       in, out, n, batch, twm, chirp, bhat, scale, kpart, parts);
   return hipGetLastError();
 }
 
