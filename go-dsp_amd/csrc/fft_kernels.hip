@@ -236,6 +236,9 @@ __host__ __device__ constexpr int blu_epi_mode(int log2m, int log2e) {
 #ifndef GDSP_BLU_PF
 #define GDSP_BLU_PF 16
 #endif
+#ifndef GDSP_BLU_PF_PARTS
+#define GDSP_BLU_PF_PARTS 2
+#endif
 #ifndef GDSP_BLU_PARTS_YMAJOR
 #define GDSP_BLU_PARTS_YMAJOR 0
 #endif
@@ -299,13 +302,16 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
   // block's row loads hit L2 / MALL instead of waiting on HBM
   // (n <= M/2 = T*E/2, so a row is at most T*E*16/2^SH pieces of 2^SH bytes:
   // E*8/2^SH per thread of the transform's T)
-  constexpr int SH = GDSP_BLU_PF_SHIFT, NPF = (G::E * 8 >> SH) > 0 ? (G::E * 8 >> SH) : 1;
+  // (PARTS: n <= M, twice the pieces; the row's part-0 block touches the row
+  // GDSP_BLU_PF_PARTS rows on)
+  constexpr int SH = GDSP_BLU_PF_SHIFT,
+                NPF = ((PARTS ? 2 : 1) * G::E * 8 >> SH) > 0 ? ((PARTS ? 2 : 1) * G::E * 8 >> SH) : 1;
   double pf[NPF];
 #pragma unroll
   for (int k = 0; k < NPF; ++k) pf[k] = 0.0;
-  if constexpr (!PARTS) {
-    const int64_t gp = g + (int64_t)GDSP_BLU_PF * G::TPW;
-    if (valid && gp < batch) {
+  if constexpr (!PARTS || GDSP_BLU_PF_PARTS > 0) {
+    const int64_t gp = g + (PARTS ? (int64_t)GDSP_BLU_PF_PARTS : (int64_t)GDSP_BLU_PF * G::TPW);
+    if (valid && gp < batch && part == 0) {
       const char *prow = reinterpret_cast<const char *>(in + gp * n);
       const int pieces = (int)((n * 16 + (1 << SH) - 1) >> SH);
 #pragma unroll
