@@ -20,8 +20,8 @@ KERNELS = {"radix4096": "fft_lds_kernel<12", "bluestein3000": "fft_mixed_fixed_k
            # one FFTN step = the row pass + two column-tile axes
            "fftn_512": ["fft_lds_kernel<9", ("colfft_tile_kernel<9", 2)],
            "wav_decode": "wav_decode_vec_kernel",
-           # one 2^20 four-step: column tiles, row FFTs, transpose
-           "fft_2p20": ["colfft_tile_kernel<7", "fft_lds_kernel<13", "transpose_kernel"]}
+           # one 2^20 four-step at batch 1: column tiles (256), rows of 4096, transpose
+           "fft_2p20": ["colfft_tile_kernel<8", "fft_lds_kernel<12", "transpose_kernel"]}
 
 
 def values(w, counter, kernel):
