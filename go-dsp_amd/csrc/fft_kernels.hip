@@ -236,6 +236,9 @@ __host__ __device__ constexpr int blu_epi_mode(int log2m, int log2e) {
 #ifndef GDSP_BLU_PF
 #define GDSP_BLU_PF 16
 #endif
+#ifndef GDSP_BLU_PF14  // M = 16384: one block per CU
+#define GDSP_BLU_PF14 4  // 2-4 % faster than 8 or 16 (scripts/dev/blu_pf14_ab.sh)
+#endif
 #ifndef GDSP_BLU_PF_PARTS
 #define GDSP_BLU_PF_PARTS 2
 #endif
@@ -310,7 +313,8 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
 #pragma unroll
   for (int k = 0; k < NPF; ++k) pf[k] = 0.0;
   if constexpr (!PARTS || GDSP_BLU_PF_PARTS > 0) {
-    const int64_t gp = g + (PARTS ? (int64_t)GDSP_BLU_PF_PARTS : (int64_t)GDSP_BLU_PF * G::TPW);
+    const int64_t gp = g + (PARTS ? (int64_t)GDSP_BLU_PF_PARTS
+                                  : (int64_t)(LOG2M == 14 ? GDSP_BLU_PF14 : GDSP_BLU_PF) * G::TPW);
     if (valid && gp < batch && part == 0) {
       const char *prow = reinterpret_cast<const char *>(in + gp * n);
       const int pieces = (int)((n * 16 + (1 << SH) - 1) >> SH);
