@@ -38,6 +38,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+HBM_COPY_GBS = 6290.0  # MI355X_MICROARCH.md: measured float4 copy rate (BASELINE.md:33)
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (tools/fp64peak.hip measures 67.3 FMA-only)
 # kernels whose FP64 work is taken from the committed SQ counter passes
 # (profiles/r02/sq_counters.json: 64 x (2 FMA + ADD + MUL) F64 instructions)
@@ -77,10 +78,10 @@ def parse():
 
 
 WORKLOADS = ["radix4096", "bluestein3000", "chirpz3000", "fft2_8192", "fft2_dist", "pwelch",
-             "fftn_512", "wav_decode", "fft_2p20"]
+             "fftn_512", "wav_decode", "fft_2p20", "fftreal1024"]
 # the BASELINE configs nested in the default line: configs[2] (production
 # dispatch and the reference's chirp-z algorithm), configs[3], configs[4]
-NESTED = ["bluestein3000", "chirpz3000", "fft2_8192", "pwelch"]
+NESTED = ["bluestein3000", "chirpz3000", "fft2_8192", "pwelch", "fftreal1024"]
 HEADLINE_METRIC = "Gsamples/s + % HBM roofline, batched N=4096 complex128 FFT at 1/2/4/8 GPUs"
 
 
@@ -159,7 +160,7 @@ def setup(w: str, c: Ctx, weak: bool = False) -> dict:
         def step():
             D.fft2(x, y, work=work, stream=stream)
 
-        return dict(step=step, total_samples=rows * cols, rank_samples=rows * cols,
+        return dict(step=step, x=x, y=y, total_samples=rows * cols, rank_samples=rows * cols,
                     alg_bytes=2 * 2 * 16 * rows * cols, kernel="fft2 (all launches)",
                     metric="Gsamples/s, fft.FFT2 8192x8192 complex128", scaling="strong",
                     cfg={"workload": "fft.FFT2 complex128 8192x8192", "rows": rows,
@@ -250,7 +251,8 @@ def setup(w: str, c: Ctx, weak: bool = False) -> dict:
     def step():
         result["pxx"], _ = Dd.pwelch(x, 1.0, opts, sh, stream=stream)
 
-    return dict(step=step, total_samples=total, rank_samples=total // world,
+    return dict(step=step, x=x, shard=sh, opts=opts, result=result, total_samples=total,
+                rank_samples=total // world,
                 alg_bytes=8 * x.numel(), kernel="pwelch_half_kernel<12>",
                 metric="Gsamples/s, spectral.Pwelch 2^30 samples NFFT 4096 50% overlap",
                 scaling="strong",
@@ -316,11 +318,187 @@ def parity(w: str, wl: dict, c: Ctx):
         ref = oracle.wav_floats(wl["raw"][:2 * m].cpu().numpy().tobytes(), m, 1, 16)
         got = wl["y"][:m].cpu().numpy()
         return {"samples": m, "bit_exact": bool(np.array_equal(got, ref.astype(np.float64)))}
+    if w == "fft2_8192" and "y" in wl:
+        return parity_fft2(wl, np, oracle)
+    if w == "pwelch":
+        return parity_pwelch(wl, c, np, oracle)
     return None
+
+
+def parity_fft2(wl: dict, np, oracle) -> dict:
+    """Whole output rows of this run's 8192^2 FFT2 against the oracle
+    (fft/fft_test.go:148-162 pins the same transform at 2x3 / 3x5): output
+    row k1 is FFT_C(sum_r x[r, :] e^{-2 pi i k1 r / R}) (computeFFT2,
+    fft/fft.go:123-154, column DFT then row DFT), so the column sum is taken
+    in float64 on the host and the row FFT by the oracle; plus five single
+    bins as direct 2-D DFT sums, error / sqrt(R C)."""
+    x, y = wl["x"], wl["y"]
+    R, C = x.shape
+    xr = x.cpu().numpy()
+    r = np.arange(R)
+    rows = [0, 1, 1234, R - 1]
+    nrel = 0.0
+    for k1 in rows:
+        col = np.exp(-2j * np.pi * ((k1 * r) % R) / R) @ xr
+        ref = oracle.fft(col)
+        got = y[k1].cpu().numpy()
+        nrel = max(nrel, float(np.linalg.norm(got - ref) / np.linalg.norm(ref)))
+    c = np.arange(C)
+    bins = [(0, 0), (1, 0), (0, 1), (1234, 4321), (8191, 17)]
+    berr = 0.0
+    for k1, k2 in bins:
+        want = np.exp(-2j * np.pi * ((k1 * r) % R) / R) @ (
+            xr @ np.exp(-2j * np.pi * ((k2 * c) % C) / C))
+        berr = max(berr, abs(complex(y[k1, k2].item()) - want) / np.sqrt(R * C))
+    return {"rows": len(rows), "max_nrel_vs_oracle": nrel, "bins": len(bins),
+            "max_bin_err_over_sqrt_RC": float(berr),
+            "check": "output rows 0, 1, 1234, 8191 = oracle.fft of the float64 column DFT; "
+                     "5 bins as direct 2-D DFT sums"}
+
+
+def parity_pwelch(wl: dict, c: Ctx, np, oracle) -> dict:
+    """This run's Pwelch path against the oracle (spectral/pwelch_test.go:31-46
+    pins the same function on 100 samples): the first 2^22 samples of the
+    same HBM stream through the same device accumulate + finalize as the
+    timed step and through the host C ABI (gdsp.spectral.Pwelch), each vs
+    oracle.pwelch; plus the timed full-size Pxx itself (finite, 2049 bins,
+    the white uniform[-1,1) stream's level 2/3 at Fs = 1)."""
+    Dd, spectral = c.Dd, c.gdsp.spectral
+    sh, opts = wl["shard"], wl["opts"]
+    pre = 1 << 22
+    x = wl["x"]
+    if sh.sample_lo != 0 or x.numel() < pre:
+        return None
+    nfft, nov = sh.nfft, sh.noverlap
+    xp = x[:pre]
+    host = xp.cpu().numpy()
+    ref, _ = oracle.pwelch(host, 1.0, nfft=nfft, noverlap=nov)
+    sp = Dd.plan_pwelch(pre, 1, 0, nfft, 0, nov)
+    win = c.torch.as_tensor(c.gdsp.window.Hann(sp.flen), dtype=c.torch.float64, device=x.device)
+    acc = c.torch.zeros(sp.flen, dtype=c.torch.float64, device=x.device)
+    Dd.gpu_accumulate(xp, sp, win, acc, stream=c.stream)
+    c.torch.cuda.synchronize()
+    dev_p, _ = spectral.finalize(acc.cpu().numpy(), sp.nsegs_total, nfft, nfft,
+                                 np.asarray(c.gdsp.window.Hann(nfft)), 1.0, False)
+    host_p, _ = spectral.Pwelch(host, 1.0, opts)
+    e_dev = float(np.linalg.norm(dev_p - ref) / np.linalg.norm(ref))
+    e_host = float(np.linalg.norm(host_p - ref) / np.linalg.norm(ref))
+    full = wl["result"].get("pxx")
+    level = float(np.median(full[1:-1])) if full is not None else None
+    return {"samples": pre, "segments": sp.nsegs_total,
+            "max_nrel_vs_oracle": max(e_dev, e_host), "nrel_device_path": e_dev,
+            "nrel_host_api": e_host,
+            "full_size": {"bins": None if full is None else int(full.size),
+                          "finite": None if full is None else bool(np.all(np.isfinite(full))),
+                          "median_interior": level, "expected": 2.0 / 3.0}}
+
+
+def run_fftreal1024(c: Ctx) -> dict:
+    """BASELINE configs[0]: fft.FFTReal of one N = 1024 float64 vector
+    (fft/fft.go:25-27), called the way the reference is called: a host slice
+    in, a fresh complex128 slice out, through the host-pointer C ABI
+    (gdsp_fft_real: mapped pinned buffers, one launch, one synchronisation).
+    A step is one call; each timed step is the mean of 200 calls. The kernel's
+    own duration (HIP events, device-resident row) is the roofline figure."""
+    import numpy as np
+    torch, D, args = c.torch, c.D, c.args
+    n = 1024
+    xd = torch.empty(n, dtype=torch.float64, device=c.dev)
+    D.fill_uniform(xd, SEED, stream=c.stream)
+    torch.cuda.synchronize()
+    xh = xd.cpu().numpy()
+    fr = c.gdsp.fft.FFTReal
+    reps = 200
+    for _ in range(args.warmup * reps):
+        fr(xh)
+    c.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps * reps):
+        y = fr(xh)
+    elapsed = time.perf_counter() - t0
+    per_call = elapsed / (args.steps * reps)
+    # the kernel alone: the same transform on a device-resident complex row
+    xc = xd.to(torch.complex128).reshape(1, n)
+    yc = torch.empty_like(xc)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for _ in range(10):
+        D.fft_batch(xc, yc, stream=c.stream)
+    ev[0].record(c.stream)
+    for _ in range(reps):
+        D.fft_batch(xc, yc, stream=c.stream)
+    ev[1].record(c.stream)
+    torch.cuda.synchronize()
+    kern_s = ev[0].elapsed_time(ev[1]) / reps / 1e3
+    alg = 8 * n + 16 * n  # float64 in, complex128 out
+    check = None
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    if c.rank == 0 and args.check_rows > 0:
+        ref = oracle.fft_real(xh)
+        check = {"rows": 1, "max_nrel_vs_oracle": float(np.linalg.norm(y - ref) /
+                                                          np.linalg.norm(ref)),
+                 "nrel_vs_numpy": float(np.linalg.norm(y - np.fft.fft(xh)) /
+                                        np.linalg.norm(ref))}
+    crossover = None
+    if c.rank == 0 and args.check_rows > 0:
+        crossover = small_call_crossover(c, np, oracle)
+    return {
+        "metric": "Gsamples/s (us per call), fft.FFTReal N=1024 on a host vector",
+        "value": round(n / per_call / 1e9, 6),
+        "unit": "Gsamples/s",
+        "small_n": crossover,
+        "ms_per_step": round(per_call * 1e3, 5),
+        "us_per_call": round(per_call * 1e6, 2),
+        "scaling": "weak",
+        "dtype": "f64 in, complex128 out",
+        "config": {"workload": "fft.FFTReal of one N=1024 float64 host vector per call "
+                               "(BASELINE configs[0]; host C ABI, PCIe-inclusive)",
+                   "n": n, "batch": 1, "calls_timed": args.steps * reps,
+                   "parallelism": f"replicas{c.world}"},
+        "roofline": {"bound": "latency", "kernel": "fft_lds_kernel<10> (one row)",
+                     "achieved": round(alg / kern_s / 1e9, 3), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(alg / kern_s / 1e9 / HBM_PEAK_GBS, 6),
+                     "frac_vs_copy": round(alg / kern_s / 1e9 / HBM_COPY_GBS, 6),
+                     "avg_launch_ms": round(kern_s * 1e3, 5), "alg_bytes_per_launch": alg,
+                     "traffic": None,
+                     "note": "one 24 KiB transform: launch-latency bound, not HBM bound; "
+                             "the call's cost is launch + synchronisation (us_per_call)"},
+        "fp64": None,
+        "cpu_baseline": None,
+        "parity": check,
+    }
+
+
+def small_call_crossover(c: Ctx, np, oracle) -> dict:
+    """fft.FFTReal per-call time through the host C ABI against the
+    reference algorithm's restatement on one host thread, by length: where
+    a one-vector call starts to pay on the GPU (small-n
+    policy)."""
+    rows = []
+    cross = None
+    for n in (64, 256, 1024, 2048, 4096, 8192, 16384, 65536):
+        x = oracle.fill_uniform(n, SEED)
+        reps = 200 if n <= 16384 else 40
+        c.gdsp.fft.FFTReal(x)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            c.gdsp.fft.FFTReal(x)
+        g = (time.perf_counter() - t0) / reps
+        oracle.fft_real(x)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            oracle.fft_real(x)
+        h = (time.perf_counter() - t0) / reps
+        rows.append({"n": n, "gpu_call_us": round(g * 1e6, 2), "cpu_1thread_us": round(h * 1e6, 2)})
+        if cross is None and g < h:
+            cross = n
+    return {"by_n": rows, "first_n_gpu_faster": cross}
 
 
 def run(w: str, c: Ctx, weak: bool = False) -> dict:
     """One workload: setup, timed steps, its bench-line fields."""
+    if w == "fftreal1024":
+        return run_fftreal1024(c)
     wl = setup(w, c, weak=weak)
     m = measure(wl, c)
     check = parity(w, wl, c)
@@ -348,6 +526,7 @@ def run(w: str, c: Ctx, weak: bool = False) -> dict:
         "roofline": {"bound": "hbm", "kernel": wl["kernel"],
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "frac_vs_copy": round(achieved / HBM_COPY_GBS, 4),
                      "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                      "alg_bytes_per_launch": wl["alg_bytes"], "traffic": traffic},
         "fp64": fp64_info(w, avg_launch_s, share),
@@ -445,6 +624,40 @@ def cpu_baseline(workload: str, seconds: float):
     import oracle
     cores = min(os.cpu_count() or 1, 16)  # the GPU box's CPU share is 16
     pool = f"reference worker pool of {cores} threads per radix-2 transform (radix2.go:89-151)"
+    out = _cpu_baseline(workload, seconds, cores, pool, np, oracle)
+    out["cpu_model"] = cpu_model()
+    return out
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def _cpu_baseline(workload: str, seconds: float, cores: int, pool: str, np, oracle) -> dict:
+    if workload == "fftreal1024":
+        # fft.FFTReal(N=1024) restated: ToComplex + radix2FFT, one call at a
+        # time on one thread (the reference's pool of goroutines is not
+        # restated here: OS threads per call would overstate its overhead)
+        x = oracle.fill_uniform(1024, SEED)
+        done = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            for _ in range(100):
+                oracle.fft_real(x)
+            done += 100
+        dt = time.perf_counter() - t0
+        return {"value": round(done * 1024 / dt / 1e9, 6), "unit": "Gsamples/s", "cores": 1,
+                "kind": "port", "us_per_call": round(dt / done * 1e6, 2),
+                "sample": f"{done} fft.FFTReal calls of N=1024 ({dt:.1f} s), one thread, "
+                          f"called from Python (ctypes) like the GPU line"}
     if workload == "pwelch":
         n = 1 << 20
         t0 = time.perf_counter()

@@ -282,11 +282,62 @@ __device__ __forceinline__ cd pass_base(const cd *__restrict__ tw, int j) {
   return tw[(j & (NS - 1)) * (N / (NS * R))];
 }
 
+// Twiddles held in registers (a persistent kernel's loop over many
+// transforms of one geometry, every pass of radix R with one butterfly per
+// thread, j = t): pass p's base W_{NS R}^(t % NS) is the same for every
+// transform, so it is read once per kernel instead of from a table per
+// transform; with RH = R - 1, pass 1's powers base^1..base^(R-1) are held too
+// (its power chain then runs once per kernel). Passed as fft_regs' TWP.
+template <int NP, int RH = 0>
+struct RegTw {
+  static constexpr int HELD = RH;
+  cd base[NP];          // base[p], p >= 1
+  cd pw[RH > 0 ? RH : 1];  // pass 1: base[1]^(r+1), r < RH
+};
+template <class T>
+struct is_regtw {
+  static constexpr bool v = false;
+  static constexpr int held = 0;
+};
+template <int NP, int RH>
+struct is_regtw<RegTw<NP, RH>> {
+  static constexpr bool v = true;
+  static constexpr int held = RH;
+};
+
+// the powers w^1..w^(R-1) as pass_compute forms them (two interleaved
+// recurrences, odd and even exponents): pw[r-1] = w^r
+template <int R>
+__device__ __forceinline__ void twiddle_powers(cd w, cd (&pw)[R - 1]) {
+  pw[0] = w;
+  if constexpr (R > 2) {
+    const cd w2 = cmul(w, w);
+    cd wo = w, we = w2;
+    pw[1] = w2;
+#pragma unroll
+    for (int r = 3; r < R; ++r) {
+      if (r & 1) {
+        wo = cmul(wo, w2);
+        pw[r - 1] = wo;
+      } else {
+        we = cmul(we, w2);
+        pw[r - 1] = we;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ cd opaque_cd(cd w) {
+  asm volatile("" : "+v"(w.x), "+v"(w.y));
+  return w;
+}
+
 // WPRE: the butterflies' twiddle bases come in wpre[b] (loaded by the caller
 // a pass ahead: fft_regs PREW) instead of being read here
+// PASS: this pass's index (selects a RegTw's base / held powers)
 template <int N, int E, int T, int R, int NS, bool HALF_IN = false, class EPI = NoEpi,
-          bool WPRE = false>
-__device__ __forceinline__ void pass_compute(cd (&v)[E], int t, const cd *__restrict__ tw,
+          bool WPRE = false, int PASS = 0, class TWP = const cd *>
+__device__ __forceinline__ void pass_compute(cd (&v)[E], int t, TWP tw,
                                              const EPI &epi = EPI(), const cd *wpre = nullptr) {
   constexpr int B = E / R;
 #pragma unroll
@@ -301,12 +352,19 @@ __device__ __forceinline__ void pass_compute(cd (&v)[E], int t, const cd *__rest
     cd u[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) u[r] = v[b + r * B];
-    if constexpr (NS > 1) {
+    if constexpr (NS > 1 && PASS == 1 && is_regtw<TWP>::held == R - 1) {
+      static_assert(B == 1, "register twiddles need one butterfly per thread");
+#pragma unroll
+      for (int r = 1; r < R; ++r) u[r] = cmul(u[r], tw.pw[r - 1]);
+    } else if constexpr (NS > 1) {
       // W_{NS*R}^{(j%NS)*r}: one table read, powers by two interleaved
       // recurrences (odd and even exponents) to keep the product depth ~R/2
       cd w;
       if constexpr (WPRE) w = wpre[b];
-      else w = pass_base<N, R, NS>(tw, j);
+      else if constexpr (is_regtw<TWP>::v) {
+        static_assert(B == 1, "register twiddles need one butterfly per thread");
+        w = tw.base[PASS];
+      } else w = pass_base<N, R, NS>(tw, j);
       u[1] = cmul(u[1], w);
       if constexpr (R > 2) {
         const cd w2 = cmul(w, w);
@@ -370,31 +428,76 @@ __device__ __forceinline__ int lds_off(int i) {
   else return padi(i);
 }
 
-template <int N, int E, int T, int R, int NS, bool SPLIT, int ILV = 0, bool LINEAR = false>
+// LAYOUT 2 (E = 16, T >= 32): the first exchange (after a pass with NS = 1,
+// whose stride-E writes need the XOR swizzle) as XOR; every later one as
+// i + 16 * (i / 256): its writes are runs of >= 16 contiguous slots and its
+// reads runs of 32, so a 16-slot shift per 256-block keeps both
+// conflict-free, and every address is a per-thread base plus a compile-time
+// offset (no vector instruction per element).
+template <int ILV, int E, bool XOR, int LAYOUT, int NS_PREV>
+__device__ __forceinline__ int xoff(int i) {
+  if constexpr (LAYOUT == 2 && ILV == 0 && XOR && E == 16 && NS_PREV > 1)
+    return i + ((i >> 8) << 4);
+  else
+    return lds_off<ILV, E, XOR, LAYOUT == 1>(i);
+}
+
+template <int N, int E, int T, int R, int NS, bool SPLIT, int ILV = 0, int LAYOUT = 0>
 __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, double *lim,
                                               bool first) {
   constexpr int B = E / R;
+  // LAYOUT 2 with one butterfly per thread and T = 256 (N = 4096, E = 16),
+  // written out so the compiler sees the per-thread base: the first exchange
+  // writes 16 t + (r ^ (t & 15)) and reads (t ^ ((t >> 4) & 15)) + 256 k; the
+  // second (NS R = 256) writes (t / NS) 272 + t % NS + r NS and reads
+  // t + 272 k
+  constexpr bool L2 = LAYOUT == 2 && ILV == 0 && E == 16 && T == 256 && B == 1 &&
+                      (NS == 1 || NS * R == 256);
   int dst[E];
+  if constexpr (L2 && NS == 1) {
+    const int m = t & 15;
 #pragma unroll
-  for (int b = 0; b < B; ++b) {
-    const int j = t + b * T;
-    const int base = (j / NS) * (NS * R) + (j & (NS - 1));
+    for (int r = 0; r < R; ++r) dst[r] = 16 * t + (r ^ m);
+  } else if constexpr (L2) {
+    const int base = (t / NS) * 272 + (t & (NS - 1));
 #pragma unroll
-    for (int r = 0; r < R; ++r) dst[b + r * B] = lds_off<ILV, E, (T >= 32), (LINEAR && T >= 32)>(base + r * NS);
+    for (int r = 0; r < R; ++r) dst[r] = base + r * NS;
+  } else {
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const int j = t + b * T;
+      const int base = (j / NS) * (NS * R) + (j & (NS - 1));
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        dst[b + r * B] = xoff<ILV, E, (T >= 32), (T >= 32 ? LAYOUT : 0), NS>(base + r * NS);
+    }
   }
+  // reads of element t + k T: rbase + k rstep
+  int rbase = 0, rstep = 0;
+  if constexpr (L2 && NS == 1) {
+    rbase = t ^ ((t >> 4) & 15);
+    rstep = 256;
+  } else if constexpr (L2) {
+    rbase = t;
+    rstep = 272;
+  }
+  auto src = [&](int k) -> int {
+    if constexpr (L2) return rbase + k * rstep;
+    else return xoff<ILV, E, (T >= 32), (T >= 32 ? LAYOUT : 0), NS>(t + k * T);
+  };
   if (!first) __syncthreads();
   if constexpr (SPLIT) {
 #pragma unroll
     for (int k = 0; k < E; ++k) lre[dst[k]] = v[k].x;
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < E; ++k) v[k].x = lre[lds_off<ILV, E, (T >= 32), (LINEAR && T >= 32)>(t + k * T)];
+    for (int k = 0; k < E; ++k) v[k].x = lre[src(k)];
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < E; ++k) lre[dst[k]] = v[k].y;
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < E; ++k) v[k].y = lre[lds_off<ILV, E, (T >= 32), (LINEAR && T >= 32)>(t + k * T)];
+    for (int k = 0; k < E; ++k) v[k].y = lre[src(k)];
   } else {
 #pragma unroll
     for (int k = 0; k < E; ++k) {
@@ -403,8 +506,10 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < E; ++k)
-      v[k] = {lre[lds_off<ILV, E, (T >= 32), (LINEAR && T >= 32)>(t + k * T)], lim[lds_off<ILV, E, (T >= 32), (LINEAR && T >= 32)>(t + k * T)]};
+    for (int k = 0; k < E; ++k) {
+      const int o = src(k);
+      v[k] = {lre[o], lim[o]};
+    }
   }
 }
 
@@ -446,7 +551,7 @@ using RegArr = cd[Geo<LOG2N, LOG2E>::E];
 // latency hides behind that work instead of opening the pass; only for
 // passes with at most PREW bases per thread (0: off)
 template <int LOG2N, bool SPLIT, int OPAQUE = 0, int LOG2E = 4, int ILV = 0, int P = 0,
-          class TWP = const cd *, bool LINEAR = false, bool HALF_IN = false, class EPI = NoEpi,
+          class TWP = const cd *, int LINEAR = 0, bool HALF_IN = false, class EPI = NoEpi,
           int PREW = 0>
 __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw, double *lre,
                                          double *lim, bool first_exchange = true,
@@ -454,7 +559,7 @@ __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw,
   using G = Geo<LOG2N, LOG2E>;
   if constexpr (OPAQUE && P == 0 && G::NPASS > 1) {
     t = opaque_int(t);
-    if constexpr (OPAQUE == 1) tw = opaque_ptr(tw);
+    if constexpr (OPAQUE == 1 && !is_regtw<TWP>::v) tw = opaque_ptr(tw);
   }
   if constexpr (P < G::NPASS) {
     constexpr int R = G::radix(P);
@@ -477,10 +582,11 @@ __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw,
     }
     constexpr bool USE_PRE = PREW >= G::E / R && P > 0 && NS > 1;
     if constexpr (P == G::NPASS - 1)
-      pass_compute<G::N, G::E, G::T, R, NS, HALF_IN && P == 0, EPI, USE_PRE>(v, t, tw, epi, wpre);
+      pass_compute<G::N, G::E, G::T, R, NS, HALF_IN && P == 0, EPI, USE_PRE, P, TWP>(v, t, tw, epi,
+                                                                                    wpre);
     else
-      pass_compute<G::N, G::E, G::T, R, NS, HALF_IN && P == 0, NoEpi, USE_PRE>(v, t, tw, NoEpi(),
-                                                                                wpre);
+      pass_compute<G::N, G::E, G::T, R, NS, HALF_IN && P == 0, NoEpi, USE_PRE, P, TWP>(
+          v, t, tw, NoEpi(), wpre);
     fft_regs<LOG2N, SPLIT, 0, LOG2E, ILV, P + 1, TWP, LINEAR, false, EPI, PREW>(
         v, t, tw, lre, lim, first_exchange, epi, PRE_NEXT ? wn : nullptr);
   }

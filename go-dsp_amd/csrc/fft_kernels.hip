@@ -500,8 +500,16 @@ constexpr bool kPwLinear = true;
 #else
 constexpr bool kPwLinear = false;
 #endif
+// TWM: where the pass twiddles come from. 0 the global table (L1/L2) per
+// pair. 1 the bases T_N[0 .. N/R_last) in an LDS table, and the next pair's
+// samples prefetched while this pair's FFT runs (the only global loads left
+// in the loop are the samples, so vmcnt covers only them). 2 as 1, but each
+// pass's base (one butterfly per thread: W_{NS R}^(t % NS), the same for
+// every pair) read once per kernel into registers. 3 as 2, with pass 1's
+// powers held in registers too (its power chain runs once per kernel). 4 as
+// 3 without the next-pair sample prefetch (the registers it held).
 template <int LOG2F, int WMODE = 2, int MINW = 1, int LOG2E = 4, bool SPLIT = true,
-          bool PF = false>
+          int TWM = 0>
 __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_kernel(
     const double *__restrict__ x, int64_t seg_begin, int64_t seg_end, int64_t pairs_per_worker,
     const double *__restrict__ win, const cd *__restrict__ tw, double *__restrict__ partial) {
@@ -509,13 +517,18 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_ker
   constexpr int E = G::E, H = E / 2;
   constexpr int64_t STRIDE = G::N / 2;
   constexpr int XD = (SPLIT ? 1 : 2) * G::LDS_DOUBLES;  // exchange buffer(s)
-  // PF: the pass twiddle bases (T_N[0 .. N/R_last)) live in LDS, so the only
-  // global loads in the loop are the samples, and the next pair's samples are
-  // prefetched while this pair's FFT runs (vmcnt then covers only them)
-  constexpr int TWN = PF ? G::N / G::radix(G::NPASS - 1) : 0;
+  constexpr bool PF = TWM >= 1 && TWM <= 3;
+  constexpr bool REGTW = TWM >= 2;
+  static_assert(!REGTW || (G::E == G::EMAX && G::NPE == G::NPASS),
+                "register twiddles need radix-E passes with one butterfly per thread");
+  constexpr int TWN = TWM == 1 ? G::N / G::radix(G::NPASS - 1) : 0;
   __shared__ double lds[XD + (WMODE == 2 ? G::N : 0) + 2 * TWN];
   const int lt = threadIdx.x;
-  const int slot = lt / G::T;
+  // one worker per workgroup (TPW = 1, F >= 4096): the worker index, its
+  // pairs, their segment offsets and the active / has-partner tests are
+  // wave-uniform (scalar registers and branches), and the sample loads are
+  // a scalar row base plus the lane's 32-bit offset
+  const int slot = G::TPW == 1 ? 0 : lt / G::T;
   const int t = lt & (G::T - 1);
   const int64_t worker = (int64_t)blockIdx.x * G::TPW + slot;
   double *lre = lds + slot * G::STRIDE;
@@ -530,10 +543,21 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_ker
     for (int i = lt; i < G::N; i += G::WG) wl[i] = win[i];
   }
   cd *twl = reinterpret_cast<cd *>(lds + XD + (WMODE == 2 ? G::N : 0));
-  if constexpr (PF) {
+  if constexpr (TWM == 1) {
     for (int i = lt; i < TWN; i += G::WG) twl[i] = tw[i];
   }
-  if constexpr (WMODE == 2 || PF) __syncthreads();
+  using RT = RegTw<G::NPASS, TWM >= 3 ? G::EMAX - 1 : 0>;
+  RT rtw;
+  if constexpr (REGTW) {
+#pragma unroll
+    for (int p = 1; p < G::NPASS; ++p) rtw.base[p] = {0.0, 0.0};
+    if constexpr (G::NPASS > 1) rtw.base[1] = pass_base<G::N, G::EMAX, G::ns(1)>(tw, t);
+    if constexpr (G::NPASS > 2) rtw.base[2] = pass_base<G::N, G::EMAX, G::ns(2)>(tw, t);
+    if constexpr (G::NPASS > 3) rtw.base[3] = pass_base<G::N, G::EMAX, G::ns(3)>(tw, t);
+    static_assert(G::NPASS <= 4, "bases of up to 4 passes");
+    if constexpr (TWM >= 3 && G::NPASS > 1) twiddle_powers<G::EMAX>(rtw.base[1], rtw.pw);
+  }
+  if constexpr (WMODE == 2 || TWM == 1) __syncthreads();
   double acc[E];
 #pragma unroll
   for (int k = 0; k < E; ++k) acc[k] = 0.0;
@@ -552,11 +576,30 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_ker
     const bool active = p < npairs;
     const int64_t s0 = seg_begin + 2 * p;
     const bool has1 = active && (s0 + 1 < seg_end);
-    const double *b = opaque_ptr(x) + s0 * STRIDE + t;
+    if constexpr (G::TPW == 1) {
+      const double *b = opaque_ptr(x) + s0 * STRIDE;
+      const uint32_t lane = (uint32_t)t;
+      if (active) {
 #pragma unroll
-    for (int k = 0; k < H; ++k) {
-      a2[k] = active ? b[(H + k) * G::T] : 0.0;
-      c2[k] = has1 ? b[(E + k) * G::T] : 0.0;
+        for (int k = 0; k < H; ++k) a2[k] = (b + (H + k) * G::T)[lane];
+      } else {
+#pragma unroll
+        for (int k = 0; k < H; ++k) a2[k] = 0.0;
+      }
+      if (has1) {
+#pragma unroll
+        for (int k = 0; k < H; ++k) c2[k] = (b + (E + k) * G::T)[lane];
+      } else {
+#pragma unroll
+        for (int k = 0; k < H; ++k) c2[k] = 0.0;
+      }
+    } else {
+      const double *b = opaque_ptr(x) + s0 * STRIDE + t;
+#pragma unroll
+      for (int k = 0; k < H; ++k) {
+        a2[k] = active ? b[(H + k) * G::T] : 0.0;
+        c2[k] = has1 ? b[(E + k) * G::T] : 0.0;
+      }
     }
   };
   double na2[H], nc2[H];  // PF: the next pair's samples, in flight
@@ -595,7 +638,15 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_ker
     }
 #pragma unroll
     for (int k = 0; k < H; ++k) carry[k] = c2[k];
-    if constexpr (PF)
+    if constexpr (REGTW) {
+      // the bases are re-laundered every pair so the compiler does not hoist
+      // the per-pass power chains out of the loop (registers)
+      RT rl = rtw;
+#pragma unroll
+      for (int p = 1; p < G::NPASS; ++p) rl.base[p] = opaque_cd(rl.base[p]);
+      fft_regs<LOG2F, SPLIT, 2, LOG2E, 0, 0, RT, kPwLinear, false, NoEpi, 0>(
+          v, opaque_int(t), rl, lre, lim, it == 0);
+    } else if constexpr (PF)
       fft_regs<LOG2F, SPLIT, 2, LOG2E, 0, 0, const cd *, kPwLinear, false, NoEpi, kPwPrew>(
           v, opaque_int(t), (const cd *)twl, lre, lim, it == 0);
     else
@@ -611,6 +662,105 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_ker
 #pragma unroll
     for (int k = 0; k < E; ++k) dst[t + k * G::T] = acc[k];
   }
+}
+
+// Half-overlap Pwelch with one worker per workgroup (TPW = 1: F >= 4096, the
+// BASELINE configuration). Same packing, carry and accumulation as
+// pwelch_half_kernel, arranged so that the loop's bookkeeping costs no
+// vector instructions:
+//  - the worker's pair range, segment offsets and the has-partner test are
+//    wave-uniform (scalar registers and branches); the loop runs over the
+//    worker's own pairs only, full pairs first, then at most one pair whose
+//    second segment does not exist (odd count: zero partner, its own body);
+//  - each sample row is a scalar base pointer plus the lane's 32-bit offset
+//    (global_load saddr: no 64-bit address arithmetic per load);
+//  - the next pair's samples are loaded into the registers this pair's
+//    samples just left (after the window multiply), so they are in flight
+//    during the FFT with no double buffer to copy between;
+//  - REGTW: each pass's twiddle base (the same for every pair) is read once
+//    per kernel into registers (no LDS table, no bank conflicts on it).
+template <int LOG2F, int LOG2E = 4, bool REGTW = true, int LAYOUT = 2>
+__global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_row_kernel(
+    const double *__restrict__ x, int64_t seg_begin, int64_t seg_end, int64_t pairs_per_worker,
+    const double *__restrict__ win, const cd *__restrict__ tw, double *__restrict__ partial) {
+  using G = Geo<LOG2F, LOG2E>;
+  static_assert(G::TPW == 1, "one worker per workgroup");
+  static_assert(!REGTW || (G::E == G::EMAX && G::NPE == G::NPASS && G::NPASS <= 4),
+                "register twiddles need radix-E passes with one butterfly per thread");
+  constexpr int E = G::E, H = E / 2, T = G::T;
+  constexpr int64_t STRIDE = G::N / 2;
+  __shared__ double lds[G::LDS_DOUBLES + G::N];
+  double *const lx = lds;                   // exchange (real / imaginary halves in turn)
+  double *const wl = lds + G::LDS_DOUBLES;  // window
+  const int t = threadIdx.x;
+  const uint32_t lane = (uint32_t)t;
+  for (int i = t; i < G::N; i += G::WG) wl[i] = win[i];
+  using RT = RegTw<G::NPASS, 0>;
+  RT rtw;
+#pragma unroll
+  for (int p = 0; p < G::NPASS; ++p) rtw.base[p] = {1.0, 0.0};
+  if constexpr (REGTW) {
+    if constexpr (G::NPASS > 1) rtw.base[1] = pass_base<G::N, G::EMAX, G::ns(1)>(tw, t);
+    if constexpr (G::NPASS > 2) rtw.base[2] = pass_base<G::N, G::EMAX, G::ns(2)>(tw, t);
+    if constexpr (G::NPASS > 3) rtw.base[3] = pass_base<G::N, G::EMAX, G::ns(3)>(tw, t);
+  }
+  __syncthreads();
+  const int64_t npairs = (seg_end - seg_begin + 1) / 2;  // pairs, the last maybe partnerless
+  const int64_t nfull = (seg_end - seg_begin) / 2;       // pairs with both segments
+  const int64_t p0 = (int64_t)blockIdx.x * pairs_per_worker;
+  const int64_t pend = p0 + pairs_per_worker < npairs ? p0 + pairs_per_worker : npairs;
+  const int64_t fend = pend < nfull ? pend : nfull;
+  if (p0 >= pend) return;  // whole workgroup (uniform): no barrier follows
+  // row r of a pair's samples: x[(seg_begin + 2p) STRIDE + r T + lane]; the
+  // rows a pair needs beyond its carry are H .. 2E-1 ... as scalar pointers
+  auto row = [&](int64_t p, int r) -> const double * {
+    return opaque_ptr(x + (seg_begin + 2 * p) * STRIDE + (int64_t)r * T);
+  };
+  double carry[H], a2[H], c2[H];
+#pragma unroll
+  for (int k = 0; k < H; ++k) carry[k] = row(p0, k)[lane];
+  // samples of pair p: a = (carry, a2) is segment s0, (a2, c2) segment s0+1;
+  // c2 of a partnerless pair is not read (its rows are clamped onto a2's)
+  auto issue = [&](int64_t p) {
+    const int cr = p < nfull ? E : H;
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      a2[k] = row(p, H + k)[lane];
+      c2[k] = row(p, cr + k)[lane];
+    }
+  };
+  issue(p0);
+  double acc[E];
+#pragma unroll
+  for (int k = 0; k < E; ++k) acc[k] = 0.0;
+  auto pair = [&](int64_t p, bool first, bool partner) {
+    const int tt = opaque_int(t);
+    cd v[E];
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      const double w0 = wl[tt + k * T], w1 = wl[tt + (H + k) * T];
+      v[k] = {carry[k] * w0, partner ? a2[k] * w0 : 0.0};
+      v[H + k] = {a2[k] * w1, partner ? c2[k] * w1 : 0.0};
+    }
+#pragma unroll
+    for (int k = 0; k < H; ++k) carry[k] = c2[k];
+    if (p + 1 < pend) issue(p + 1);
+    RT rl = rtw;
+#pragma unroll
+    for (int q = 1; q < G::NPASS; ++q) rl.base[q] = opaque_cd(rl.base[q]);
+    if constexpr (REGTW)
+      fft_regs<LOG2F, true, 2, LOG2E, 0, 0, RT, LAYOUT, false, NoEpi, 0>(v, tt, rl, lx, lx, first);
+    else
+      fft_regs<LOG2F, true, 1, LOG2E, 0, 0, const cd *, LAYOUT>(v, tt, tw, lx, lx, first);
+#pragma unroll
+    for (int k = 0; k < E; ++k) acc[k] = fma(v[k].y, v[k].y, fma(v[k].x, v[k].x, acc[k]));
+  };
+  int64_t p = p0;
+  for (; p < fend; ++p) pair(p, p == p0, true);
+  if (p < pend) pair(p, p == p0, false);  // the odd count's last segment, zero partner
+  double *dst = partial + blockIdx.x * (int64_t)G::N;
+#pragma unroll
+  for (int k = 0; k < E; ++k) dst[t + k * T] = acc[k];
 }
 
 // Deterministic two-level reduction of the per-worker partial spectra:
@@ -1129,14 +1279,14 @@ static hipError_t launch_pw_t(const double *x, int64_t nfft, int64_t stride, int
 }
 
 template <int LOG2F, int WMODE = 2, int MINW = 1, int LOG2E = 4, bool SPLIT = true,
-          bool PF = false>
+          int TWM = 0>
 static hipError_t launch_pwh_t(const double *x, int64_t seg_begin, int64_t seg_end, int64_t ppw,
                                int64_t nworkers, const double *win, const cd *tw, double *partial,
                                hipStream_t s) {
   using G = Geo<LOG2F, LOG2E>;
   if (G::TPW != Geo<LOG2F>::TPW) return hipErrorInvalidValue;  // workers per block
   const int64_t nblk = (nworkers + G::TPW - 1) / G::TPW;
-  hipLaunchKernelGGL((pwelch_half_kernel<LOG2F, WMODE, MINW, LOG2E, SPLIT, PF>), dim3((unsigned)nblk), dim3(G::WG), 0, s,
+  hipLaunchKernelGGL((pwelch_half_kernel<LOG2F, WMODE, MINW, LOG2E, SPLIT, TWM>), dim3((unsigned)nblk), dim3(G::WG), 0, s,
                      x, seg_begin, seg_end, ppw, win, tw, partial);
   return hipGetLastError();
 }
@@ -1159,8 +1309,22 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
       }();
       if (shfl)
         return launch_pwelch4096_shfl(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
-      return launch_pwh_t<12, 2, 1, 4, true, true>(x, seg_begin, seg_end, ppw, nworkers, win, tw,
-                                                   partial, s);
+#ifndef GDSP_PW_TWM
+#define GDSP_PW_TWM 1
+#endif
+#ifndef GDSP_PW_ROW
+#define GDSP_PW_ROW 1
+#endif
+#ifndef GDSP_PW_LAYOUT
+#define GDSP_PW_LAYOUT 2
+#endif
+      if (GDSP_PW_ROW) {
+        hipLaunchKernelGGL((pwelch_row_kernel<12, 4, GDSP_PW_ROW == 1, GDSP_PW_LAYOUT>), dim3((unsigned)nworkers),
+                           dim3(Geo<12>::WG), 0, s, x, seg_begin, seg_end, ppw, win, tw, partial);
+        return hipGetLastError();
+      }
+      return launch_pwh_t<12, 2, 1, 4, true, GDSP_PW_TWM>(x, seg_begin, seg_end, ppw, nworkers,
+                                                          win, tw, partial, s);
     }
     GDSP_PWH(13)
 #undef GDSP_PWH

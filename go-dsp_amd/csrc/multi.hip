@@ -27,6 +27,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <functional>
 #include <map>
@@ -62,8 +63,11 @@ using gdsp_api::set_error;
 // ---- device set -------------------------------------------------------------
 
 std::mutex g_set_mu;
-std::vector<int> g_set;  // empty: every visible device (or GDSP_DEVICES)
+std::vector<int> g_set;  // empty: the calling thread's current device (or GDSP_DEVICES)
 bool g_set_env_read = false;
+
+// call counters for tests and diagnostics (gdsp_multi_stats)
+std::atomic<int64_t> g_batch_calls{0}, g_pwelch_calls{0}, g_rccl_reduces{0}, g_host_reduces{0};
 
 int visible_devices() {
   int c = 0;
@@ -71,6 +75,10 @@ int visible_devices() {
   return c;
 }
 
+// A device may be listed more than once: its shards then run side by side
+// on separate worker streams of that device (and a Pwelch over such a set
+// combines its accumulators on the host, since an RCCL clique needs
+// distinct devices).
 int validate(const int *devices, int ndev, int count, std::vector<int> &out) {
   out.clear();
   for (int i = 0; i < ndev; ++i) {
@@ -78,46 +86,54 @@ int validate(const int *devices, int ndev, int count, std::vector<int> &out) {
     if (d < 0 || d >= count)
       return set_error(GDSP_ERR_INVALID, "device " + std::to_string(d) + " not visible (" +
                                              std::to_string(count) + " devices)");
-    for (int e : out)
-      if (e == d) return set_error(GDSP_ERR_INVALID, "device listed twice");
     out.push_back(d);
   }
   return GDSP_OK;
 }
 
-// GDSP_DEVICES="0,2,3": the initial device set of a process (deployment knob).
+// GDSP_DEVICES="0,2,3" or "all": the initial device set of a process
+// (deployment knob). Unset, a call uses the calling thread's current device.
 void read_env_locked(int count) {
   if (g_set_env_read) return;
   g_set_env_read = true;
   const char *e = getenv("GDSP_DEVICES");
   if (!e || !*e) return;
   std::vector<int> ids;
-  for (const char *p = e; *p;) {
-    char *end = nullptr;
-    const long v = strtol(p, &end, 10);
-    if (end == p) break;
-    ids.push_back((int)v);
-    p = *end == ',' ? end + 1 : end;
+  if (strcmp(e, "all") == 0) {
+    for (int d = 0; d < count; ++d) ids.push_back(d);
+  } else {
+    for (const char *p = e; *p;) {
+      char *end = nullptr;
+      const long v = strtol(p, &end, 10);
+      if (end == p) break;
+      ids.push_back((int)v);
+      p = *end == ',' ? end + 1 : end;
+    }
   }
   std::vector<int> ok;
   if (validate(ids.data(), (int)ids.size(), count, ok) == GDSP_OK) g_set = ok;
 }
 
 // The devices of a call: the explicit list, else the library's set, else
-// every visible device.
-int resolve(const int *devices, int ndev, std::vector<int> &out) {
+// the calling thread's current device.
+int resolve(const int *devices, int ndev, std::vector<int> &out, bool *configured = nullptr) {
   const int count = visible_devices();
+  if (configured) *configured = false;
   if (count <= 0) return set_error(GDSP_ERR_NO_DEVICE, "no HIP device visible");
   if (ndev < 0) return set_error(GDSP_ERR_INVALID, "negative device count");
   if (devices && ndev > 0) return validate(devices, ndev, count, out);
-  std::lock_guard<std::mutex> lk(g_set_mu);
-  read_env_locked(count);
-  if (!g_set.empty()) {
-    out = g_set;
-    return GDSP_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_set_mu);
+    read_env_locked(count);
+    if (!g_set.empty()) {
+      out = g_set;
+      if (configured) *configured = true;
+      return GDSP_OK;
+    }
   }
-  out.clear();
-  for (int d = 0; d < count; ++d) out.push_back(d);
+  int cur = 0;
+  if (hipGetDevice(&cur) != hipSuccess) return set_error(GDSP_ERR_NO_DEVICE, "hipGetDevice failed");
+  out.assign(1, cur);
   return GDSP_OK;
 }
 
@@ -296,11 +312,16 @@ int64_t multi_min_bytes() {
 
 namespace gdsp_api {
 
+// Automatic routing of the plain host entries is opt-in: only a configured
+// set (gdsp_set_devices or GDSP_DEVICES) of more than one entry splits a
+// call; by default every call stays on the caller's current device, so a
+// one-rank-per-GPU job never fans out onto its neighbours' GPUs.
 bool multi_wanted(size_t bytes, int64_t units) {
   if (units < 2 || (int64_t)bytes < multi_min_bytes()) return false;
   std::vector<int> devs;
-  if (resolve(nullptr, 0, devs) != GDSP_OK) return false;
-  return devs.size() > 1;
+  bool configured = false;
+  if (resolve(nullptr, 0, devs, &configured) != GDSP_OK) return false;
+  return configured && devs.size() > 1;
 }
 
 int fft_batch_multi(const void *x, size_t in_elem_bytes, double *out, int64_t n, int64_t batch,
@@ -311,6 +332,7 @@ int fft_batch_multi(const void *x, size_t in_elem_bytes, double *out, int64_t n,
   if (batch == 0 || n == 0) return batch_on_current_device(x, in_elem_bytes, out, n, batch, inv, load);
   if (!x || !out) return set_error(GDSP_ERR_INVALID, "NULL pointer");
   const int parts = (int)std::min<int64_t>((int64_t)devs.size(), batch);
+  ++g_batch_calls;
   return Pool::get().run(parts, [&](int i) -> int {
     int64_t lo, hi;
     shard(batch, parts, i, &lo, &hi);
@@ -320,6 +342,37 @@ int fft_batch_multi(const void *x, size_t in_elem_bytes, double *out, int64_t n,
                                    out + (size_t)lo * row_out, n, hi - lo, inv, load);
   });
 }
+
+// All workers of one Pool::run meet here between accumulating and reducing:
+// the collective starts only when every shard has its accumulator, so a
+// failing shard cannot leave the others waiting inside it.
+class Rendezvous {
+ public:
+  explicit Rendezvous(int n) : n_(n) {}
+  // true when every worker arrived without failing
+  bool arrive(bool ok) {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (!ok) failed_ = true;
+    if (++arrived_ == n_) cv_.notify_all();
+    else cv_.wait(lk, [this] { return arrived_ == n_; });
+    return !failed_;
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int n_, arrived_ = 0;
+  bool failed_ = false;
+};
+
+// Device buffer owned by one call (the accumulators the reduce reads: never
+// a worker's shared scratch, which the next call would reuse).
+struct CallBuf {
+  void *p = nullptr;
+  ~CallBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
 
 int pwelch_multi(const double *x, int64_t n, double fs, int64_t nfft, int64_t pad,
                  int64_t noverlap, const double *win_seg, const double *win_nfft, int scale_off,
@@ -362,60 +415,73 @@ int pwelch_multi(const double *x, int64_t n, double fs, int64_t nfft, int64_t pa
       }
     } guard;
     const int D = (int)devs.size();
+    // RCCL over a clique of the (distinct) devices; a set that repeats a
+    // device, or a process without a usable librccl, sums the D
+    // accumulators (flen float64 each) on the host in device order instead
+    std::vector<int> sorted(devs);
+    std::sort(sorted.begin(), sorted.end());
+    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
     std::vector<ncclComm_t> *comms = nullptr;
-    MSTCHK(comms_for(devs, &comms));
-    std::vector<double *> dacc(D, nullptr);
-    // phase 1: every device accumulates its shard (no collective yet, so a
-    // failing shard cannot leave the others waiting inside one)
+    const bool use_rccl = distinct && comms_for(devs, &comms) == GDSP_OK;
+    std::vector<std::vector<double>> part(use_rccl ? 1 : D);
+    Rendezvous meet(D);
+    ++g_pwelch_calls;
+    // one Pool::run holds the whole call (accumulate, reduce, copy back), so
+    // concurrent calls from other host threads queue behind it and never
+    // share its accumulators, streams or clique
     MSTCHK(Pool::get().run(D, [&](int i) -> int {
-      MHIPCHK(hipSetDevice(devs[i]));
-      hipStream_t s = stream_for(devs[i]);
-      if (!s) return set_error(GDSP_ERR_HIP, "stream creation failed");
-      int64_t seg_lo, seg_hi, x_lo, x_hi;
-      pwelch_shard(nsegs, nfft, noverlap, D, i, &seg_lo, &seg_hi, &x_lo, &x_hi);
-      void *dx = nullptr, *dw = nullptr, *da = nullptr;
-      const int64_t len = x_hi - x_lo;
-      MSTCHK(scratch((size_t)(len > 0 ? len : 1) * sizeof(double), s, SCRATCH_SIGNAL, &dx));
-      MSTCHK(scratch((size_t)flen * sizeof(double), s, SCRATCH_WINDOW, &dw));
-      MSTCHK(scratch((size_t)flen * sizeof(double), s, SCRATCH_ACC, &da));
-      MHIPCHK(hipMemsetAsync(da, 0, (size_t)flen * sizeof(double), s));
-      if (len > 0) {
-        const int64_t have = (x_hi < n ? x_hi : n) - x_lo;  // past n: ZeroPadF's zeros
-        if (have < len)
-          MHIPCHK(hipMemsetAsync(dx, 0, (size_t)len * sizeof(double), s));
-        if (have > 0) MSTCHK(h2d(dx, x + x_lo, (size_t)have * sizeof(double), s));
-        MSTCHK(h2d(dw, win_seg, (size_t)flen * sizeof(double), s));
-        MSTCHK(gdsp_pwelch_accumulate_device((const double *)dx, len, nfft, pad, noverlap, 0,
-                                             seg_hi - seg_lo, (const double *)dw, (double *)da,
-                                             s));
+      CallBuf dacc;
+      hipStream_t s = nullptr;
+      auto accumulate = [&]() -> int {
+        MHIPCHK(hipSetDevice(devs[i]));
+        s = stream_for(devs[i]);
+        if (!s) return set_error(GDSP_ERR_HIP, "stream creation failed");
+        int64_t seg_lo, seg_hi, x_lo, x_hi;
+        pwelch_shard(nsegs, nfft, noverlap, D, i, &seg_lo, &seg_hi, &x_lo, &x_hi);
+        void *dx = nullptr, *dw = nullptr;
+        const int64_t len = x_hi - x_lo;
+        MHIPCHK(hipMalloc(&dacc.p, (size_t)flen * sizeof(double)));
+        MSTCHK(scratch((size_t)(len > 0 ? len : 1) * sizeof(double), s, SCRATCH_SIGNAL, &dx));
+        MSTCHK(scratch((size_t)flen * sizeof(double), s, SCRATCH_WINDOW, &dw));
+        MHIPCHK(hipMemsetAsync(dacc.p, 0, (size_t)flen * sizeof(double), s));
+        if (len > 0) {
+          const int64_t have = (x_hi < n ? x_hi : n) - x_lo;  // past n: ZeroPadF's zeros
+          if (have < len) MHIPCHK(hipMemsetAsync(dx, 0, (size_t)len * sizeof(double), s));
+          if (have > 0) MSTCHK(h2d(dx, x + x_lo, (size_t)have * sizeof(double), s));
+          MSTCHK(h2d(dw, win_seg, (size_t)flen * sizeof(double), s));
+          MSTCHK(gdsp_pwelch_accumulate_device((const double *)dx, len, nfft, pad, noverlap, 0,
+                                               seg_hi - seg_lo, (const double *)dw,
+                                               (double *)dacc.p, s));
+        }
+        return GDSP_OK;
+      };
+      const int st = accumulate();
+      if (!meet.arrive(st == GDSP_OK)) return st != GDSP_OK ? st : GDSP_ERR_HIP;
+      double *da = (double *)dacc.p;
+      if (use_rccl) {
+        // every worker issues its rank's reduce on the stream that produced
+        // its accumulator; root 0 receives the sum
+        const Rccl &r = rccl();
+        const ncclResult_t e =
+            r.reduce(da, da, (size_t)flen, ncclFloat64, ncclSum, 0, (*comms)[i], s);
+        if (e != ncclSuccess) return nccl_fail(r, e, "ncclReduce");
+        if (i == 0) {
+          part[0].resize((size_t)flen);
+          return d2h(part[0].data(), da, (size_t)flen * sizeof(double), s);
+        }
+        MHIPCHK(hipStreamSynchronize(s));
+        return GDSP_OK;
       }
-      MHIPCHK(hipStreamSynchronize(s));
-      dacc[i] = (double *)da;
-      return GDSP_OK;
+      part[i].resize((size_t)flen);
+      return d2h(part[i].data(), da, (size_t)flen * sizeof(double), s);
     }));
-    // phase 2: one RCCL reduce (sum, float64) onto the first device, issued
-    // for the whole clique from this thread (ncclGroupStart/End)
-    const Rccl &r = rccl();
-    std::vector<hipStream_t> ss(D);
-    for (int i = 0; i < D; ++i) {
-      MHIPCHK(hipSetDevice(devs[i]));
-      ss[i] = stream_for(devs[i]);
-      if (!ss[i]) return set_error(GDSP_ERR_HIP, "stream creation failed");
-    }
-    ncclResult_t e = r.group_start();
-    if (e != ncclSuccess) return nccl_fail(r, e, "ncclGroupStart");
-    ncclResult_t first = ncclSuccess;
-    for (int i = 0; i < D; ++i) {
-      e = r.reduce(dacc[i], dacc[i], (size_t)flen, ncclFloat64, ncclSum, 0, (*comms)[i], ss[i]);
-      if (e != ncclSuccess && first == ncclSuccess) first = e;
-    }
-    e = r.group_end();
-    if (first != ncclSuccess) return nccl_fail(r, first, "ncclReduce");
-    if (e != ncclSuccess) return nccl_fail(r, e, "ncclGroupEnd");
-    for (int i = D - 1; i >= 0; --i) {
-      MHIPCHK(hipSetDevice(devs[i]));
-      if (i == 0) MSTCHK(d2h(acc.data(), dacc[0], (size_t)flen * sizeof(double), ss[0]));
-      else MHIPCHK(hipStreamSynchronize(ss[i]));
+    if (use_rccl) {
+      acc.swap(part[0]);
+      ++g_rccl_reduces;
+    } else {
+      for (int i = 0; i < D; ++i)
+        for (int64_t k = 0; k < flen; ++k) acc[(size_t)k] += part[i][(size_t)k];
+      ++g_host_reduces;
     }
   }
   MSTCHK(gdsp_pwelch_finalize(acc.data(), flen, nsegs, nfft, pad, win_nfft, fs, scale_off, pxx,
@@ -448,6 +514,15 @@ int gdsp_get_devices(int *devices, int cap) {
   if (resolve(nullptr, 0, v) != GDSP_OK) return 0;
   for (int i = 0; i < cap && i < (int)v.size(); ++i) devices[i] = v[i];
   return (int)v.size();
+}
+
+int gdsp_multi_stats(int64_t *batch_calls, int64_t *pwelch_calls, int64_t *rccl_reduces,
+                     int64_t *host_reduces) {
+  if (batch_calls) *batch_calls = g_batch_calls.load();
+  if (pwelch_calls) *pwelch_calls = g_pwelch_calls.load();
+  if (rccl_reduces) *rccl_reduces = g_rccl_reduces.load();
+  if (host_reduces) *host_reduces = g_host_reduces.load();
+  return GDSP_OK;
 }
 
 int gdsp_batch_shard(int64_t batch, int ndev, int i, int64_t *lo, int64_t *hi) {

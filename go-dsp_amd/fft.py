@@ -181,9 +181,11 @@ def _dev_array(devices):
 
 
 def SetDevices(devices=None) -> None:
-    """Device set of the host-pointer calls (gdsp_set_devices): large
-    FFTBatch / FFTRealBatch / spectral.Pwelch calls split over it. None or []
-    restores the default (every visible device, or GDSP_DEVICES)."""
+    """Device set of the host-pointer calls (gdsp_set_devices): once set to
+    more than one entry, large FFTBatch / FFTRealBatch / spectral.Pwelch calls
+    split over it. A device may repeat (its shards then share it on separate
+    streams). None or [] restores the default: the calling thread's current
+    device (or GDSP_DEVICES), i.e. no automatic split."""
     arr, n = _dev_array(devices or [])
     check(lib().gdsp_set_devices(arr, n), "SetDevices")
 
@@ -195,6 +197,16 @@ def Devices() -> list[int]:
     arr = (ctypes.c_int * max(n, 1))()
     n = int(lib().gdsp_get_devices(arr, n))
     return list(arr[:n])
+
+
+def MultiStats() -> dict:
+    """gdsp_multi_stats: calls split over a device set since process start,
+    and how Pwelch accumulators were combined."""
+    import ctypes
+    v = [ctypes.c_int64() for _ in range(4)]
+    check(lib().gdsp_multi_stats(*[ctypes.byref(a) for a in v]), "MultiStats")
+    return dict(zip(("batch_calls", "pwelch_calls", "rccl_reduces", "host_reduces"),
+                    (a.value for a in v)))
 
 
 def FFTBatchMulti(x, inverse: bool = False, devices=None) -> np.ndarray:

@@ -163,18 +163,30 @@ int gdsp_wav_read_floats(const void *in, int64_t count, int audio_format, int bi
  * splits its rows into contiguous shards, one per device, with no
  * collective; Pwelch splits its segments (each device reads its samples plus
  * the nfft - stride halo) and combines the per-device accumulators with one
- * in-process RCCL reduce (sum, float64) before the host finalises Pxx. */
+ * in-process RCCL reduce (sum, float64) before the host finalises Pxx. Each
+ * multi-device call runs whole (accumulate, reduce, copy back) before the
+ * next one from any host thread starts. */
 
-/* Library-wide device set used by gdsp_fft_batch, gdsp_fft_real_batch and
- * gdsp_pwelch when a call's input is at least GDSP_MULTI_MIN_BYTES (64 MiB by
- * default) and has at least 2 rows / segments; smaller calls stay on the
- * calling thread's current device. ndev = 0 restores the default: every
- * visible device (or the list in GDSP_DEVICES, e.g. "0,1,2,3"). Devices must
- * be visible and distinct. */
+/* Library-wide device set. When it has been configured (here, or by
+ * GDSP_DEVICES="0,1,2,3" / "all" at first use) with more than one entry,
+ * gdsp_fft_batch, gdsp_fft_real_batch and gdsp_pwelch split calls whose input
+ * is at least GDSP_MULTI_MIN_BYTES (64 MiB by default) and has at least 2
+ * rows / segments over it. Unconfigured (the default, or ndev = 0 here) the
+ * set is the calling thread's current device, so no call leaves it. A device
+ * may be listed more than once: its shards run side by side on separate
+ * streams (a Pwelch over such a set, or without a loadable librccl, sums the
+ * per-device accumulators on the host instead of by RCCL). Devices must be
+ * visible. */
 int gdsp_set_devices(const int *devices, int ndev);
 /* The current device set: writes up to cap ids, returns the set's size (0
  * without a GPU). */
 int gdsp_get_devices(int *devices, int cap);
+/* Multi-device calls since process start (diagnostics and tests): batched
+ * FFT calls and Pwelch calls split over a device set, and how the Pwelch
+ * accumulators were combined (RCCL reduce / host sum). Any pointer may be
+ * NULL. */
+int gdsp_multi_stats(int64_t *batch_calls, int64_t *pwelch_calls, int64_t *rccl_reduces,
+                     int64_t *host_reduces);
 
 /* fft.FFT / fft.IFFT over `batch` rows of n complex128 (as gdsp_fft_batch),
  * always split over `devices` (NULL or ndev = 0: the library's device set);
@@ -184,7 +196,8 @@ int gdsp_fft_batch_multi(const double *x, double *out, int64_t n, int64_t batch,
 
 /* spectral.Pwelch (as gdsp_pwelch), always split over `devices` (NULL or
  * ndev = 0: the library's device set) with the RCCL reduce of the per-bin
- * accumulators — also for a single device. */
+ * accumulators — also for a single device (host sum for a set that repeats
+ * a device). Thread-safe: the accumulators are owned by the call. */
 int gdsp_pwelch_multi(const double *x, int64_t n, double fs, int64_t nfft, int64_t pad,
                       int64_t noverlap, const double *win_seg, const double *win_nfft,
                       int scale_off, double *pxx, double *freqs, int64_t *lp_out,

@@ -106,17 +106,17 @@ def test_multi_entries_without_gpu(gdsp):
 @pytest.mark.gpu
 def test_device_set(gdsp):
     n = gdsp.device_count()
-    assert gdsp.fft.Devices() == list(range(n))
-    gdsp.fft.SetDevices([0])
+    # unconfigured: the calling thread's current device, so no call fans out
+    assert gdsp.fft.Devices() == [0]
+    gdsp.fft.SetDevices([0, 0])  # a device may repeat: shards share it
     try:
-        assert gdsp.fft.Devices() == [0]
-        with pytest.raises(gdsp.GDSPError):
-            gdsp.fft.SetDevices([0, 0])
+        assert gdsp.fft.Devices() == [0, 0]
         with pytest.raises(gdsp.GDSPError):
             gdsp.fft.SetDevices([n])
+        assert gdsp.fft.Devices() == [0, 0]  # a rejected list leaves the set alone
     finally:
         gdsp.fft.SetDevices(None)
-    assert gdsp.fft.Devices() == list(range(n))
+    assert gdsp.fft.Devices() == [0]
 
 
 @pytest.mark.gpu
@@ -155,15 +155,119 @@ def test_pwelch_multi_rccl_vs_oracle(gdsp, oracle, c):
 
 
 @pytest.mark.gpu
-def test_host_calls_route_over_device_set(gdsp, oracle, monkeypatch):
-    """gdsp_fft_batch / gdsp_pwelch split calls of >= GDSP_MULTI_MIN_BYTES
-    over the device set; with one device they stay on the single path. The
-    result is the same either way."""
+def test_shards_on_one_device_vs_oracle(gdsp, oracle):
+    """The shard logic of the multi-device calls on the one-GPU box: a device
+    set that repeats device 0 runs 3 shards side by side (own worker thread,
+    stream and staging each). Rows: offsets of every shard; Pwelch: segment
+    shards with their halo and the host sum of the 3 accumulators (an RCCL
+    clique needs distinct devices), against the reference restatement."""
+    st0 = gdsp.fft.MultiStats()
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((37, 3000)) + 1j * rng.standard_normal((37, 3000))
+    y = gdsp.fft.FFTBatchMulti(x, devices=[0, 0, 0])
+    assert max(nrel(a, b) for a, b in zip(y, oracle.fft_rows(x))) < 1e-9
+    for c in ({"n": 300001, "nfft": 4096, "noverlap": 2048, "pad": 0},
+              {"n": 30001, "nfft": 1000, "noverlap": 250, "pad": 2048},
+              {"n": 9000, "nfft": 4096, "noverlap": 2048, "pad": 0}):  # 3 segments, 3 shards
+        xs = np.sin(2 * np.pi * 0.1234 * np.arange(c["n"])) + 0.5 * rng.standard_normal(c["n"])
+        o = gdsp.spectral.PwelchOptions(NFFT=c["nfft"], Noverlap=c["noverlap"], Pad=c["pad"])
+        p, f = gdsp.spectral.PwelchMulti(xs, 2.0, o, devices=[0, 0, 0])
+        pr, fr = oracle.pwelch(xs, 2.0, c["nfft"], c["pad"], c["noverlap"])
+        assert nrel(p, pr) < 1e-9 and nrel(f, fr) < 1e-15, c
+    st1 = gdsp.fft.MultiStats()
+    assert st1["batch_calls"] == st0["batch_calls"] + 1
+    assert st1["pwelch_calls"] == st0["pwelch_calls"] + 3
+    assert st1["host_reduces"] == st0["host_reduces"] + 3
+
+
+_ROUTE = r"""
+import importlib, os, sys
+sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
+import numpy as np, oracle
+g = importlib.import_module("go-dsp_amd")
+def nrel(a, b):
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+assert g.fft.Devices() == [0, 0], g.fft.Devices()
+s0 = g.fft.MultiStats()
+rng = np.random.default_rng(1)
+x = rng.standard_normal((6, 1024)) + 1j * rng.standard_normal((6, 1024))
+assert max(nrel(a, b) for a, b in zip(g.fft.FFTBatch(x), oracle.fft_rows(x))) < 1e-9
+xs = rng.standard_normal(50000)
+o = g.spectral.PwelchOptions(NFFT=4096, Noverlap=2048)
+p, _ = g.spectral.Pwelch(xs, 1.0, o)
+assert nrel(p, oracle.pwelch(xs, 1.0, 4096, 0, 2048)[0]) < 1e-9
+s1 = g.fft.MultiStats()
+assert s1["batch_calls"] == s0["batch_calls"] + 1, (s0, s1)
+assert s1["pwelch_calls"] == s0["pwelch_calls"] + 1, (s0, s1)
+print("ok")
+"""
+
+
+@pytest.mark.gpu
+def test_host_calls_route_over_device_set():
+    """gdsp_fft_batch / gdsp_pwelch split a call of >= GDSP_MULTI_MIN_BYTES
+    over a configured device set (GDSP_DEVICES; here device 0 twice, with the
+    threshold lowered to 1 byte in a subprocess), counted by gdsp_multi_stats,
+    with the same results as the reference restatement."""
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, REPO=repo, GDSP_DEVICES="0,0", GDSP_MULTI_MIN_BYTES="1")
+    r = subprocess.run(["python", "-c", _ROUTE], capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr[-3000:]
+
+
+@pytest.mark.gpu
+def test_host_calls_stay_on_current_device_by_default(gdsp, oracle):
+    """Unconfigured, a large host call (>= 64 MiB) is not split: the set is
+    the caller's current device (no fan-out onto other ranks' GPUs)."""
     n, batch = 1024, 8192  # 128 MiB in
     x = oracle.fill_uniform(2 * n * batch, 7).view(np.complex128).reshape(batch, n)
+    s0 = gdsp.fft.MultiStats()
     y = gdsp.fft.FFTBatch(x)
+    assert gdsp.fft.MultiStats()["batch_calls"] == s0["batch_calls"]
     for r in (0, batch - 1):
         assert nrel(y[r], oracle.fft(x[r])) < 1e-12
+
+
+@pytest.mark.gpu
+def test_concurrent_pwelch_multi(gdsp, oracle):
+    """gdsp_pwelch_multi is thread-safe (include/gdsp_fft.h): 8 host threads
+    call PwelchMulti over [0], [0, 0] and [0, 0, 0] and the single-device
+    Pwelch at once, twice each, on different signals; every result equals
+    the reference restatement (spectral/pwelch.go:107-122)."""
+    import threading
+    rng = np.random.default_rng(21)
+    cases = []
+    for k in range(4):
+        n = 200000 + 37 * k
+        xs = np.sin(2 * np.pi * (0.1 + 0.05 * k) * np.arange(n)) + rng.standard_normal(n)
+        nfft, nov = (4096, 2048) if k % 2 == 0 else (1000, 250)
+        cases.append((xs, nfft, nov, oracle.pwelch(xs, 1.5, nfft, 0, nov)[0]))
+    sets = [[0], [0, 0], [0, 0, 0], None]
+    errs, fails = [], []
+
+    def work(t):
+        try:
+            for rep in range(2):
+                xs, nfft, nov, ref = cases[(t + rep) % len(cases)]
+                o = gdsp.spectral.PwelchOptions(NFFT=nfft, Noverlap=nov)
+                devs = sets[t % len(sets)]
+                if devs is None:
+                    p, _ = gdsp.spectral.Pwelch(xs, 1.5, o)
+                else:
+                    p, _ = gdsp.spectral.PwelchMulti(xs, 1.5, o, devices=devs)
+                errs.append(nrel(p, ref))
+        except Exception as e:  # noqa: BLE001
+            fails.append(repr(e))
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not fails, fails
+    assert len(errs) == 16 and max(errs) < 1e-9, max(errs)
 
 
 def _free_port() -> int:
