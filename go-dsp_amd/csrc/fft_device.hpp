@@ -49,6 +49,35 @@ __device__ __forceinline__ void st_nt(cd *p, cd v) {
   __builtin_nontemporal_store(v.y, &p->y);
 }
 
+// Bounds-checked buffer access to one wave-uniform region [base, base +
+// bytes): loads past the end return 0 and stores past it are dropped by the
+// hardware, so a row of n elements needs no per-element test or branch (and
+// the address is a 32-bit lane offset, not 64-bit arithmetic per element).
+// The descriptor must be built from wave-uniform values only.
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void *base, int64_t bytes) {
+  const int nb = bytes <= 0 ? 0 : (bytes >= 0x7fffffff ? 0x7fffffff : (int)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, nb, 0x00020000);
+}
+__device__ __forceinline__ cd buf_ld(rsrc_t r, uint32_t off) {
+  const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  cd v;
+  __builtin_memcpy(&v, &q, sizeof(cd));
+  return v;
+}
+__device__ __forceinline__ double buf_ld1(rsrc_t r, uint32_t off) {
+  const auto q = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+  double v;
+  __builtin_memcpy(&v, &q, sizeof(double));
+  return v;
+}
+// nontemporal store (aux bit 1: nt)
+__device__ __forceinline__ void buf_st_nt(rsrc_t r, uint32_t off, cd v) {
+  decltype(__builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 0)) q;
+  __builtin_memcpy(&q, &v, sizeof(cd));
+  __builtin_amdgcn_raw_buffer_store_b128(q, r, off, 0, 2);
+}
+
 // cos/sin(pi/8) and sqrt(2)/2 to double precision
 #define GDSP_C8 0.92387953251128675613
 #define GDSP_S8 0.38268343236508977173
@@ -453,8 +482,25 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
   // t + 272 k
   constexpr bool L2 = LAYOUT == 2 && ILV == 0 && E == 16 && T == 256 && B == 1 &&
                       (NS == 1 || NS * R == 256);
+  // LAYOUT 1 (LINEAR, slot i + i / E) where it is a per-thread base plus a
+  // compile-time offset: a first exchange of one butterfly per thread
+  // (i = E t + r), or NS a multiple of E (i / E splits exactly)
+  constexpr bool LIN = LAYOUT == 1 && ILV == 0 && T >= 32 && E >= 16 && T % E == 0 &&
+                       ((NS == 1 && B == 1) || NS % E == 0);
   int dst[E];
-  if constexpr (L2 && NS == 1) {
+  if constexpr (LIN && NS == 1) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) dst[r] = t * (E + 1) + r;
+  } else if constexpr (LIN) {
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const int j = t + b * T;
+      const int a = (j / NS) * (NS * R) + (j & (NS - 1));
+      const int base = a + (j / NS) * (NS * R / E) + (j & (NS - 1)) / E;
+#pragma unroll
+      for (int r = 0; r < R; ++r) dst[b + r * B] = base + r * (NS + NS / E);
+    }
+  } else if constexpr (L2 && NS == 1) {
     const int m = t & 15;
 #pragma unroll
     for (int r = 0; r < R; ++r) dst[r] = 16 * t + (r ^ m);
@@ -474,7 +520,10 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
   }
   // reads of element t + k T: rbase + k rstep
   int rbase = 0, rstep = 0;
-  if constexpr (L2 && NS == 1) {
+  if constexpr (LIN) {
+    rbase = t + t / E;
+    rstep = T + T / E;
+  } else if constexpr (L2 && NS == 1) {
     rbase = t ^ ((t >> 4) & 15);
     rstep = 256;
   } else if constexpr (L2) {
@@ -482,7 +531,7 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
     rstep = 272;
   }
   auto src = [&](int k) -> int {
-    if constexpr (L2) return rbase + k * rstep;
+    if constexpr (L2 || LIN) return rbase + k * rstep;
     else return xoff<ILV, E, (T >= 32), (T >= 32 ? LAYOUT : 0), NS>(t + k * T);
   };
   if (!first) __syncthreads();

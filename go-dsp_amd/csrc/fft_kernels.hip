@@ -179,6 +179,35 @@ struct ChirpOutEpi {
   }
 };
 
+// The same two epilogues for one transform per workgroup, through
+// bounds-checked buffer descriptors (row, chirp, bhat): no per-element test,
+// branch or 64-bit address (loads past n read 0, stores past n are dropped).
+template <int T>
+struct BhatBufEpi {
+  rsrc_t m;      // bhat (M values)
+  uint32_t off;  // the lane's byte offset, t * 16
+  static constexpr bool on = true;
+  __device__ static constexpr bool want(int) { return true; }
+  __device__ cd load(int k) const { return buf_ld(m, off + (uint32_t)(k * T * 16)); }
+  template <int E>
+  __device__ void apply(cd (&v)[E], int k, cd u, cd f) const { v[k] = conjg(cmul(u, f)); }
+};
+template <int T, int KH, bool INV>
+struct ChirpOutBufEpi {
+  rsrc_t chirp, dst;  // n values each
+  uint32_t off;
+  double scale;
+  static constexpr bool on = true;
+  __device__ static constexpr bool want(int k) { return k < KH; }
+  __device__ cd load(int k) const { return buf_ld(chirp, off + (uint32_t)(k * T * 16)); }
+  template <int E>
+  __device__ void apply(cd (&)[E], int k, cd u, cd f) const {
+    cd y = cmul(conjg(u), f);
+    if constexpr (INV) y = {y.x * scale, -y.y * scale};
+    buf_st_nt(dst, off + (uint32_t)(k * T * 16), y);
+  }
+};
+
 // Which chirp-z steps ride in an FFT's last pass (EPI): 2 both the bhat step
 // and the output postmultiply, 1 the bhat step only, 0 neither. Chosen per M
 // by occupancy and measurement (forced chirp-z, ms per 2^27 samples, 2 runs
@@ -298,6 +327,50 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
     bhat += (int64_t)part * G::N;
   }
   cd v[G::E];
+  constexpr int EPI = blu_epi_mode(LOG2M, LOG2E);
+  if constexpr (G::TPW == 1 && !PARTS && EPI == 2) {
+    // one transform per workgroup: the row, its successor (touch-ahead), the
+    // chirp and bhat through wave-uniform buffer descriptors, every load
+    // issued before the first use
+    const int64_t gu = gb;
+    const uint32_t off = (uint32_t)t * 16u;
+    const int64_t rowb = n * 16;
+    const rsrc_t rin = make_rsrc(in + gu * n, rowb);
+    const rsrc_t rch = make_rsrc(chirp, rowb);
+    const int64_t gp = gu + (LOG2M == 14 ? GDSP_BLU_PF14 : GDSP_BLU_PF);
+    const rsrc_t rpf = make_rsrc(in + (gp < batch ? gp : gu) * n, gp < batch ? rowb : 0);
+    constexpr int SH = GDSP_BLU_PF_SHIFT, NPF = (G::E * 8 >> SH) > 0 ? (G::E * 8 >> SH) : 1;
+    double pf[NPF];
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) pf[k] = buf_ld1(rpf, ((uint32_t)t + (uint32_t)(k * G::T)) << SH);
+    cd xv[KIN], cv[KIN];
+#pragma unroll
+    for (int k = 0; k < KIN; ++k) {
+      xv[k] = buf_ld(rin, off + (uint32_t)(k * G::T * 16));
+      cv[k] = buf_ld(rch, off + (uint32_t)(k * G::T * 16));
+    }
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) asm volatile("" ::"v"(pf[k]));
+#pragma unroll
+    for (int k = 0; k < G::E; ++k) {
+      if (k < KIN) {
+        cd x = xv[k];
+        if constexpr (INV) x.y = -x.y;
+        v[k] = cmul(x, cv[k]);
+      } else {
+        v[k] = {0.0, 0.0};
+      }
+    }
+    const BhatBufEpi<G::T> be{make_rsrc(bhat, (int64_t)G::N * 16), off};
+    fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, HALF, BhatBufEpi<G::T>,
+             blu_prew(LOG2M)>(v, t, twm, lre, lim, true, be);
+    const ChirpOutBufEpi<G::T, KH, INV> oe{make_rsrc(opaque_ptr(chirp), rowb),
+                                           make_rsrc(out + gu * n, rowb), (uint32_t)opaque_int(t) * 16u,
+                                           scale};
+    fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, false,
+             ChirpOutBufEpi<G::T, KH, INV>, blu_prew(LOG2M)>(v, t, twm, lre, lim, false, oe);
+    return;
+  }
   const cd *src = in + g * n;
 #if GDSP_BLU_PF > 0
   // touch every 128-B line of the row the block GDSP_BLU_PF places later on
@@ -341,7 +414,6 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
 #pragma unroll
   for (int k = 0; k < NPF; ++k) asm volatile("" ::"v"(pf[k]));
 #endif
-  constexpr int EPI = blu_epi_mode(LOG2M, LOG2E);
   if constexpr (EPI >= 1) {
     // x bhat, conj: fused into FFT 1's last pass, each butterfly's factors
     // loaded ahead of its arithmetic
