@@ -78,6 +78,8 @@ SIGNATURES = {
     "gdsp_fill_uniform_device": (_I, [_P, _I64, _U64, _U64, _P]),
     "gdsp_set_devices": (_I, [ctypes.POINTER(_I), _I]),
     "gdsp_get_devices": (_I, [ctypes.POINTER(_I), _I]),
+    "gdsp_set_algorithm": (_I, [ctypes.c_uint]),
+    "gdsp_get_algorithm": (ctypes.c_uint, []),
     "gdsp_multi_stats": (_I, [ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64),
                               ctypes.POINTER(_I64)]),
     "gdsp_fft_batch_multi": (_I, [_P, _P, _I64, _I64, _I, ctypes.POINTER(_I), _I]),

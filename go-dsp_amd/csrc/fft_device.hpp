@@ -238,12 +238,9 @@ __device__ __forceinline__ void dft_half_in(cd (&a)[R]) {
   }
 }
 
-// XOR-swizzled exchange slots (lds_off); -DGDSP_LDS_PAD16 restores the padded layout
-#ifndef GDSP_LDS_PAD16
+// XOR-swizzled exchange slots (lds_off; the padded layout i + i/16 it
+// replaced left 33 % of the chirp-z kernel's LDS cycles bank-conflicted)
 constexpr bool kLdsXor = true;
-#else
-constexpr bool kLdsXor = false;
-#endif
 __host__ __device__ constexpr int clog2(int v) { return v <= 1 ? 0 : 1 + clog2(v / 2); }
 
 // ---------------------------------------------------------------------------
@@ -315,46 +312,19 @@ __device__ __forceinline__ cd pass_base(const cd *__restrict__ tw, int j) {
 // transforms of one geometry, every pass of radix R with one butterfly per
 // thread, j = t): pass p's base W_{NS R}^(t % NS) is the same for every
 // transform, so it is read once per kernel instead of from a table per
-// transform; with RH = R - 1, pass 1's powers base^1..base^(R-1) are held too
-// (its power chain then runs once per kernel). Passed as fft_regs' TWP.
-template <int NP, int RH = 0>
+// transform. Passed as fft_regs' TWP.
+template <int NP>
 struct RegTw {
-  static constexpr int HELD = RH;
-  cd base[NP];          // base[p], p >= 1
-  cd pw[RH > 0 ? RH : 1];  // pass 1: base[1]^(r+1), r < RH
+  cd base[NP];  // base[p], p >= 1
 };
 template <class T>
 struct is_regtw {
   static constexpr bool v = false;
-  static constexpr int held = 0;
 };
-template <int NP, int RH>
-struct is_regtw<RegTw<NP, RH>> {
+template <int NP>
+struct is_regtw<RegTw<NP>> {
   static constexpr bool v = true;
-  static constexpr int held = RH;
 };
-
-// the powers w^1..w^(R-1) as pass_compute forms them (two interleaved
-// recurrences, odd and even exponents): pw[r-1] = w^r
-template <int R>
-__device__ __forceinline__ void twiddle_powers(cd w, cd (&pw)[R - 1]) {
-  pw[0] = w;
-  if constexpr (R > 2) {
-    const cd w2 = cmul(w, w);
-    cd wo = w, we = w2;
-    pw[1] = w2;
-#pragma unroll
-    for (int r = 3; r < R; ++r) {
-      if (r & 1) {
-        wo = cmul(wo, w2);
-        pw[r - 1] = wo;
-      } else {
-        we = cmul(we, w2);
-        pw[r - 1] = we;
-      }
-    }
-  }
-}
 
 __device__ __forceinline__ cd opaque_cd(cd w) {
   asm volatile("" : "+v"(w.x), "+v"(w.y));
@@ -363,7 +333,7 @@ __device__ __forceinline__ cd opaque_cd(cd w) {
 
 // WPRE: the butterflies' twiddle bases come in wpre[b] (loaded by the caller
 // a pass ahead: fft_regs PREW) instead of being read here
-// PASS: this pass's index (selects a RegTw's base / held powers)
+// PASS: this pass's index (selects a RegTw's base)
 template <int N, int E, int T, int R, int NS, bool HALF_IN = false, class EPI = NoEpi,
           bool WPRE = false, int PASS = 0, class TWP = const cd *>
 __device__ __forceinline__ void pass_compute(cd (&v)[E], int t, TWP tw,
@@ -381,11 +351,7 @@ __device__ __forceinline__ void pass_compute(cd (&v)[E], int t, TWP tw,
     cd u[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) u[r] = v[b + r * B];
-    if constexpr (NS > 1 && PASS == 1 && is_regtw<TWP>::held == R - 1) {
-      static_assert(B == 1, "register twiddles need one butterfly per thread");
-#pragma unroll
-      for (int r = 1; r < R; ++r) u[r] = cmul(u[r], tw.pw[r - 1]);
-    } else if constexpr (NS > 1) {
+    if constexpr (NS > 1) {
       // W_{NS*R}^{(j%NS)*r}: one table read, powers by two interleaved
       // recurrences (odd and even exponents) to keep the product depth ~R/2
       cd w;

@@ -218,31 +218,16 @@ struct ChirpOutBufEpi {
 // / 1.72 / 1.74; 2^12 (1201, 2039; both: 2 waves per SIMD, else 3) 2.65 /
 // 2.23 / 2.24-2.27 and 1.83 / 1.76 / 1.77; 2^13 (3000, 4093) 2.16-2.18 /
 // 2.17-2.19 / 2.24 and 1.83 / 1.91 / 1.98; 2^14 (8191) 2.35 / 2.27-2.28 / 2.26.
-// GDSP_BLU_NOEPI / GDSP_BLU_OUT_AFTER force 0 / at most 1 (experiments).
 // Twiddle-base prefetch (fft_regs PREW) for passes with one base per thread;
 // not at M = 2^10, where it costs that kernel a wave per SIMD
-#ifndef GDSP_NO_PREW
 constexpr int kPwPrew = 1;
 __host__ __device__ constexpr int blu_prew(int log2m) { return log2m == 10 ? 0 : 1; }
-#else
-constexpr int kPwPrew = 0;
-__host__ __device__ constexpr int blu_prew(int) { return 0; }
-#endif
 __host__ __device__ constexpr int blu_epi_mode(int log2m, int log2e) {
-#if defined(GDSP_BLU_NOEPI)
-  return 0 * log2m * log2e;
-#else
-  // (the 16-points-per-thread kernels of M = 2^13 / 2^14, GDSP_BLU_E16=1: none;
-  // with both chirpz3000 took 4.86 against 3.40 ms)
-  const int m = (log2m == 5 || log2m == 6 || log2m == 10 || (log2m >= 13 && log2e == 4))   ? 0
-                : (log2m == 12 || log2m == 14) ? 1
-                                               : 2;
-#if defined(GDSP_BLU_OUT_AFTER)
-  return m < 1 ? m : 1;
-#else
-  return m;
-#endif
-#endif
+  // (the 16-points-per-thread kernels of M = 2^13 / 2^14: none; with both
+  // chirpz3000 took 4.86 against 3.40 ms)
+  return (log2m == 5 || log2m == 6 || log2m == 10 || (log2m >= 13 && log2e == 4)) ? 0
+         : (log2m == 12 || log2m == 14)                                          ? 1
+                                                                                 : 2;
 }
 
 // Fused Bluestein (chirp-z) for non-power-of-2 n with M = NextPowerOf2(2n-1):
@@ -260,23 +245,12 @@ __host__ __device__ constexpr int blu_epi_mode(int log2m, int log2e) {
 // Rows ahead a chirp-z block touches for its successor on the XCD (0: off).
 // chirpz3000 2.95-3.05 -> 2.80-2.89 ms at 8-32, 2.84-2.85 at 48, 2.94-3.03 at
 // 64-128 (scripts/dev/blu_pf_ab.sh); blocks of several transforms (M <= 2048)
-// touch the same slot's row GDSP_BLU_PF blocks on: primes 13..1021 10-22 %
+// touch the same slot's row kBluPf blocks on: primes 13..1021 10-22 %
 // faster (scripts/dev/blu_pfall_ab.sh)
-#ifndef GDSP_BLU_PF
-#define GDSP_BLU_PF 16
-#endif
-#ifndef GDSP_BLU_PF14  // M = 16384: one block per CU
-#define GDSP_BLU_PF14 4  // 2-4 % faster than 8 or 16 (scripts/dev/blu_pf14_ab.sh)
-#endif
-#ifndef GDSP_BLU_PF_PARTS
-#define GDSP_BLU_PF_PARTS 2
-#endif
-#ifndef GDSP_BLU_PARTS_YMAJOR
-#define GDSP_BLU_PARTS_YMAJOR 0
-#endif
-#ifndef GDSP_BLU_PF_SHIFT
-#define GDSP_BLU_PF_SHIFT 7  // touch granularity: one load per 2^SHIFT bytes
-#endif
+constexpr int kBluPf = 16;
+constexpr int kBluPf14 = 4;     // M = 16384, one block per CU: 2-4 % faster than 8 or 16
+constexpr int kBluPfParts = 2;  // PARTS: the row's part-0 block touches 2 rows on
+constexpr int kBluPfShift = 7;  // touch granularity: one load per 2^7 bytes (a line)
 template <int LOG2M, bool INV, bool SPLIT, int LOG2E = 4, bool PARTS = false>
 __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
     const cd *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
@@ -289,17 +263,13 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
   const int t = lt & (G::T - 1);
   // PARTS: the parts of a row are adjacent block indices (after the XCD
   // remap, so on one XCD at about the same time), and its 2nd..nth reads of
-  // the row hit L2 instead of HBM (GDSP_BLU_PARTS_YMAJOR=1: part = blockIdx.y)
+  // the row hit L2 instead of HBM (the part-major grid was 3-9 % slower)
   int64_t gb = xcd_remap(blockIdx.x, gridDim.x);
   int part = 0;
   if constexpr (PARTS) {
-#if GDSP_BLU_PARTS_YMAJOR
-    part = (int)blockIdx.y;
-#else
     const int64_t q = gb / nparts;
     part = (int)(gb - q * nparts);
     gb = q;
-#endif
   }
   const int64_t g = gb * G::TPW + slot;
   const bool valid = g < batch;
@@ -307,13 +277,8 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
   double *lim = SPLIT ? lre : lds + G::LDS_DOUBLES + slot * G::STRIDE;
   // n <= M/2 (M is a power of 2 >= 2n - 1): registers k >= E/2 hold no input
   // and no output, so the first pass of FFT 1 and the last of FFT 2 are pruned
-#ifndef GDSP_BLU_NOPRUNE
   constexpr int KH = G::E > 1 ? G::E / 2 : G::E;
   constexpr bool HALF = G::E >= 4 && !PARTS;
-#else
-  constexpr int KH = G::E;
-  constexpr bool HALF = false;
-#endif
   constexpr int KIN = PARTS ? G::E : KH;
   // this block's outputs: X[k0 + k], k < nout
   int64_t nout = n;
@@ -337,9 +302,9 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
     const int64_t rowb = n * 16;
     const rsrc_t rin = make_rsrc(in + gu * n, rowb);
     const rsrc_t rch = make_rsrc(chirp, rowb);
-    const int64_t gp = gu + (LOG2M == 14 ? GDSP_BLU_PF14 : GDSP_BLU_PF);
+    const int64_t gp = gu + (LOG2M == 14 ? kBluPf14 : kBluPf);
     const rsrc_t rpf = make_rsrc(in + (gp < batch ? gp : gu) * n, gp < batch ? rowb : 0);
-    constexpr int SH = GDSP_BLU_PF_SHIFT, NPF = (G::E * 8 >> SH) > 0 ? (G::E * 8 >> SH) : 1;
+    constexpr int SH = kBluPfShift, NPF = (G::E * 8 >> SH) > 0 ? (G::E * 8 >> SH) : 1;
     double pf[NPF];
 #pragma unroll
     for (int k = 0; k < NPF; ++k) pf[k] = buf_ld1(rpf, ((uint32_t)t + (uint32_t)(k * G::T)) << SH);
@@ -372,22 +337,21 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
     return;
   }
   const cd *src = in + g * n;
-#if GDSP_BLU_PF > 0
-  // touch every 128-B line of the row the block GDSP_BLU_PF places later on
+  // touch every 128-B line of the row the block kBluPf places later on
   // this XCD will take (xcd_remap keeps an XCD's rows contiguous), so that
   // block's row loads hit L2 / MALL instead of waiting on HBM
   // (n <= M/2 = T*E/2, so a row is at most T*E*16/2^SH pieces of 2^SH bytes:
   // E*8/2^SH per thread of the transform's T)
   // (PARTS: n <= M, twice the pieces; the row's part-0 block touches the row
-  // GDSP_BLU_PF_PARTS rows on)
-  constexpr int SH = GDSP_BLU_PF_SHIFT,
+  // kBluPfParts rows on)
+  constexpr int SH = kBluPfShift,
                 NPF = ((PARTS ? 2 : 1) * G::E * 8 >> SH) > 0 ? ((PARTS ? 2 : 1) * G::E * 8 >> SH) : 1;
   double pf[NPF];
 #pragma unroll
   for (int k = 0; k < NPF; ++k) pf[k] = 0.0;
-  if constexpr (!PARTS || GDSP_BLU_PF_PARTS > 0) {
-    const int64_t gp = g + (PARTS ? (int64_t)GDSP_BLU_PF_PARTS
-                                  : (int64_t)(LOG2M == 14 ? GDSP_BLU_PF14 : GDSP_BLU_PF) * G::TPW);
+  {
+    const int64_t gp = g + (PARTS ? (int64_t)kBluPfParts
+                                  : (int64_t)(LOG2M == 14 ? kBluPf14 : kBluPf) * G::TPW);
     if (valid && gp < batch && part == 0) {
       const char *prow = reinterpret_cast<const char *>(in + gp * n);
       const int pieces = (int)((n * 16 + (1 << SH) - 1) >> SH);
@@ -397,7 +361,6 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
           pf[k] = *reinterpret_cast<const double *>(prow + ((int64_t)(t + k * G::T) << SH));
     }
   }
-#endif
 #pragma unroll
   for (int k = 0; k < G::E; ++k) {
     const int idx = t + k * G::T;
@@ -408,12 +371,10 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
       v[k] = cmul(x, chirp[idx]);
     }
   }
-#if GDSP_BLU_PF > 0
   // the prefetches were issued before the row loads the premultiply waited
   // for (loads return in order), so consuming them here costs no wait
 #pragma unroll
   for (int k = 0; k < NPF; ++k) asm volatile("" ::"v"(pf[k]));
-#endif
   if constexpr (EPI >= 1) {
     // x bhat, conj: fused into FFT 1's last pass, each butterfly's factors
     // loaded ahead of its arithmetic
@@ -566,22 +527,15 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_kernel(
 // a complex (two-buffer) exchange 3.45 ms.
 // Exchange slot layout of the Pwelch kernels: XOR-swizzled (conflict-free);
 // the linear padded layout (fewer address instructions, 2-way conflicted
-// reads at E = 16) measured 3.08-3.09 against 3.03-3.05 ms (GDSP_PW_LINEAR).
-#ifdef GDSP_PW_LINEAR
-constexpr bool kPwLinear = true;
-#else
-constexpr bool kPwLinear = false;
-#endif
-// TWM: where the pass twiddles come from. 0 the global table (L1/L2) per
-// pair. 1 the bases T_N[0 .. N/R_last) in an LDS table, and the next pair's
-// samples prefetched while this pair's FFT runs (the only global loads left
-// in the loop are the samples, so vmcnt covers only them). 2 as 1, but each
-// pass's base (one butterfly per thread: W_{NS R}^(t % NS), the same for
-// every pair) read once per kernel into registers. 3 as 2, with pass 1's
-// powers held in registers too (its power chain runs once per kernel). 4 as
-// 3 without the next-pair sample prefetch (the registers it held).
+// reads at E = 16) measured 3.08-3.09 against 3.03-3.05 ms; the row kernel
+// below takes XOR for its first exchange and a block-padded layout for the
+// second (LAYOUT 2, fft_device.hpp).
+constexpr int kPwLinear = 0;
+// PF: the pass twiddle bases (T_N[0 .. N/R_last)) live in LDS, so the only
+// global loads in the loop are the samples, and the next pair's samples are
+// prefetched while this pair's FFT runs (vmcnt then covers only them)
 template <int LOG2F, int WMODE = 2, int MINW = 1, int LOG2E = 4, bool SPLIT = true,
-          int TWM = 0>
+          bool PF = false>
 __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_kernel(
     const double *__restrict__ x, int64_t seg_begin, int64_t seg_end, int64_t pairs_per_worker,
     const double *__restrict__ win, const cd *__restrict__ tw, double *__restrict__ partial) {
@@ -589,11 +543,7 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_ker
   constexpr int E = G::E, H = E / 2;
   constexpr int64_t STRIDE = G::N / 2;
   constexpr int XD = (SPLIT ? 1 : 2) * G::LDS_DOUBLES;  // exchange buffer(s)
-  constexpr bool PF = TWM >= 1 && TWM <= 3;
-  constexpr bool REGTW = TWM >= 2;
-  static_assert(!REGTW || (G::E == G::EMAX && G::NPE == G::NPASS),
-                "register twiddles need radix-E passes with one butterfly per thread");
-  constexpr int TWN = TWM == 1 ? G::N / G::radix(G::NPASS - 1) : 0;
+  constexpr int TWN = PF ? G::N / G::radix(G::NPASS - 1) : 0;
   __shared__ double lds[XD + (WMODE == 2 ? G::N : 0) + 2 * TWN];
   const int lt = threadIdx.x;
   // one worker per workgroup (TPW = 1, F >= 4096): the worker index, its
@@ -615,21 +565,10 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_ker
     for (int i = lt; i < G::N; i += G::WG) wl[i] = win[i];
   }
   cd *twl = reinterpret_cast<cd *>(lds + XD + (WMODE == 2 ? G::N : 0));
-  if constexpr (TWM == 1) {
+  if constexpr (PF) {
     for (int i = lt; i < TWN; i += G::WG) twl[i] = tw[i];
   }
-  using RT = RegTw<G::NPASS, TWM >= 3 ? G::EMAX - 1 : 0>;
-  RT rtw;
-  if constexpr (REGTW) {
-#pragma unroll
-    for (int p = 1; p < G::NPASS; ++p) rtw.base[p] = {0.0, 0.0};
-    if constexpr (G::NPASS > 1) rtw.base[1] = pass_base<G::N, G::EMAX, G::ns(1)>(tw, t);
-    if constexpr (G::NPASS > 2) rtw.base[2] = pass_base<G::N, G::EMAX, G::ns(2)>(tw, t);
-    if constexpr (G::NPASS > 3) rtw.base[3] = pass_base<G::N, G::EMAX, G::ns(3)>(tw, t);
-    static_assert(G::NPASS <= 4, "bases of up to 4 passes");
-    if constexpr (TWM >= 3 && G::NPASS > 1) twiddle_powers<G::EMAX>(rtw.base[1], rtw.pw);
-  }
-  if constexpr (WMODE == 2 || TWM == 1) __syncthreads();
+  if constexpr (WMODE == 2 || PF) __syncthreads();
   double acc[E];
 #pragma unroll
   for (int k = 0; k < E; ++k) acc[k] = 0.0;
@@ -710,15 +649,7 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_ker
     }
 #pragma unroll
     for (int k = 0; k < H; ++k) carry[k] = c2[k];
-    if constexpr (REGTW) {
-      // the bases are re-laundered every pair so the compiler does not hoist
-      // the per-pass power chains out of the loop (registers)
-      RT rl = rtw;
-#pragma unroll
-      for (int p = 1; p < G::NPASS; ++p) rl.base[p] = opaque_cd(rl.base[p]);
-      fft_regs<LOG2F, SPLIT, 2, LOG2E, 0, 0, RT, kPwLinear, false, NoEpi, 0>(
-          v, opaque_int(t), rl, lre, lim, it == 0);
-    } else if constexpr (PF)
+    if constexpr (PF)
       fft_regs<LOG2F, SPLIT, 2, LOG2E, 0, 0, const cd *, kPwLinear, false, NoEpi, kPwPrew>(
           v, opaque_int(t), (const cd *)twl, lre, lim, it == 0);
     else
@@ -749,8 +680,14 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG), MINW) void pwelch_half_ker
 //  - the next pair's samples are loaded into the registers this pair's
 //    samples just left (after the window multiply), so they are in flight
 //    during the FFT with no double buffer to copy between;
-//  - REGTW: each pass's twiddle base (the same for every pair) is read once
-//    per kernel into registers (no LDS table, no bank conflicts on it).
+//  - each pass's twiddle base (the same for every pair) is read once per
+//    kernel into registers (no LDS table, no bank conflicts on it); pass 1's
+//    powers from an LDS table instead of each pair's chain measured slower
+//    (2.99-3.01 against 2.86-2.87 ms: LDS, not the vector unit, is the
+//    scarcer resource here);
+//  - LAYOUT 2 exchange slots (fft_device.hpp): every LDS address a per-thread
+//    base plus a compile-time offset (2.81-2.84 against 2.94-2.97 ms with
+//    XOR-swizzled slots throughout).
 template <int LOG2F, int LOG2E = 4, bool REGTW = true, int LAYOUT = 2>
 __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_row_kernel(
     const double *__restrict__ x, int64_t seg_begin, int64_t seg_end, int64_t pairs_per_worker,
@@ -767,7 +704,7 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_row_kernel(
   const int t = threadIdx.x;
   const uint32_t lane = (uint32_t)t;
   for (int i = t; i < G::N; i += G::WG) wl[i] = win[i];
-  using RT = RegTw<G::NPASS, 0>;
+  using RT = RegTw<G::NPASS>;
   RT rtw;
 #pragma unroll
   for (int p = 0; p < G::NPASS; ++p) rtw.base[p] = {1.0, 0.0};
@@ -1161,7 +1098,7 @@ static hipError_t launch_lds_t(const void *in, cd *out, int64_t batch, const cd 
   // samples for 16 (1024 threads, four passes), alternating runs
   // (GDSP_LDS14_E16=1 to compare)
   if constexpr (LOG2N == 14) {
-    static const bool e32 = getenv("GDSP_LDS14_E16") == nullptr;
+    static const bool e32 = dev_switch("GDSP_LDS14_E16") == nullptr;
     if (e32) {
       using G5 = Geo<LOG2N, 5>;
       const int64_t nb5 = (batch + G5::TPW - 1) / G5::TPW;
@@ -1224,7 +1161,7 @@ static hipError_t launch_blu_t(const cd *in, cd *out, int64_t n, int64_t batch, 
   // 124 VGPRs, 4 waves per SIMD): chirp-z 3000 3.44 against 3.56 ms, primes
   // 4099..8191 (M = 16384) 2-5 % (GDSP_BLU_E16=1 to compare)
   if constexpr (LOG2M == 13 || LOG2M == 14) {
-    static const bool e32 = getenv("GDSP_BLU_E16") == nullptr;
+    static const bool e32 = dev_switch("GDSP_BLU_E16") == nullptr;
     if (e32) {
       using G5 = Geo<LOG2M, 5>;
       const int64_t nb5 = (batch + G5::TPW - 1) / G5::TPW;
@@ -1252,13 +1189,9 @@ static hipError_t launch_blu_parts_t(bool inv, const cd *in, cd *out, int64_t n,
   if (parts < 1 || parts > 65535 || kpart < 1 || kpart > G::N / 2 || n + kpart - 1 > G::N ||
       kpart * parts < n)
     return hipErrorInvalidValue;
-#if GDSP_BLU_PARTS_YMAJOR
-  const dim3 grid((unsigned)((batch + G::TPW - 1) / G::TPW), (unsigned)parts);
-#else
   const int64_t nb = (batch + G::TPW - 1) / G::TPW * parts;
   if (nb > 0x7fffffff) return hipErrorInvalidValue;
   const dim3 grid((unsigned)nb);
-#endif
   if (inv)
     hipLaunchKernelGGL((bluestein_kernel<LOG2M, true, true, 5, true>), grid, dim3(G::WG), 0, s,
                        in, out, n, batch, twm, chirp, bhat, scale, kpart, parts);
@@ -1351,14 +1284,14 @@ static hipError_t launch_pw_t(const double *x, int64_t nfft, int64_t stride, int
 }
 
 template <int LOG2F, int WMODE = 2, int MINW = 1, int LOG2E = 4, bool SPLIT = true,
-          int TWM = 0>
+          bool PF = false>
 static hipError_t launch_pwh_t(const double *x, int64_t seg_begin, int64_t seg_end, int64_t ppw,
                                int64_t nworkers, const double *win, const cd *tw, double *partial,
                                hipStream_t s) {
   using G = Geo<LOG2F, LOG2E>;
   if (G::TPW != Geo<LOG2F>::TPW) return hipErrorInvalidValue;  // workers per block
   const int64_t nblk = (nworkers + G::TPW - 1) / G::TPW;
-  hipLaunchKernelGGL((pwelch_half_kernel<LOG2F, WMODE, MINW, LOG2E, SPLIT, TWM>), dim3((unsigned)nblk), dim3(G::WG), 0, s,
+  hipLaunchKernelGGL((pwelch_half_kernel<LOG2F, WMODE, MINW, LOG2E, SPLIT, PF>), dim3((unsigned)nblk), dim3(G::WG), 0, s,
                      x, seg_begin, seg_end, ppw, win, tw, partial);
   return hipGetLastError();
 }
@@ -1373,30 +1306,19 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
     // F = 4096 (the BASELINE configuration): twiddle bases in LDS and the
     // next pair prefetched (3.16 -> 3.11 ms; 244 VGPRs, still 2 waves/SIMD)
     case 12: {
-      // the wavefront-shuffle variant (pwelch_shfl.hip): one exchange in LDS,
-      // the other inside the wave (GDSP_PW_SHFL=0 restores the two-exchange one)
-      static const int shfl = [] {
-        const char *e = getenv("GDSP_PW_SHFL");
-        return e ? atoi(e) : 0;
-      }();
-      if (shfl)
+#ifdef GDSP_DEV_BUILD
+      // measured alternatives: the wavefront-shuffle variant (pwelch_shfl.hip,
+      // GDSP_PW_SHFL=1) and round 2's pwelch_half_kernel (GDSP_PW_HALF=1)
+      if (const char *e = dev_switch("GDSP_PW_SHFL"); e && e[0] == '1')
         return launch_pwelch4096_shfl(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
-#ifndef GDSP_PW_TWM
-#define GDSP_PW_TWM 1
+      if (const char *e = dev_switch("GDSP_PW_HALF"); e && e[0] == '1')
+        return launch_pwh_t<12, 2, 1, 4, true, true>(x, seg_begin, seg_end, ppw, nworkers, win, tw,
+                                                     partial, s);
 #endif
-#ifndef GDSP_PW_ROW
-#define GDSP_PW_ROW 1
-#endif
-#ifndef GDSP_PW_LAYOUT
-#define GDSP_PW_LAYOUT 2
-#endif
-      if (GDSP_PW_ROW) {
-        hipLaunchKernelGGL((pwelch_row_kernel<12, 4, GDSP_PW_ROW == 1, GDSP_PW_LAYOUT>), dim3((unsigned)nworkers),
-                           dim3(Geo<12>::WG), 0, s, x, seg_begin, seg_end, ppw, win, tw, partial);
-        return hipGetLastError();
-      }
-      return launch_pwh_t<12, 2, 1, 4, true, GDSP_PW_TWM>(x, seg_begin, seg_end, ppw, nworkers,
-                                                          win, tw, partial, s);
+      // the row kernel: 2.81-2.84 against 3.13-3.14 ms for pwelch_half_kernel
+      hipLaunchKernelGGL((pwelch_row_kernel<12>), dim3((unsigned)nworkers), dim3(Geo<12>::WG), 0,
+                         s, x, seg_begin, seg_end, ppw, win, tw, partial);
+      return hipGetLastError();
     }
     GDSP_PWH(13)
 #undef GDSP_PWH
@@ -1405,7 +1327,7 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
     case 14: {
       // 32 points per thread (512 threads): 2.25-2.27 against 2.37-2.40 ms at
       // 2^28 samples for 16 (1024 threads); both spill (GDSP_PWH14_E16=1)
-      static const bool e32 = getenv("GDSP_PWH14_E16") == nullptr;
+      static const bool e32 = dev_switch("GDSP_PWH14_E16") == nullptr;
       if (e32)
         return launch_pwh_t<14, 1, 1, 5>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial,
                                          s);
@@ -1548,7 +1470,7 @@ hipError_t launch_transpose(const cd *in, cd *out, int64_t rows, int64_t cols, h
   // 2^22 elements, where twice the tiles spread better over the CUs (one
   // 2^20 transform: 8.3 against 10.3 us); GDSP_TRANSPOSE=32 (32 x 32) and 64
   // (64 x 64) to compare
-  static const int forced = getenv("GDSP_TRANSPOSE") ? atoi(getenv("GDSP_TRANSPOSE")) : 0;
+  static const int forced = dev_switch("GDSP_TRANSPOSE") ? atoi(dev_switch("GDSP_TRANSPOSE")) : 0;
   const int shape = forced ? forced : (rows * cols * batch < ((int64_t)1 << 22) ? 32 : 0);
   const int tr = shape == 64 ? 64 : 32, tc = shape == 32 ? 32 : 64;
   const int64_t tiles = ((rows + tr - 1) / tr) * ((cols + tc - 1) / tc) * batch;

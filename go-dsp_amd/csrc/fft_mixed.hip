@@ -19,6 +19,7 @@
 // the passes between exchange through LDS (complex128, ds_*_b128). Per-pass
 // twiddles come from a table laid out butterfly-major (long-double accurate,
 // built with the plan), so a butterfly's R-1 factors are one contiguous run.
+#include "gdsp_fft.h"
 #include "mixed_core.hpp"
 #include "mixed_specs.hpp"
 
@@ -368,12 +369,12 @@ hipError_t launch_colradix(int L, bool conj_in, const cd *in, cd *out, int64_t C
 }
 
 // Radix list of the compiled specialisation for n, if there is one
-// (launch_fft_mixed picks the kernel by n and list). GDSP_MIXED_GENERIC=1
+// (launch_fft_mixed picks the kernel by n and list). GDSP_ALGO_GENERIC_MIXED
 // disables them. n = 3000: 1.10 ms per 65536 transforms for 25*15*8 against
 // 1.14-1.18 ms for the other orders of these radices and 1.82 ms for the
 // generic 8*5*5*5*3 kernel; a split (re/im) exchange measured 3-4 % slower.
 bool mixed_fixed_radices(int n, int *rad, int *npass) {
-  if (getenv("GDSP_MIXED_GENERIC")) return false;
+  if (algo_flags() & GDSP_ALGO_GENERIC_MIXED) return false;
   return specs0_find(n, rad, npass) || specs1_find(n, rad, npass) ||
          specs2_find(n, rad, npass) || specs3_find(n, rad, npass);
 }

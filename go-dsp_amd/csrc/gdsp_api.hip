@@ -8,7 +8,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <map>
+#include <tuple>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -22,7 +24,7 @@
 
 using gdsp::cd;
 
-#define GDSP_VERSION "gdspfft 0.2.0 (gfx950)"
+#define GDSP_VERSION "gdspfft 0.3.0 (gfx950)"
 
 namespace {
 
@@ -83,13 +85,19 @@ hipStream_t thread_stream(int dev) {
   return s;
 }
 
+// The one-kernel transform exchanges real and imaginary halves in turn
+// (half the LDS; GDSP_LDS_SPLIT=0 in the development build for two buffers).
 bool lds_split_default() {
   static int v = [] {
-    const char *e = getenv("GDSP_LDS_SPLIT");
+    const char *e = gdsp::dev_switch("GDSP_LDS_SPLIT");
     return (e && e[0] == '0') ? 0 : 1;
   }();
   return v != 0;
 }
+
+std::atomic<unsigned> g_algo{GDSP_ALGO_DEFAULT};
+constexpr unsigned kAlgoAll = GDSP_ALGO_GENERIC_MIXED | GDSP_ALGO_NO_CHIRPZ_PARTS |
+                              GDSP_ALGO_CHIRPZ_POW2 | GDSP_ALGO_CHIRPZ_UNFUSED;
 
 // Scratch device memory: a grow-only buffer per (device, stream, use-site
 // slot), allocated with hipMalloc. Reuse is ordered by the stream itself: a
@@ -334,6 +342,8 @@ struct gdsp_plan {
   // NextPowerOf2(2n-1) = 32768 exceeds one kernel runs as `parts` fused
   // convolutions of M = 16384, each giving kpart outputs; bhat holds parts * M
   int parts = 1;
+  // composed chirp-z without its fused transposes (GDSP_ALGO_CHIRPZ_UNFUSED)
+  bool unfused = false;
   int64_t kpart = 0;
 };
 
@@ -342,8 +352,9 @@ namespace {
 // recursive: building a Bluestein plan runs FFT_M(b), whose four-step path
 // fetches sub-plans from this cache on the same thread
 std::recursive_mutex g_plan_mu;
-std::map<std::pair<int, int64_t>, gdsp_plan *> g_plans;
-std::map<std::pair<int, int64_t>, gdsp_plan *> g_chirpz_plans;  // forced Bluestein
+// keyed by (device, n, algorithm flags the plan was built under)
+std::map<std::tuple<int, int64_t, unsigned>, gdsp_plan *> g_plans;
+std::map<std::tuple<int, int64_t, unsigned>, gdsp_plan *> g_chirpz_plans;  // forced Bluestein
 
 int exec_plan(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
               hipStream_t s);
@@ -471,7 +482,7 @@ int build_mixed(int dev, int64_t n, const std::vector<int> &rad, gdsp_plan *p) {
 // one kernel, else 0 (composed chirp-z). P = 8 (n <= 14563) measured 10.8
 // against 11.5 ms for the composed chirp-z per 2^27 samples, P = 2 4x faster.
 int chirpz_parts(int64_t n) {
-  static const bool off = getenv("GDSP_BLU_NOPARTS") != nullptr;
+  const bool off = (gdsp::algo_flags() & GDSP_ALGO_NO_CHIRPZ_PARTS) != 0;
   const int64_t mk = (int64_t)1 << gdsp::kMaxLdsLog2;
   if (off || next_pow2_ref(2 * n - 1) <= mk) return 0;
   for (int parts = 2; parts <= 8; ++parts)
@@ -560,12 +571,14 @@ bool mixcol_build(int dev, int64_t n, gdsp_plan *p) {
   return false;
 }
 
+#ifdef GDSP_DEV_BUILD
+// ---- measured and rejected chirp-z kernels (development build) ----
 // The wave-resident chirp-z kernel (fft_wave.hip) for 512 < n <= 4096, when
 // GDSP_BLU_WAVE=1. Measured slower than the block-wide bluestein_kernel at
 // every Q (chirp-z 3000: 3.83 against 3.35 ms), so it is opt-in.
 bool wave_chirpz_enabled() {
   static const bool on = [] {
-    const char *e = getenv("GDSP_BLU_WAVE");
+    const char *e = gdsp::dev_switch("GDSP_BLU_WAVE");
     return e && e[0] == '1';
   }();
   return on;
@@ -605,7 +618,7 @@ int build_wave_tables(int dev, gdsp_plan *p) {
 // (bluestein_shfl.hip), when GDSP_BLU_SHFL=1.
 bool shfl_chirpz_enabled() {
   static const bool on = [] {
-    const char *e = getenv("GDSP_BLU_SHFL");
+    const char *e = gdsp::dev_switch("GDSP_BLU_SHFL");
     return e && e[0] == '1';
   }();
   return on;
@@ -623,6 +636,7 @@ int build_shfl_tables(gdsp_plan *p) {
   HIPCHK(hipStreamSynchronize(s));
   return GDSP_OK;
 }
+#endif  // GDSP_DEV_BUILD
 
 int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   p->device = dev;
@@ -697,7 +711,7 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
     // all n outputs, 2n - 1), so P parts of kpart = ceil(n/P) run on the
     // one-kernel M = 16384 wherever n + kpart - 1 <= 16384 with P <= 8
     // (n <= 14563); the composed chirp-z over 32768 moves ~8 HBM passes of M
-    // per transform. GDSP_BLU_NOPARTS=1 keeps the composed path.
+    // per transform. GDSP_ALGO_NO_CHIRPZ_PARTS keeps the composed path.
     if (const int parts = chirpz_parts(n)) {
       p->m = (int64_t)1 << gdsp::kMaxLdsLog2;
       p->log2m = gdsp::kMaxLdsLog2;
@@ -706,7 +720,9 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
       p->kpart = (n + parts - 1) / parts;
     }
   }
-  if (p->kind == KIND_BLUESTEIN_COMPOSED && !chirpz && !getenv("GDSP_CHIRPZ_POW2")) {
+  p->unfused = (gdsp::algo_flags() & GDSP_ALGO_CHIRPZ_UNFUSED) != 0;
+  if (p->kind == KIND_BLUESTEIN_COMPOSED && !chirpz &&
+      !(gdsp::algo_flags() & GDSP_ALGO_CHIRPZ_POW2)) {
     // The composed chirp-z is HBM-bound, so its cost follows M: take the
     // smallest M >= 2n - 1 with a three-pass split (power-of-2 or
     // single-radix columns, one-kernel rows) instead of bluestein.go:70's
@@ -774,17 +790,19 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
     if (e != hipSuccess) st = fail(GDSP_ERR_HIP, hipGetErrorString(e));
   }
   (void)hipFree(db);
+#ifdef GDSP_DEV_BUILD
   if (st == GDSP_OK && wave_chirpz_enabled() && gdsp::bluestein_wave_q(n, p->m))
     st = build_wave_tables(dev, p);
   if (st == GDSP_OK && !p->wq && shfl_chirpz_enabled() && p->kind == KIND_BLUESTEIN &&
       p->m == 8192 && 2 * n <= p->m)
     st = build_shfl_tables(p);
+#endif
   return st;
 }
 
 int get_plan_locked(int dev, int64_t n, gdsp_plan **out, bool chirpz = false) {
   auto &cache = chirpz ? g_chirpz_plans : g_plans;
-  auto key = std::make_pair(dev, n);
+  auto key = std::make_tuple(dev, n, gdsp::algo_flags());
   auto it = cache.find(key);
   if (it != cache.end()) {
     *out = it->second;
@@ -868,7 +886,7 @@ int exec_fourstep(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bo
     lc = 12;
     lr += 1;
   }
-  if (const char *e = getenv("GDSP_FS_LC")) {  // experiment: force the row length
+  if (const char *e = gdsp::dev_switch("GDSP_FS_LC")) {  // experiment: force the row length
     const int f = atoi(e);
     if (f >= 4 && f <= 13 && ln - f >= gdsp::kColMinLog2 && ln - f <= gdsp::kColMaxLog2) {
       lc = f;
@@ -1002,9 +1020,8 @@ int exec_bluestein_composed(const gdsp_plan *p, const cd *in, cd *out, int64_t b
   STCHK(a.alloc((size_t)batch * (size_t)p->m * sizeof(cd), s, SLOT_BLU));
   cd *da = (cd *)a.p;
   HIPCHK(gdsp::launch_chirp_premul(in, da, p->n, p->m, batch, p->chirp, inv, s));
-  static const bool unfused = getenv("GDSP_BLU_UNFUSED") != nullptr;
   const gdsp_plan *mp = p->mplan;
-  if (!unfused && mp->kind == KIND_MIXED4 && (mp->pow2col || mp->radixcol || mp->mixcol)) {
+  if (!p->unfused && mp->kind == KIND_MIXED4 && (mp->pow2col || mp->radixcol || mp->mixcol)) {
     // smooth M (a three-pass mixed four-step): the same two fused transposes
     const int64_t M = p->m;
     DevBuf work;
@@ -1026,7 +1043,7 @@ int exec_bluestein_composed(const gdsp_plan *p, const cd *in, cd *out, int64_t b
   }
   int lr = 0, lc = 0;
   fourstep_split(p->log2m, &lr, &lc);
-  if (!unfused && lc <= 13 && p->mplan->kind == KIND_GLOBAL) {
+  if (!p->unfused && lc <= 13 && p->mplan->kind == KIND_GLOBAL) {
     // both FFT_M as exec_fourstep's column tiles + rows, each final
     // transpose carrying the chirp-z step after it: conj(A * bhat) into da,
     // then conj(r) * chirp into out (two passes over M fewer)
@@ -1110,6 +1127,7 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
         HIPCHK(gdsp::launch_real_to_complex((const double *)in, (cd *)tmp.p, batch * p->n, s));
         src = (const cd *)tmp.p;
       }
+#ifdef GDSP_DEV_BUILD
       if (p->kind == KIND_BLUESTEIN && p->wq) {
         HIPCHK(gdsp::launch_bluestein_wave(p->wq, inv, src, out, p->n, batch, p->t2048, p->wbase,
                                            p->bhatw, p->chirp, scale, s));
@@ -1120,6 +1138,7 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
                                            p->bhats, scale, s));
         return GDSP_OK;
       }
+#endif
       if (p->kind == KIND_BLUESTEIN && p->parts > 1) {
         // the parts of a row run in different workgroups, so a part may
         // write the row before another has read it: in place (the four-step
@@ -1220,6 +1239,26 @@ int segment_count(int64_t lx, int64_t size, int64_t noverlap, int64_t *count) {
 
 }  // namespace
 
+// Configuration (launch.hpp): the deployment knobs, the development build's
+// experiment switches and the algorithm flags.
+namespace gdsp {
+const char *knob(Knob k) {
+  static const char *const names[] = {"GDSP_DEVICES",   "GDSP_MULTI_MIN_BYTES", "GDSP_JIT",
+                                      "GDSP_JIT_INCLUDE", "GDSP_JIT_CACHE",     "GDSP_JIT_VERBOSE",
+                                      "XDG_CACHE_HOME",  "HOME"};
+  return (int)k >= 0 && (int)k < (int)(sizeof names / sizeof names[0]) ? getenv(names[k]) : nullptr;
+}
+const char *dev_switch(const char *name) {
+#ifdef GDSP_DEV_BUILD
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
+unsigned algo_flags() { return g_algo.load(std::memory_order_relaxed); }
+}  // namespace gdsp
+
 // Forwarders for the multi-device layer (api_internal.hpp, multi.hip).
 namespace gdsp_api {
 int set_error(int st, const std::string &msg) { return fail(st, msg); }
@@ -1276,6 +1315,14 @@ int gdsp_device_count(void) {
   if (hipGetDeviceCount(&c) != hipSuccess) return 0;
   return c;
 }
+
+int gdsp_set_algorithm(unsigned flags) {
+  if (flags & ~kAlgoAll) return fail(GDSP_ERR_INVALID, "unknown algorithm flag");
+  g_algo.store(flags);
+  return GDSP_OK;
+}
+
+unsigned gdsp_get_algorithm(void) { return g_algo.load(); }
 
 int gdsp_fft(const double *x, double *out, int64_t n) {
   return host_batch(x, sizeof(cd), out, n, 1, false, gdsp::LOAD_COMPLEX);
@@ -1617,9 +1664,10 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
     // fused path: packed segment pairs, persistent workers over contiguous
     // pair ranges (the 50 % overlap of consecutive pairs is re-read from L2)
     const int64_t npairs = (nseg + 1) / 2;
-    static const int64_t wmul = [] {  // workers per workgroup slot (tuning switch)
-      const char *e = getenv("GDSP_PW_WORKERS");
-      return e ? (int64_t)atoll(e) : (int64_t)2048;
+    static const int64_t wmul = [] {  // workers per workgroup slot (development tuning switch)
+      const char *e = gdsp::dev_switch("GDSP_PW_WORKERS");
+      const int64_t v = e ? (int64_t)atoll(e) : 0;
+      return v >= 1 ? v : (int64_t)2048;
     }();
     int64_t target = wmul * (int64_t)gdsp::pwelch_workers_per_block(p->log2n);
     if (target > npairs) target = npairs;
@@ -1642,7 +1690,7 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
     return GDSP_OK;
   }
   if (p->kind == KIND_MIXED && (p->jit || gdsp::pwelch_fixed_workers_per_block(p->md) > 0) &&
-      !getenv("GDSP_PW_GENERIC")) {
+      !(gdsp::algo_flags() & GDSP_ALGO_GENERIC_MIXED)) {
     // fused path on a compiled specialisation (e.g. NFFT 1000, 3000)
     const int64_t npairs = (nseg + 1) / 2;
     const int wpb = p->jit ? gdsp::jit_pw_tpw(p->jit) : gdsp::pwelch_fixed_workers_per_block(p->md);

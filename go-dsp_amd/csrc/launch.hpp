@@ -30,6 +30,27 @@ constexpr int kMixedSpecMax = 8192;
 
 #ifndef __HIPCC_RTC__
 
+// ---- configuration (gdsp_api.hip) ------------------------------------------
+// Deployment knobs: the only process environment the library reads.
+enum Knob {
+  KNOB_DEVICES,          // GDSP_DEVICES: initial multi-device set ("0,1,2" / "all")
+  KNOB_MULTI_MIN_BYTES,  // GDSP_MULTI_MIN_BYTES: split threshold of host calls
+  KNOB_JIT,              // GDSP_JIT=0: no runtime-compiled specialisations
+  KNOB_JIT_INCLUDE,      // GDSP_JIT_INCLUDE: header directory for hipRTC
+  KNOB_JIT_CACHE,        // GDSP_JIT_CACHE: code-object cache directory
+  KNOB_JIT_VERBOSE,      // GDSP_JIT_VERBOSE: log runtime compilations
+  KNOB_XDG_CACHE_HOME,   // default cache location
+  KNOB_HOME,
+};
+const char *knob(Knob k);
+// Experiment switches of the development build (make DEV=1, GDSP_DEV_BUILD):
+// the switch's value there; nullptr in the default build, whose paths are the
+// measured ones.
+const char *dev_switch(const char *name);
+// Algorithm selection flags (gdsp_set_algorithm, include/gdsp_fft.h) in
+// force when a plan is built.
+unsigned algo_flags();
+
 hipError_t launch_fft_lds(int log2n, bool inv, int load, bool split, const void *in, cd *out,
                           int64_t batch, const cd *tw, double scale, hipStream_t s);
 // fused Pwelch over a mixed-radix segment length d.n = max(pad, nfft) with
@@ -72,6 +93,8 @@ hipError_t launch_bluestein(int log2m, bool inv, const cd *in, cd *out, int64_t 
 hipError_t launch_bluestein_parts(int log2m, bool inv, const cd *in, cd *out, int64_t n,
                                   int64_t batch, int parts, int64_t kpart, const cd *twm,
                                   const cd *chirp, const cd *bhat, double scale, hipStream_t s);
+#ifdef GDSP_DEV_BUILD
+// ---- measured and rejected kernels (development build only) ----
 // wave-resident chirp-z (fft_wave.hip): waves per transform Q = M / 2048 for
 // 512 < n <= 1024 Q, 2n - 1 <= M (0: not this kernel's case)
 int bluestein_wave_q(int64_t n, int64_t m);
@@ -85,6 +108,12 @@ int bluestein_shfl_bin(int t, int r);
 hipError_t launch_bluestein_shfl(bool inv, const cd *in, cd *out, int64_t n, int64_t batch,
                                  const cd *twm, const cd *chirp, const cd *bhatp, double scale,
                                  hipStream_t s);
+// NFFT = 4096 half overlap with the in-wave second exchange (pwelch_shfl.hip);
+// same arguments and partial layout as launch_pwelch_half(12, ...)
+hipError_t launch_pwelch4096_shfl(const double *x, int64_t seg_begin, int64_t seg_end, int64_t ppw,
+                                  int64_t nworkers, const double *win, const cd *tw,
+                                  double *partial, hipStream_t s);
+#endif  // GDSP_DEV_BUILD
 hipError_t launch_global_pass(int radix, bool conj_in, int load, bool conj_scale_out,
                               const void *in, cd *out, const cd *tw, int log2n, int log2ns,
                               int64_t batch, double scale, hipStream_t s);
@@ -96,11 +125,6 @@ hipError_t launch_pwelch(int log2f, const double *x, int64_t nfft, int64_t strid
 hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int64_t seg_end,
                               int64_t ppw, int64_t nworkers, const double *win, const cd *tw,
                               double *partial, hipStream_t s);
-// NFFT = 4096 half overlap with the in-wave second exchange (pwelch_shfl.hip);
-// same arguments and partial layout as launch_pwelch_half(12, ...)
-hipError_t launch_pwelch4096_shfl(const double *x, int64_t seg_begin, int64_t seg_end, int64_t ppw,
-                                  int64_t nworkers, const double *win, const cd *tw,
-                                  double *partial, hipStream_t s);
 hipError_t launch_reduce_partials(const double *partial, int64_t nworkers, int64_t F, double *acc,
                                   double *scratch, hipStream_t s);
 int64_t reduce_scratch_doubles(int64_t nworkers, int64_t F);

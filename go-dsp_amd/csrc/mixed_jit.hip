@@ -117,7 +117,7 @@ void search(int n, int depth, int maxdepth, Choice &cur, Choice &best) {
 
 // GDSP_JIT_INCLUDE: compile against headers on disk (empty: the embedded ones)
 std::string include_dir() {
-  const char *e = getenv("GDSP_JIT_INCLUDE");
+  const char *e = knob(KNOB_JIT_INCLUDE);
   return e ? e : "";
 }
 
@@ -139,24 +139,34 @@ uint64_t fnv1a(const std::string &s, uint64_t h) {
 }
 
 std::string cache_dir() {
-  const char *e = getenv("GDSP_JIT_CACHE");
+  const char *e = knob(KNOB_JIT_CACHE);
   if (e && (!strcmp(e, "off") || !strcmp(e, "0"))) return "";
   std::string d;
   if (e && *e) d = e;
-  else if (const char *x = getenv("XDG_CACHE_HOME")) d = std::string(x) + "/gdspfft";
-  else if (const char *h = getenv("HOME")) d = std::string(h) + "/.cache/gdspfft";
+  else if (const char *x = knob(KNOB_XDG_CACHE_HOME)) d = std::string(x) + "/gdspfft";
+  else if (const char *h = knob(KNOB_HOME)) d = std::string(h) + "/.cache/gdspfft";
   else d = "/tmp/gdspfft-" + std::to_string((long)getuid());
   return d;
 }
 
+// The cache directory (created 0700) is used only when it is a real
+// directory owned by this user that nobody else can write: code objects
+// loaded from it run on the GPU, so another local user must not be able to
+// plant them (e.g. by pre-creating /tmp/gdspfft-<uid>).
 bool make_dirs(const std::string &d) {
   for (size_t p = 1; p <= d.size(); ++p) {
     if (p == d.size() || d[p] == '/') {
       const std::string sub = d.substr(0, p);
-      if (mkdir(sub.c_str(), 0755) != 0 && errno != EEXIST) return false;
+      if (mkdir(sub.c_str(), p == d.size() ? 0700 : 0755) != 0 && errno != EEXIST) return false;
     }
   }
   return true;
+}
+
+bool cache_dir_trusted(const std::string &d) {
+  struct stat st;
+  if (lstat(d.c_str(), &st) != 0) return false;
+  return S_ISDIR(st.st_mode) && st.st_uid == getuid() && (st.st_mode & (S_IWGRP | S_IWOTH)) == 0;
 }
 
 // cache file: "GDSPJIT1\n", the lowered (mangled) name of each kernel, then
@@ -224,7 +234,7 @@ bool load_functions(const std::vector<char> &code, const std::vector<std::string
 }
 
 bool verbose() {
-  static const bool v = getenv("GDSP_JIT_VERBOSE") != nullptr;
+  static const bool v = knob(KNOB_JIT_VERBOSE) != nullptr;
   return v;
 }
 
@@ -232,11 +242,11 @@ bool verbose() {
 
 bool jit_enabled() {
   static const bool on = [] {
-    const char *e = getenv("GDSP_JIT");
-    // GDSP_MIXED_GENERIC=1 (tests of the runtime-radix kernel) turns it off too
-    return !(e && e[0] == '0') && !getenv("GDSP_MIXED_GENERIC");
+    const char *e = knob(KNOB_JIT);
+    return !(e && e[0] == '0');
   }();
-  return on;
+  // GDSP_ALGO_GENERIC_MIXED (the runtime-radix kernel) turns it off too
+  return on && !(algo_flags() & GDSP_ALGO_GENERIC_MIXED);
 }
 
 bool jit_radices(int n, int *rad, int *npass) {
@@ -270,11 +280,33 @@ bool compile_module(int dev, const std::vector<std::string> &names, const std::s
   const std::string incdir = include_dir();
   const std::string inc = "-I" + (incdir.empty() ? std::string(".") : incdir);
   const char *opts[] = {arch.c_str(), "-O3", "-std=c++17", inc.c_str()};
-  // cache key: everything the code object depends on
+  // cache key: everything the code object depends on — the library and
+  // runtime-compiler versions, the headers (embedded, or the files in
+  // GDSP_JIT_INCLUDE by content), architecture, options and names
+  int rtc_major = 0, rtc_minor = 0;
+  (void)hiprtcVersion(&rtc_major, &rtc_minor);
   uint64_t key = fnv1a(gdsp_version(), gdsp_jit_embed::kHash);
+  key = fnv1a("hiprtc " + std::to_string(rtc_major) + "." + std::to_string(rtc_minor), key);
   key = fnv1a(arch + "|" + incdir + "|-O3 -std=c++17", key);
+  if (!incdir.empty()) {
+    for (int h = 0; h < gdsp_jit_embed::kCount; ++h) {
+      std::string text;
+      if (FILE *f = fopen((incdir + "/" + gdsp_jit_embed::kNames[h]).c_str(), "rb")) {
+        char buf[65536];
+        size_t got;
+        while ((got = fread(buf, 1, sizeof buf, f)) > 0) text.append(buf, got);
+        fclose(f);
+      }
+      key = fnv1a(std::string(gdsp_jit_embed::kNames[h]) + "\n" + text, key);
+    }
+  }
   for (const auto &nm : names) key = fnv1a(nm + ";", key);
-  const std::string cdir = cache_dir();
+  std::string cdir = cache_dir();
+  if (!cdir.empty() && !(make_dirs(cdir) && cache_dir_trusted(cdir))) {
+    if (verbose()) fprintf(stderr, "gdsp: hipRTC cache %s not used (not a private directory)\n",
+                           cdir.c_str());
+    cdir.clear();
+  }
   char hex[17];
   snprintf(hex, sizeof hex, "%016llx", (unsigned long long)key);
   const std::string cpath = cdir.empty() ? "" : cdir + "/" + hex + ".co";
@@ -382,8 +414,8 @@ JitCol *jit_col_build(int dev, const int *rad, int np) {
   // both (GDSP_COL_LDS / GDSP_COL_SPLIT=0 to compare)
   const int sl = ((L + 7) & ~7) + 1;
   int lds_max = 81920;
-  if (const char *e = getenv("GDSP_COL_LDS")) lds_max = atoi(e);
-  const char *se = getenv("GDSP_COL_SPLIT");
+  if (const char *e = dev_switch("GDSP_COL_LDS")) lds_max = atoi(e);
+  const char *se = dev_switch("GDSP_COL_SPLIT");
   const bool split = !(se && se[0] == '0');
   const int bytes = split ? 8 : 16;
   int w = 64;

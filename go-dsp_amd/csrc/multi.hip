@@ -96,7 +96,7 @@ int validate(const int *devices, int ndev, int count, std::vector<int> &out) {
 void read_env_locked(int count) {
   if (g_set_env_read) return;
   g_set_env_read = true;
-  const char *e = getenv("GDSP_DEVICES");
+  const char *e = gdsp::knob(gdsp::KNOB_DEVICES);
   if (!e || !*e) return;
   std::vector<int> ids;
   if (strcmp(e, "all") == 0) {
@@ -302,8 +302,9 @@ void pwelch_shard(int64_t nsegs, int64_t nfft, int64_t noverlap, int parts, int 
 
 int64_t multi_min_bytes() {
   static const int64_t v = [] {
-    const char *e = getenv("GDSP_MULTI_MIN_BYTES");
-    return e ? (int64_t)strtoll(e, nullptr, 10) : ((int64_t)64 << 20);
+    const char *e = gdsp::knob(gdsp::KNOB_MULTI_MIN_BYTES);
+    const int64_t v = e ? (int64_t)strtoll(e, nullptr, 10) : 0;
+    return v > 0 ? v : ((int64_t)64 << 20);
   }();
   return v;
 }

@@ -199,6 +199,24 @@ def Devices() -> list[int]:
     return list(arr[:n])
 
 
+# algorithm selection (gdsp_set_algorithm, include/gdsp_fft.h)
+ALGO_DEFAULT = 0
+ALGO_GENERIC_MIXED = 1
+ALGO_NO_CHIRPZ_PARTS = 2
+ALGO_CHIRPZ_POW2 = 4
+ALGO_CHIRPZ_UNFUSED = 8
+
+
+def SetAlgorithm(flags: int = ALGO_DEFAULT) -> None:
+    """Select alternative paths of the engine (same DFT) for plans built and
+    Pwelch calls made after this call (gdsp_set_algorithm)."""
+    check(lib().gdsp_set_algorithm(int(flags)), "SetAlgorithm")
+
+
+def Algorithm() -> int:
+    return int(lib().gdsp_get_algorithm())
+
+
 def MultiStats() -> dict:
     """gdsp_multi_stats: calls split over a device set since process start,
     and how Pwelch accumulators were combined."""

@@ -63,6 +63,30 @@ int gdsp_jit_stats(int64_t *built, int64_t *cached, int64_t *failed, char *last_
  * beyond hipGetDeviceCount). */
 int gdsp_device_count(void);
 
+/* Algorithm selection (no reference equivalent; additive). Every selection
+ * computes the same DFT (the reference's results within the 1e-9 bound)
+ * by another of the engine's paths; the default (0) takes the measured
+ * fastest. Flags apply to plans built after the call (plans are cached per
+ * length and flag set) and to Pwelch calls made after it; process-wide. */
+enum {
+  GDSP_ALGO_DEFAULT = 0,
+  /* smooth non-power-of-2 lengths (transforms and fused Pwelch) on the
+   * runtime-radix mixed kernels, without the compiled or runtime-compiled
+   * (hipRTC) specialisations */
+  GDSP_ALGO_GENERIC_MIXED = 1,
+  /* primes in (8192, 14563] on the composed chirp-z instead of the
+   * output-split fused kernel */
+  GDSP_ALGO_NO_CHIRPZ_PARTS = 2,
+  /* the composed chirp-z on the reference's M = NextPowerOf2(2n-1)
+   * (fft/bluestein.go:70) instead of a smaller smooth M */
+  GDSP_ALGO_CHIRPZ_POW2 = 4,
+  /* the composed chirp-z without its fused transposes */
+  GDSP_ALGO_CHIRPZ_UNFUSED = 8
+};
+/* Unknown bits → GDSP_ERR_INVALID (the selection is left unchanged). */
+int gdsp_set_algorithm(unsigned flags);
+unsigned gdsp_get_algorithm(void);
+
 /* ---- fft package: host pointers, synchronous ----------------------------- */
 
 /* fft.FFT — fft/fft.go:72-87. n <= 1 copies; power of 2 → Stockham radix-16

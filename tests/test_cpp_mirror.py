@@ -92,7 +92,7 @@ print("ok")
 
 @pytest.mark.gpu
 def test_mixed_generic_kernel_for_specialised_lengths():
-    """GDSP_MIXED_GENERIC=1 routes lengths that have a compiled
+    """GDSP_ALGO_GENERIC_MIXED routes lengths that have a compiled
     specialisation (n = 3000) through the generic mixed-radix kernel: both
     kernels must agree with the oracle (the bench times the specialisation)."""
     code = r'''
@@ -101,6 +101,8 @@ sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.envir
 import numpy as np, oracle
 g = importlib.import_module("go-dsp_amd")
 D = importlib.import_module("go-dsp_amd.device")
+g.fft.SetAlgorithm(g.fft.ALGO_GENERIC_MIXED)
+assert g.fft.Algorithm() == g.fft.ALGO_GENERIC_MIXED
 import torch
 assert D.plan(3000).kind == 5
 rng = np.random.default_rng(3)
@@ -113,7 +115,7 @@ for n in (3000, 1000, 2000, 1500, 2400, 1200, 960, 1920, 480, 1536, 3072, 12):
         assert err < 1e-9, (n, inv, err)
 print("ok")
 '''
-    env = dict(os.environ, GDSP_MIXED_GENERIC="1", REPO=REPO)
+    env = dict(os.environ, REPO=REPO)
     r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 

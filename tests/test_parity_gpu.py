@@ -669,7 +669,18 @@ def test_chirpz_primes(gdsp, oracle, n):
     assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
 
 
-# the wave-resident chirp-z kernel (fft_wave.hip, opt-in: GDSP_BLU_WAVE=1):
+def _dev_lib() -> str:
+    """The development build (make -C go-dsp_amd/csrc DEV=1, built by
+    __graft_entry__.build()): the measured-and-rejected kernels below and
+    their switches live only there."""
+    path = os.path.join(REPO, "go-dsp_amd", "lib_dev", "libgdspfft.so")
+    if not os.path.exists(path):
+        pytest.skip("development build (go-dsp_amd/lib_dev) not built")
+    return path
+
+
+# the wave-resident chirp-z kernel (fft_wave.hip, development build,
+# GDSP_BLU_WAVE=1):
 # Q = M/2048 waves per transform, Q = 1 (n <= 1024), 2, 4; the edges of each
 # range, primes, and batches that leave the last workgroup partly empty (2 or
 # 4 transforms per workgroup at Q = 2, 1). Its exchanges are a wave-local LDS
@@ -702,7 +713,8 @@ for n in [int(v) for v in os.environ["WAVE_N"].split()]:
         assert D.plan(n).wave_q == m // 2048, n
 print("ok")
 '''
-    env = dict(os.environ, REPO=REPO, GDSP_BLU_WAVE="1", WAVE_N=" ".join(map(str, WAVE_N)))
+    env = dict(os.environ, REPO=REPO, GDSP_BLU_WAVE="1", WAVE_N=" ".join(map(str, WAVE_N)),
+               GDSP_LIB=_dev_lib())
     r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 
@@ -733,7 +745,8 @@ for n in [int(v) for v in os.environ["SHFL_N"].split()]:
         assert e < 1e-9 and ei < 1e-9, (n, batch, e, ei)
 print("ok")
 '''
-    env = dict(os.environ, REPO=REPO, GDSP_BLU_SHFL="1", SHFL_N=" ".join(map(str, SHFL_N)))
+    env = dict(os.environ, REPO=REPO, GDSP_BLU_SHFL="1", SHFL_N=" ".join(map(str, SHFL_N)),
+               GDSP_LIB=_dev_lib())
     r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 
@@ -758,7 +771,7 @@ for n, win in ((40960, "hann"), (38913, "hann"), (6144, "hann"), (100000, "hammi
     assert e < 1e-9, (n, win, e)
 print("ok")
 '''
-    env = dict(os.environ, REPO=REPO, GDSP_PW_SHFL="1")
+    env = dict(os.environ, REPO=REPO, GDSP_PW_SHFL="1", GDSP_LIB=_dev_lib())
     r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 
@@ -790,9 +803,10 @@ def test_chirpz_convolution_length_selection():
     """Which convolution length M the composed chirp-z takes (gdsp_plan_info),
     and that every selectable path agrees with the oracle: by default 8209
     runs as the output-split chirp-z (2 parts on M = 16384) and 16411 on a
-    smooth M (<= 0.55 of the power of 2); GDSP_BLU_NOPARTS=1 puts 8209 on the
-    smooth M too, GDSP_CHIRPZ_POW2=1 keeps the reference's NextPowerOf2(2n-1)
-    (bluestein.go:70), and GDSP_BLU_UNFUSED=1 takes the unfused composition."""
+    smooth M (<= 0.55 of the power of 2); GDSP_ALGO_NO_CHIRPZ_PARTS puts 8209
+    on the smooth M too, GDSP_ALGO_CHIRPZ_POW2 keeps the reference's
+    NextPowerOf2(2n-1) (bluestein.go:70), and GDSP_ALGO_CHIRPZ_UNFUSED takes
+    the unfused composition (gdsp_set_algorithm)."""
     code = r'''
 import importlib, os, sys
 sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
@@ -800,8 +814,10 @@ import numpy as np, oracle
 g = importlib.import_module("go-dsp_amd")
 D = importlib.import_module("go-dsp_amd.device")
 import torch
-pow2 = os.environ.get("GDSP_CHIRPZ_POW2") == "1"
-parts = os.environ.get("GDSP_BLU_NOPARTS") != "1"
+flags = int(os.environ["ALGO"])
+g.fft.SetAlgorithm(flags)
+pow2 = bool(flags & g.fft.ALGO_CHIRPZ_POW2)
+parts = not flags & g.fft.ALGO_NO_CHIRPZ_PARTS
 rng = np.random.default_rng(8)
 for n in (8209, 16411):
     p = D.plan(n)
@@ -823,12 +839,12 @@ for n in (8209, 16411):
         ref = oracle.ifft_rows(x) if inv else oracle.fft_rows(x)
         err = max(np.linalg.norm(a - b) / np.linalg.norm(b) for a, b in zip(y, ref))
         assert err < 1e-9, (n, inv, err)
-print("ok", os.environ.get("GDSP_CHIRPZ_POW2"), os.environ.get("GDSP_BLU_UNFUSED"))
+print("ok", flags)
 '''
-    for extra in ({}, {"GDSP_BLU_NOPARTS": "1"},
-                  {"GDSP_CHIRPZ_POW2": "1", "GDSP_BLU_NOPARTS": "1"},
-                  {"GDSP_BLU_UNFUSED": "1", "GDSP_BLU_NOPARTS": "1"}):
-        env = dict(os.environ, REPO=REPO, **extra)
+    F = __import__("importlib").import_module("go-dsp_amd.fft")
+    for extra in (0, F.ALGO_NO_CHIRPZ_PARTS, F.ALGO_CHIRPZ_POW2 | F.ALGO_NO_CHIRPZ_PARTS,
+                  F.ALGO_CHIRPZ_UNFUSED | F.ALGO_NO_CHIRPZ_PARTS):
+        env = dict(os.environ, REPO=REPO, ALGO=str(extra))
         r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300,
                            env=env)
         assert r.returncode == 0 and "ok" in r.stdout, (extra, r.stdout + r.stderr[-3000:])
