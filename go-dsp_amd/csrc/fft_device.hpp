@@ -448,6 +448,7 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
   // t + 272 k
   constexpr bool L2 = LAYOUT == 2 && ILV == 0 && E == 16 && T == 256 && B == 1 &&
                       (NS == 1 || NS * R == 256);
+  constexpr int BLK = 272;
   // LAYOUT 1 (LINEAR, slot i + i / E) where it is a per-thread base plus a
   // compile-time offset: a first exchange of one butterfly per thread
   // (i = E t + r), or NS a multiple of E (i / E splits exactly)
@@ -471,7 +472,7 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
 #pragma unroll
     for (int r = 0; r < R; ++r) dst[r] = 16 * t + (r ^ m);
   } else if constexpr (L2) {
-    const int base = (t / NS) * 272 + (t & (NS - 1));
+    const int base = (t / NS) * BLK + (t & (NS - 1));
 #pragma unroll
     for (int r = 0; r < R; ++r) dst[r] = base + r * NS;
   } else {
@@ -494,7 +495,7 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
     rstep = 256;
   } else if constexpr (L2) {
     rbase = t;
-    rstep = 272;
+    rstep = BLK;
   }
   auto src = [&](int k) -> int {
     if constexpr (L2 || LIN) return rbase + k * rstep;

@@ -125,6 +125,10 @@ hipError_t launch_pwelch(int log2f, const double *x, int64_t nfft, int64_t strid
 hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int64_t seg_end,
                               int64_t ppw, int64_t nworkers, const double *win, const cd *tw,
                               double *partial, hipStream_t s);
+// the row kernel (pwelch_row.hip) behind launch_pwelch_half(12, ...)
+hipError_t launch_pwelch_row4096(const double *x, int64_t seg_begin, int64_t seg_end, int64_t ppw,
+                                 int64_t nworkers, const double *win, const cd *tw,
+                                 double *partial, hipStream_t s);
 hipError_t launch_reduce_partials(const double *partial, int64_t nworkers, int64_t F, double *acc,
                                   double *scratch, hipStream_t s);
 int64_t reduce_scratch_doubles(int64_t nworkers, int64_t F);

@@ -1,0 +1,130 @@
+// pwelch_row.hip — the fused Pwelch kernel of the BASELINE configuration
+// (NFFT 4096, Noverlap 2048, Pad = NFFT; spectral/pwelch.go:104-122). Its own
+// translation unit so it can be compiled with the max-ILP scheduler
+// (Makefile): 2.81 against 2.85-2.89 ms with the default scheduler, at the
+// same 246-248 VGPRs (the other kernels keep the default: the chirp-z kernel
+// would lose a wave per SIMD to it).
+#include "fft_device.hpp"
+#include "launch.hpp"
+
+namespace gdsp {
+
+// Half-overlap Pwelch with one worker per workgroup (TPW = 1: F >= 4096, the
+// BASELINE configuration). Same packing, carry and accumulation as
+// pwelch_half_kernel, arranged so that the loop's bookkeeping costs no
+// vector instructions:
+//  - the worker's pair range, segment offsets and the has-partner test are
+//    wave-uniform (scalar registers and branches); the loop runs over the
+//    worker's own pairs only, full pairs first, then at most one pair whose
+//    second segment does not exist (odd count: zero partner, its own body);
+//  - each sample row is a scalar base pointer plus the lane's 32-bit offset
+//    (global_load saddr: no 64-bit address arithmetic per load);
+//  - the next pair's samples are loaded into the registers this pair's
+//    samples just left (after the window multiply), so they are in flight
+//    during the FFT with no double buffer to copy between;
+//  - each pass's twiddle base (the same for every pair) is read once per
+//    kernel into registers (no LDS table, no bank conflicts on it); pass 1's
+//    powers from an LDS table instead of each pair's chain measured slower
+//    (2.99-3.01 against 2.86-2.87 ms: LDS, not the vector unit, is the
+//    scarcer resource here);
+//  - LAYOUT 2 exchange slots (fft_device.hpp): every LDS address a per-thread
+//    base plus a compile-time offset (2.81-2.84 against 2.94-2.97 ms with
+//    XOR-swizzled slots throughout).
+// (Measured and not kept: the exchange through two unpadded buffers, real
+// and imaginary parts at once with two barriers per exchange instead of
+// four, and half the (symmetric) window in LDS to keep 80 KiB and two
+// workgroups per CU: 3.10-3.17 against 2.83 ms.)
+template <int LOG2F, int LOG2E = 4, bool REGTW = true, int LAYOUT = 2>
+__global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_row_kernel(
+    const double *__restrict__ x, int64_t seg_begin, int64_t seg_end, int64_t pairs_per_worker,
+    const double *__restrict__ win, const cd *__restrict__ tw, double *__restrict__ partial) {
+  using G = Geo<LOG2F, LOG2E>;
+  static_assert(G::TPW == 1, "one worker per workgroup");
+  static_assert(!REGTW || (G::E == G::EMAX && G::NPE == G::NPASS && G::NPASS <= 4),
+                "register twiddles need radix-E passes with one butterfly per thread");
+  constexpr int E = G::E, H = E / 2, T = G::T;
+  constexpr int64_t STRIDE = G::N / 2;
+  __shared__ double lds[G::LDS_DOUBLES + G::N];
+  double *const lx = lds;                   // exchange (real / imaginary halves in turn)
+  double *const wl = lds + G::LDS_DOUBLES;  // window
+  const int t = threadIdx.x;
+  const uint32_t lane = (uint32_t)t;
+  for (int i = t; i < G::N; i += G::WG) wl[i] = win[i];
+  using RT = RegTw<G::NPASS>;
+  RT rtw;
+#pragma unroll
+  for (int p = 0; p < G::NPASS; ++p) rtw.base[p] = {1.0, 0.0};
+  if constexpr (REGTW) {
+    if constexpr (G::NPASS > 1) rtw.base[1] = pass_base<G::N, G::EMAX, G::ns(1)>(tw, t);
+    if constexpr (G::NPASS > 2) rtw.base[2] = pass_base<G::N, G::EMAX, G::ns(2)>(tw, t);
+    if constexpr (G::NPASS > 3) rtw.base[3] = pass_base<G::N, G::EMAX, G::ns(3)>(tw, t);
+  }
+  __syncthreads();
+  const int64_t npairs = (seg_end - seg_begin + 1) / 2;  // pairs, the last maybe partnerless
+  const int64_t nfull = (seg_end - seg_begin) / 2;       // pairs with both segments
+  const int64_t p0 = (int64_t)blockIdx.x * pairs_per_worker;
+  const int64_t pend = p0 + pairs_per_worker < npairs ? p0 + pairs_per_worker : npairs;
+  const int64_t fend = pend < nfull ? pend : nfull;
+  if (p0 >= pend) return;  // whole workgroup (uniform): no barrier follows
+  // row r of a pair's samples: x[(seg_begin + 2p) STRIDE + r T + lane]; the
+  // rows a pair needs beyond its carry are H .. 2E-1 ... as scalar pointers
+  auto row = [&](int64_t p, int r) -> const double * {
+    return opaque_ptr(x + (seg_begin + 2 * p) * STRIDE + (int64_t)r * T);
+  };
+  double carry[H], a2[H], c2[H];
+#pragma unroll
+  for (int k = 0; k < H; ++k) carry[k] = row(p0, k)[lane];
+  // samples of pair p: a = (carry, a2) is segment s0, (a2, c2) segment s0+1;
+  // c2 of a partnerless pair is not read (its rows are clamped onto a2's)
+  auto issue = [&](int64_t p) {
+    const int cr = p < nfull ? E : H;
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      a2[k] = row(p, H + k)[lane];
+      c2[k] = row(p, cr + k)[lane];
+    }
+  };
+  issue(p0);
+  double acc[E];
+#pragma unroll
+  for (int k = 0; k < E; ++k) acc[k] = 0.0;
+  auto pair = [&](int64_t p, bool first, bool partner) {
+    const int tt = opaque_int(t);
+    cd v[E];
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      const double w0 = wl[tt + k * T], w1 = wl[tt + (H + k) * T];
+      v[k] = {carry[k] * w0, partner ? a2[k] * w0 : 0.0};
+      v[H + k] = {a2[k] * w1, partner ? c2[k] * w1 : 0.0};
+    }
+#pragma unroll
+    for (int k = 0; k < H; ++k) carry[k] = c2[k];
+    if (p + 1 < pend) issue(p + 1);
+    RT rl = rtw;
+#pragma unroll
+    for (int q = 1; q < G::NPASS; ++q) rl.base[q] = opaque_cd(rl.base[q]);
+    if constexpr (REGTW)
+      fft_regs<LOG2F, true, 2, LOG2E, 0, 0, RT, LAYOUT, false, NoEpi, 0>(v, tt, rl, lx, lx, first);
+    else
+      fft_regs<LOG2F, true, 1, LOG2E, 0, 0, const cd *, LAYOUT>(v, tt, tw, lx, lx, first);
+#pragma unroll
+    for (int k = 0; k < E; ++k) acc[k] = fma(v[k].y, v[k].y, fma(v[k].x, v[k].x, acc[k]));
+  };
+  int64_t p = p0;
+  for (; p < fend; ++p) pair(p, p == p0, true);
+  if (p < pend) pair(p, p == p0, false);  // the odd count's last segment, zero partner
+  double *dst = partial + blockIdx.x * (int64_t)G::N;
+#pragma unroll
+  for (int k = 0; k < E; ++k) dst[t + k * T] = acc[k];
+}
+
+
+hipError_t launch_pwelch_row4096(const double *x, int64_t seg_begin, int64_t seg_end, int64_t ppw,
+                                 int64_t nworkers, const double *win, const cd *tw,
+                                 double *partial, hipStream_t s) {
+  hipLaunchKernelGGL((pwelch_row_kernel<12>), dim3((unsigned)nworkers), dim3(Geo<12>::WG), 0, s,
+                     x, seg_begin, seg_end, ppw, win, tw, partial);
+  return hipGetLastError();
+}
+
+}  // namespace gdsp
