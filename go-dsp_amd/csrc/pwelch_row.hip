@@ -20,8 +20,8 @@ namespace gdsp {
 //  - each sample row is a scalar base pointer plus the lane's 32-bit offset
 //    (global_load saddr: no 64-bit address arithmetic per load);
 //  - the next pair's samples are loaded into the registers this pair's
-//    samples just left (after the window multiply), so they are in flight
-//    during the FFT with no double buffer to copy between;
+//    samples just left (copied into the transform's registers), so they are
+//    in flight during the FFT with no double buffer to copy between;
 //  - each pass's twiddle base (the same for every pair) is read once per
 //    kernel into registers (no LDS table, no bank conflicts on it); pass 1's
 //    powers from an LDS table instead of each pair's chain measured slower
@@ -34,6 +34,10 @@ namespace gdsp {
 // and imaginary parts at once with two barriers per exchange instead of
 // four, and half the (symmetric) window in LDS to keep 80 KiB and two
 // workgroups per CU: 3.10-3.17 against 2.83 ms.)
+// Also measured and not kept: the window folded into pass 0's first radix-2
+// stage as FMAs (w_j z_j +- w_(j+8) z_(j+8): 16 fewer FP64 instructions per
+// thread and pair), 2.92 against 2.74 ms — the weights stay live in 32 more
+// registers through the first DFT.
 template <int LOG2F, int LOG2E = 4, bool REGTW = true, int LAYOUT = 2>
 __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_row_kernel(
     const double *__restrict__ x, int64_t seg_begin, int64_t seg_end, int64_t pairs_per_worker,
@@ -91,11 +95,13 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_row_kernel(
   auto pair = [&](int64_t p, bool first, bool partner) {
     const int tt = opaque_int(t);
     cd v[E];
+    double wv[E];
 #pragma unroll
     for (int k = 0; k < H; ++k) {
-      const double w0 = wl[tt + k * T], w1 = wl[tt + (H + k) * T];
-      v[k] = {carry[k] * w0, partner ? a2[k] * w0 : 0.0};
-      v[H + k] = {a2[k] * w1, partner ? c2[k] * w1 : 0.0};
+      wv[k] = wl[tt + k * T];
+      wv[H + k] = wl[tt + (H + k) * T];
+      v[k] = {carry[k], partner ? a2[k] : 0.0};
+      v[H + k] = {a2[k], partner ? c2[k] : 0.0};
     }
 #pragma unroll
     for (int k = 0; k < H; ++k) carry[k] = c2[k];
@@ -103,6 +109,9 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_row_kernel(
     RT rl = rtw;
 #pragma unroll
     for (int q = 1; q < G::NPASS; ++q) rl.base[q] = opaque_cd(rl.base[q]);
+    // the window multiply after the next pair's loads are issued
+#pragma unroll
+    for (int k = 0; k < E; ++k) v[k] = {v[k].x * wv[k], v[k].y * wv[k]};
     if constexpr (REGTW)
       fft_regs<LOG2F, true, 2, LOG2E, 0, 0, RT, LAYOUT, false, NoEpi, 0>(v, tt, rl, lx, lx, first);
     else
