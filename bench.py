@@ -43,10 +43,10 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (tools/fp64peak.hip measures 
 # kernels whose FP64 work is taken from the committed SQ counter passes
 # (profiles/r02/sq_counters.json: 64 x (2 FMA + ADD + MUL) F64 instructions)
 SQ_KERNELS = {"radix4096": ["fft_lds_kernel<12"], "bluestein3000": ["fft_mixed_fixed_kernel"],
-              "chirpz3000": ["bluestein_kernel<13"], "pwelch": ["pwelch_half_kernel<12"],
+              "chirpz3000": ["bluestein_kernel<13"], "pwelch": ["pwelch_row_kernel<12"],
               "fft2_8192": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"],
               "fft2_dist": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"]}
-SQ_ROUND = "r02"  # the round whose SQ counter passes bench lines quote
+SQ_ROUNDS = ("r03", "r02")  # SQ counter passes quoted: the newest round that has the kernel
 SEED = 0x5EED
 # algorithmic bytes of one launch in the N=1 full-size configuration the
 # committed PMC (profiles/pmc_*.json) and SQ (profiles/r02/sq_counters.json)
@@ -253,7 +253,7 @@ def setup(w: str, c: Ctx, weak: bool = False) -> dict:
 
     return dict(step=step, x=x, shard=sh, opts=opts, result=result, total_samples=total,
                 rank_samples=total // world,
-                alg_bytes=8 * x.numel(), kernel="pwelch_half_kernel<12>",
+                alg_bytes=8 * x.numel(), kernel="pwelch_row_kernel<12>",
                 metric="Gsamples/s, spectral.Pwelch 2^30 samples NFFT 4096 50% overlap",
                 scaling="strong",
                 cfg={"workload": "spectral.Pwelch 2^30-sample stream, Hann NFFT 4096, 50% "
@@ -591,27 +591,36 @@ def main():
 
 
 def fp64_info(workload: str, launch_s: float, share: float = 1.0):
-    """FP64 work of one launch (from the committed SQ counters, FFT2 summed
-    over its kernels, times this launch's share of the profiled work)
-    against the FP64 vector peak — the second roofline of the compute-heavy
-    paths (chirp-z, Pwelch)."""
-    path = os.path.join(REPO, "profiles", SQ_ROUND, "sq_counters.json")
-    ks = SQ_KERNELS.get("fft2_8192" if workload == "fft2_dist" else workload)
-    if not ks or not os.path.exists(path):
+    """FP64 work of one launch (from the committed SQ counters of the newest
+    round that profiled this workload's kernels, FFT2 summed over its
+    kernels, times this launch's share of the profiled work) against the FP64
+    vector peak — the second roofline of the compute-heavy paths (chirp-z,
+    Pwelch)."""
+    w = "fft2_8192" if workload == "fft2_dist" else workload
+    ks = SQ_KERNELS.get(w)
+    if not ks:
         return None
-    with open(path) as f:
-        sq = json.load(f).get("fft2_8192" if workload == "fft2_dist" else workload, {})
-    flop = 0.0
-    for k in ks:
-        hit = [v for name, v in sq.items() if k in name]
-        if not hit:
-            return None
-        flop += hit[0]["f64_flop"]
-    flop *= share
-    tf = flop / launch_s / 1e12
-    return {"flop_per_launch": flop, "achieved_tflops": round(tf, 2),
-            "peak_tflops": FP64_PEAK_TFLOPS, "frac": round(tf / FP64_PEAK_TFLOPS, 4),
-            "source": f"profiles/{SQ_ROUND}/sq_counters.json (SQ_INSTS_VALU_{{FMA,ADD,MUL}}_F64)"}
+    for rnd in SQ_ROUNDS:
+        path = os.path.join(REPO, "profiles", rnd, "sq_counters.json")
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            sq = json.load(f).get(w, {})
+        flop, found = 0.0, True
+        for k in ks:
+            hit = [v for name, v in sq.items() if k in name]
+            if not hit:
+                found = False
+                break
+            flop += hit[0]["f64_flop"]
+        if not found:
+            continue
+        flop *= share
+        tf = flop / launch_s / 1e12
+        return {"flop_per_launch": flop, "achieved_tflops": round(tf, 2),
+                "peak_tflops": FP64_PEAK_TFLOPS, "frac": round(tf / FP64_PEAK_TFLOPS, 4),
+                "source": f"profiles/{rnd}/sq_counters.json (SQ_INSTS_VALU_{{FMA,ADD,MUL}}_F64)"}
+    return None
 
 
 def cpu_baseline(workload: str, seconds: float):
