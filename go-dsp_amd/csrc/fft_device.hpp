@@ -215,22 +215,104 @@ struct Dft<32> {
   __device__ __forceinline__ static void run(cd (&a)[32]) { dft_split<8, 4>(a); }
 };
 
-// DFT_R of an input whose upper half is zero (a[R/2 ..] = 0, as in the first
-// pass of a chirp-z FFT, where n <= M/2): X[2m] = DFT_{R/2}(a)[m] and
-// X[2m+1] = DFT_{R/2}(a_j W_R^j)[m], one radix-2 stage fewer than Dft<R>
-// (compile-time zeros do not fold away: x + 0.0 is not x for x = -0.0).
-template <int R>
+// DFTs of inputs known to be zero past a point (a[j] = 0 for j >= NZ, a
+// compile-time count), as in the first pass of a chirp-z FFT where the input
+// fills at most n of M points: the radix-2 stages that would add a zero are
+// left out (compile-time zeros do not fold away by themselves: x + 0.0 is
+// not x for x = -0.0).
+template <int R, int NZ>
+struct DftZ;
+
+// split R1*R2 as dft_split, column n2 of the first stage holding
+// ceil((NZ - n2) / R2) nonzero inputs
+template <int R1, int R2, int NZ, int N2 = 0>
+struct SplitZCol {
+  __device__ __forceinline__ static void run(const cd (&a)[R1 * R2], cd (&y)[R2][R1]) {
+    if constexpr (N2 < R2) {
+      constexpr int C0 = (NZ - N2 + R2 - 1) / R2;
+      constexpr int C = C0 < 0 ? 0 : (C0 > R1 ? R1 : C0);
+      cd tmp[R1];
+#pragma unroll
+      for (int n1 = 0; n1 < R1; ++n1) tmp[n1] = a[R2 * n1 + N2];
+      if constexpr (C == 0) {
+#pragma unroll
+        for (int k1 = 0; k1 < R1; ++k1) y[N2][k1] = {0.0, 0.0};
+      } else {
+        DftZ<R1, C>::run(tmp);
+#pragma unroll
+        for (int k1 = 0; k1 < R1; ++k1) y[N2][k1] = rot32(tmp[k1], N2 * k1 * (32 / (R1 * R2)));
+      }
+      SplitZCol<R1, R2, NZ, N2 + 1>::run(a, y);
+    }
+  }
+};
+
+template <int R1, int R2, int NZ>
+__device__ __forceinline__ void dft_split_z(cd (&a)[R1 * R2]) {
+  cd y[R2][R1];
+  SplitZCol<R1, R2, NZ>::run(a, y);
+#pragma unroll
+  for (int k1 = 0; k1 < R1; ++k1) {
+    cd tmp[R2];
+#pragma unroll
+    for (int n2 = 0; n2 < R2; ++n2) tmp[n2] = y[n2][k1];
+    Dft<R2>::run(tmp);
+#pragma unroll
+    for (int k2 = 0; k2 < R2; ++k2) a[k1 + R1 * k2] = tmp[k2];
+  }
+}
+
+template <int R, int NZ>
+struct DftZ {
+  __device__ __forceinline__ static void run(cd (&a)[R]) {
+    static_assert(NZ >= 1, "at least one nonzero input");
+    if constexpr (NZ >= R) {
+      Dft<R>::run(a);
+    } else if constexpr (R == 2) {
+      a[1] = a[0];
+    } else if constexpr (R == 4) {
+      // t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3, d = a1 - a3 with zeros left out
+      const cd t0 = NZ >= 3 ? a[0] + a[2] : a[0];
+      const cd t1 = NZ >= 3 ? a[0] - a[2] : a[0];
+      const cd t2 = NZ >= 2 ? a[1] : cd{0.0, 0.0};
+      const cd t3 = {t2.y, -t2.x};  // d * (-i), d = a1
+      if constexpr (NZ == 1) {
+        a[1] = a[0];
+        a[2] = a[0];
+        a[3] = a[0];
+      } else {
+        a[0] = t0 + t2;
+        a[1] = t1 + t3;
+        a[2] = t0 - t2;
+        a[3] = t1 - t3;
+      }
+    } else if constexpr (R == 8) {
+      dft_split_z<4, 2, NZ>(a);
+    } else if constexpr (R == 16) {
+      dft_split_z<4, 4, NZ>(a);
+    } else {
+      static_assert(R == 32, "pruned DFTs up to 32");
+      dft_split_z<8, 4, NZ>(a);
+    }
+  }
+};
+
+// DFT_R of an input that fills at most half of it (a[j] = 0 for j >= NZ,
+// NZ <= R/2): X[2m] = DFT_{R/2}(a)[m] and X[2m+1] = DFT_{R/2}(a_j W_R^j)[m],
+// one radix-2 stage fewer than Dft<R>, each half pruned to its NZ inputs.
+template <int R, int NZ = R / 2>
 __device__ __forceinline__ void dft_half_in(cd (&a)[R]) {
   static_assert(R >= 4 && R <= 32, "rot32 covers W_R for R <= 32");
+  static_assert(NZ >= 1 && NZ <= R / 2, "input within the first half");
   constexpr int H = R / 2;
   cd e[H], o[H];
 #pragma unroll
   for (int j = 0; j < H; ++j) {
     e[j] = a[j];
-    o[j] = rot32(a[j], j * (32 / R));
+    o[j] = j < NZ ? rot32(a[j], j * (32 / R)) : cd{0.0, 0.0};
   }
-  Dft<H>::run(e);
-  Dft<H>::run(o);
+  DftZ<H, NZ>::run(e);
+  DftZ<H, NZ>::run(o);
 #pragma unroll
   for (int m = 0; m < H; ++m) {
     a[2 * m] = e[m];
@@ -286,7 +368,7 @@ __device__ __forceinline__ int padi(int i) { return i + (i >> 4); }
 // Twiddle + DFT of one Stockham pass on the thread's registers. v[b + r*B]
 // holds input r of butterfly j = t + b*T. tw: forward table T_N[k] =
 // exp(-2 pi i k/N).
-// HALF_IN: the upper half of every butterfly's inputs is zero (first pass,
+// ZIN: only the first ZIN inputs of every butterfly are nonzero (first pass,
 // NS = 1, of a transform whose input fills at most half the points)
 // Epilogue of a transform's last pass (EPI::on): butterfly b's outputs k =
 // b + r B go through epi.apply(v, k, u, f) with f = epi.load(k) loaded before
@@ -334,7 +416,7 @@ __device__ __forceinline__ cd opaque_cd(cd w) {
 // WPRE: the butterflies' twiddle bases come in wpre[b] (loaded by the caller
 // a pass ahead: fft_regs PREW) instead of being read here
 // PASS: this pass's index (selects a RegTw's base)
-template <int N, int E, int T, int R, int NS, bool HALF_IN = false, class EPI = NoEpi,
+template <int N, int E, int T, int R, int NS, int ZIN = 0, class EPI = NoEpi,
           bool WPRE = false, int PASS = 0, class TWP = const cd *>
 __device__ __forceinline__ void pass_compute(cd (&v)[E], int t, TWP tw,
                                              const EPI &epi = EPI(), const cd *wpre = nullptr) {
@@ -377,7 +459,10 @@ __device__ __forceinline__ void pass_compute(cd (&v)[E], int t, TWP tw,
         }
       }
     }
-    if constexpr (HALF_IN && NS == 1 && R >= 4) dft_half_in<R>(u);
+    if constexpr (ZIN > 0 && NS == 1 && R >= 4) {
+      static_assert(B == 1, "input pruning of a pass with one butterfly per thread");
+      dft_half_in<R, ZIN>(u);
+    }
     else Dft<R>::run(u);
     if constexpr (EPI::on) {
 #pragma unroll
@@ -559,15 +644,16 @@ using RegArr = cd[Geo<LOG2N, LOG2E>::E];
 // address or twiddle value survives from one call to the next); 2 launder
 // only the thread index — enough to keep twiddle loads inside a loop, and it
 // leaves an LDS twiddle pointer's address space visible (ds_read, not flat).
-// HALF_IN: elements t + k T with k >= E/2 are zero on entry (pass 0 prunes
-// one radix-2 stage; pass_compute)
+// HALF_IN: elements t + k T with k >= HALF_IN (<= E/2; 0: none) are zero on
+// entry (pass 0 prunes one radix-2 stage and the additions of zeros;
+// pass_compute)
 // EPI: the last pass's epilogue (pass_compute)
 // PREW: each pass's twiddle bases are read before the previous pass's
 // arithmetic and exchange (wpre carries them down), so their L1/L2 or LDS
 // latency hides behind that work instead of opening the pass; only for
 // passes with at most PREW bases per thread (0: off)
 template <int LOG2N, bool SPLIT, int OPAQUE = 0, int LOG2E = 4, int ILV = 0, int P = 0,
-          class TWP = const cd *, int LINEAR = 0, bool HALF_IN = false, class EPI = NoEpi,
+          class TWP = const cd *, int LINEAR = 0, int HALF_IN = 0, class EPI = NoEpi,
           int PREW = 0>
 __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw, double *lre,
                                          double *lim, bool first_exchange = true,
@@ -598,10 +684,10 @@ __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw,
     }
     constexpr bool USE_PRE = PREW >= G::E / R && P > 0 && NS > 1;
     if constexpr (P == G::NPASS - 1)
-      pass_compute<G::N, G::E, G::T, R, NS, HALF_IN && P == 0, EPI, USE_PRE, P, TWP>(v, t, tw, epi,
+      pass_compute<G::N, G::E, G::T, R, NS, P == 0 ? HALF_IN : 0, EPI, USE_PRE, P, TWP>(v, t, tw, epi,
                                                                                     wpre);
     else
-      pass_compute<G::N, G::E, G::T, R, NS, HALF_IN && P == 0, NoEpi, USE_PRE, P, TWP>(
+      pass_compute<G::N, G::E, G::T, R, NS, P == 0 ? HALF_IN : 0, NoEpi, USE_PRE, P, TWP>(
           v, t, tw, NoEpi(), wpre);
     fft_regs<LOG2N, SPLIT, 0, LOG2E, ILV, P + 1, TWP, LINEAR, false, EPI, PREW>(
         v, t, tw, lre, lim, first_exchange, epi, PRE_NEXT ? wn : nullptr);

@@ -251,7 +251,11 @@ constexpr int kBluPf = 16;
 constexpr int kBluPf14 = 4;     // M = 16384, one block per CU: 2-4 % faster than 8 or 16
 constexpr int kBluPfParts = 2;  // PARTS: the row's part-0 block touches 2 rows on
 constexpr int kBluPfShift = 7;  // touch granularity: one load per 2^7 bytes (a line)
-template <int LOG2M, bool INV, bool SPLIT, int LOG2E = 4, bool PARTS = false>
+// KN (one transform per workgroup, the buffer path): n <= KN T, so
+// registers k >= KN hold no input to FFT 1 and no wanted output of FFT 2 —
+// pass 0 of FFT 1 adds no zeros and the last pass of FFT 2 forms only the
+// outputs below KN T (0: KN = E/2, what n <= M/2 guarantees for any n).
+template <int LOG2M, bool INV, bool SPLIT, int LOG2E = 4, bool PARTS = false, int KN = 0>
 __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
     const cd *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
     const cd *__restrict__ twm, const cd *__restrict__ chirp, const cd *__restrict__ bhat,
@@ -277,9 +281,11 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
   double *lim = SPLIT ? lre : lds + G::LDS_DOUBLES + slot * G::STRIDE;
   // n <= M/2 (M is a power of 2 >= 2n - 1): registers k >= E/2 hold no input
   // and no output, so the first pass of FFT 1 and the last of FFT 2 are pruned
-  constexpr int KH = G::E > 1 ? G::E / 2 : G::E;
-  constexpr bool HALF = G::E >= 4 && !PARTS;
+  static_assert(KN == 0 || (KN >= 1 && KN <= G::E / 2 && !PARTS), "KN within the first half");
+  constexpr int KH = KN > 0 ? KN : (G::E > 1 ? G::E / 2 : G::E);
   constexpr int KIN = PARTS ? G::E : KH;
+  // pass 0 of FFT 1: the nonzero inputs per butterfly (0: no pruning)
+  constexpr int ZIN = G::E >= 4 && !PARTS ? KH : 0;
   // this block's outputs: X[k0 + k], k < nout
   int64_t nout = n;
   const cd *ochirp = chirp;
@@ -327,7 +333,7 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
       }
     }
     const BhatBufEpi<G::T> be{make_rsrc(bhat, (int64_t)G::N * 16), off};
-    fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, HALF, BhatBufEpi<G::T>,
+    fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, ZIN, BhatBufEpi<G::T>,
              blu_prew(LOG2M)>(v, t, twm, lre, lim, true, be);
     const ChirpOutBufEpi<G::T, KH, INV> oe{make_rsrc(opaque_ptr(chirp), rowb),
                                            make_rsrc(out + gu * n, rowb), (uint32_t)opaque_int(t) * 16u,
@@ -378,10 +384,10 @@ __global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
   if constexpr (EPI >= 1) {
     // x bhat, conj: fused into FFT 1's last pass, each butterfly's factors
     // loaded ahead of its arithmetic
-    fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, HALF, BhatEpi<G::T>, blu_prew(LOG2M)>(
+    fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, ZIN, BhatEpi<G::T>, blu_prew(LOG2M)>(
         v, t, twm, lre, lim, true, BhatEpi<G::T>{bhat + t});
   } else {
-    fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, HALF, NoEpi, blu_prew(LOG2M)>(
+    fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, ZIN, NoEpi, blu_prew(LOG2M)>(
         v, t, twm, lre, lim, true);
 #pragma unroll
     for (int k = 0; k < G::E; ++k) v[k] = conjg(cmul(v[k], bhat[t + k * G::T]));
@@ -1060,6 +1066,17 @@ static hipError_t launch_blu_t(const cd *in, cd *out, int64_t n, int64_t batch, 
     if (e32) {
       using G5 = Geo<LOG2M, 5>;
       const int64_t nb5 = (batch + G5::TPW - 1) / G5::TPW;
+      if constexpr (LOG2M == 13) {
+        // n <= 3072 = 12 T at M = 8192 (the BASELINE n = 3000): 12 of the 32
+        // registers carry input and wanted output
+        static const bool kn_off = dev_switch("GDSP_BLU_NOKN") != nullptr;
+        if (!kn_off && n <= 12 * G5::T) {
+          hipLaunchKernelGGL((bluestein_kernel<LOG2M, INV, true, 5, false, 12>),
+                             dim3((unsigned)nb5), dim3(G5::WG), 0, s, in, out, n, batch, twm,
+                             chirp, bhat, scale, (int64_t)0, 1);
+          return hipGetLastError();
+        }
+      }
       hipLaunchKernelGGL((bluestein_kernel<LOG2M, INV, true, 5>), dim3((unsigned)nb5),
                          dim3(G5::WG), 0, s, in, out, n, batch, twm, chirp, bhat, scale,
                          (int64_t)0, 1);

@@ -34,7 +34,9 @@ namespace gdsp {
 // and imaginary parts at once with two barriers per exchange instead of
 // four, and half the (symmetric) window in LDS to keep 80 KiB and two
 // workgroups per CU: 3.10-3.17 against 2.83 ms.)
-// Also measured and not kept: the window folded into pass 0's first radix-2
+// Also measured and not kept: E = 8 (4 passes of radix 8, 512 threads,
+// 116 VGPRs, four waves per SIMD; XOR exchange slots, table twiddles):
+// 3.18-3.29 against 2.76 ms. And the window folded into pass 0's first radix-2
 // stage as FMAs (w_j z_j +- w_(j+8) z_(j+8): 16 fewer FP64 instructions per
 // thread and pair), 2.92 against 2.74 ms — the weights stay live in 32 more
 // registers through the first DFT.
