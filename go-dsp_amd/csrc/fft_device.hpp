@@ -146,6 +146,91 @@ __device__ __forceinline__ cd rot32(cd x, int m) {
   return {x.x * c + x.y * s, x.y * c - x.x * s};
 }
 
+// x * W_32^m for a constant m as scale * u(x), with u(x) = (x.x + r x.y,
+// x.y - r x.x) (form 1, |cos| >= |sin|: r = tan) or (r x.x + x.y,
+// r x.y - x.x) (form 2: r = cot): two FMAs, and the scale folds into the
+// add that follows (Linzer-Feig). Not for multiples of 8 (free rotations).
+#define GDSP_T16 0.19891236737965800691
+#define GDSP_T8 0.41421356237309504880
+#define GDSP_T316 0.66817863791929891999
+struct RotF {
+  int form;
+  double scale, r;
+};
+__device__ __forceinline__ constexpr RotF rotf(int m) {
+  switch (m & 31) {
+    case 1: return {1, GDSP_C16, GDSP_T16};
+    case 2: return {1, GDSP_C8, GDSP_T8};
+    case 3: return {1, GDSP_C316, GDSP_T316};
+    case 4: return {2, GDSP_R2, 1.0};
+    case 5: return {2, GDSP_C316, GDSP_T316};
+    case 6: return {2, GDSP_C8, GDSP_T8};
+    case 7: return {2, GDSP_C16, GDSP_T16};
+    case 9: return {2, GDSP_C16, -GDSP_T16};
+    case 10: return {2, GDSP_C8, -GDSP_T8};
+    case 11: return {2, GDSP_C316, -GDSP_T316};
+    case 12: return {1, -GDSP_R2, -1.0};
+    case 13: return {1, -GDSP_C316, -GDSP_T316};
+    case 14: return {1, -GDSP_C8, -GDSP_T8};
+    case 15: return {1, -GDSP_C16, -GDSP_T16};
+    case 17: return {1, -GDSP_C16, GDSP_T16};
+    case 18: return {1, -GDSP_C8, GDSP_T8};
+    case 19: return {1, -GDSP_C316, GDSP_T316};
+    case 20: return {1, -GDSP_R2, 1.0};
+    case 21: return {2, -GDSP_C316, GDSP_T316};
+    case 22: return {2, -GDSP_C8, GDSP_T8};
+    case 23: return {2, -GDSP_C16, GDSP_T16};
+    case 25: return {2, -GDSP_C16, -GDSP_T16};
+    case 26: return {2, -GDSP_C8, -GDSP_T8};
+    case 27: return {2, -GDSP_C316, -GDSP_T316};
+    case 28: return {2, -GDSP_R2, -1.0};
+    case 29: return {1, GDSP_C316, -GDSP_T316};
+    case 30: return {1, GDSP_C8, -GDSP_T8};
+    case 31: return {1, GDSP_C16, -GDSP_T16};
+    default: return {0, 0.0, 0.0};
+  }
+}
+
+// p = a + W_32^m b, q = a - W_32^m b (m a compile-time constant after
+// unrolling): six FMAs for a nontrivial rotation instead of a complex
+// multiply and four adds (eight instructions)
+__device__ __forceinline__ void fused_pm(cd a, cd b, int m, cd &p, cd &q) {
+  m &= 31;
+  if ((m & 7) == 0) {
+    const cd wb = rot16(b, m >> 1);
+    p = a + wb;
+    q = a - wb;
+    return;
+  }
+  const RotF f = rotf(m);
+  const cd u = f.form == 1 ? cd{fma(f.r, b.y, b.x), fma(-f.r, b.x, b.y)}
+                           : cd{fma(f.r, b.x, b.y), fma(f.r, b.y, -b.x)};
+  p = {fma(f.scale, u.x, a.x), fma(f.scale, u.y, a.y)};
+  q = {fma(-f.scale, u.x, a.x), fma(-f.scale, u.y, a.y)};
+}
+
+// The second stage of an R1 x R2 split (R2 = 2 or 4) with its twiddles
+// W_R^(n2 k1) folded into the butterflies (fused_pm): y[n2] are the first
+// stage's outputs k1 before rotation, s = 32 / R; out[k2] = sum_n2
+// W_R^(n2 k1) y[n2] W_R2^(n2 k2).
+template <int R2>
+__device__ __forceinline__ void dft_rot_stage(const cd (&y)[R2], int k1, int s, cd (&out)[R2]) {
+  if constexpr (R2 == 2) {
+    fused_pm(y[0], y[1], k1 * s, out[0], out[1]);
+  } else {
+    static_assert(R2 == 4, "fused second stage for R2 = 2 or 4");
+    cd t0, t1, t2, d;
+    fused_pm(y[0], y[2], 2 * k1 * s, t0, t1);
+    const cd y1 = rot32(y[1], k1 * s);
+    fused_pm(y1, y[3], 3 * k1 * s, t2, d);
+    const cd t3 = {d.y, -d.x};  // (a1 - a3) * (-i)
+    out[0] = t0 + t2;
+    out[1] = t1 + t3;
+    out[2] = t0 - t2;
+    out[3] = t1 - t3;
+  }
+}
+
 // In-register forward DFT of size R (natural order in, natural order out).
 template <int R>
 struct Dft;
@@ -177,7 +262,8 @@ struct Dft<4> {
   }
 };
 
-// R = R1*R2 split: n = R2*n1 + n2, k = k1 + R1*k2.
+// R = R1*R2 split: n = R2*n1 + n2, k = k1 + R1*k2; the twiddles between the
+// stages fold into the second stage's butterflies (dft_rot_stage).
 template <int R1, int R2>
 __device__ __forceinline__ void dft_split(cd (&a)[R1 * R2]) {
   constexpr int R = R1 * R2;
@@ -189,16 +275,16 @@ __device__ __forceinline__ void dft_split(cd (&a)[R1 * R2]) {
     for (int n1 = 0; n1 < R1; ++n1) tmp[n1] = a[R2 * n1 + n2];
     Dft<R1>::run(tmp);
 #pragma unroll
-    for (int k1 = 0; k1 < R1; ++k1) y[n2][k1] = rot32(tmp[k1], n2 * k1 * (32 / R));
+    for (int k1 = 0; k1 < R1; ++k1) y[n2][k1] = tmp[k1];
   }
 #pragma unroll
   for (int k1 = 0; k1 < R1; ++k1) {
-    cd tmp[R2];
+    cd col[R2], out[R2];
 #pragma unroll
-    for (int n2 = 0; n2 < R2; ++n2) tmp[n2] = y[n2][k1];
-    Dft<R2>::run(tmp);
+    for (int n2 = 0; n2 < R2; ++n2) col[n2] = y[n2][k1];
+    dft_rot_stage<R2>(col, k1, 32 / R, out);
 #pragma unroll
-    for (int k2 = 0; k2 < R2; ++k2) a[k1 + R1 * k2] = tmp[k2];
+    for (int k2 = 0; k2 < R2; ++k2) a[k1 + R1 * k2] = out[k2];
   }
 }
 
@@ -240,7 +326,7 @@ struct SplitZCol {
       } else {
         DftZ<R1, C>::run(tmp);
 #pragma unroll
-        for (int k1 = 0; k1 < R1; ++k1) y[N2][k1] = rot32(tmp[k1], N2 * k1 * (32 / (R1 * R2)));
+        for (int k1 = 0; k1 < R1; ++k1) y[N2][k1] = tmp[k1];
       }
       SplitZCol<R1, R2, NZ, N2 + 1>::run(a, y);
     }
@@ -249,16 +335,17 @@ struct SplitZCol {
 
 template <int R1, int R2, int NZ>
 __device__ __forceinline__ void dft_split_z(cd (&a)[R1 * R2]) {
+  static_assert(NZ >= R2, "every first-stage column holds an input");
   cd y[R2][R1];
   SplitZCol<R1, R2, NZ>::run(a, y);
 #pragma unroll
   for (int k1 = 0; k1 < R1; ++k1) {
-    cd tmp[R2];
+    cd col[R2], out[R2];
 #pragma unroll
-    for (int n2 = 0; n2 < R2; ++n2) tmp[n2] = y[n2][k1];
-    Dft<R2>::run(tmp);
+    for (int n2 = 0; n2 < R2; ++n2) col[n2] = y[n2][k1];
+    dft_rot_stage<R2>(col, k1, 32 / (R1 * R2), out);
 #pragma unroll
-    for (int k2 = 0; k2 < R2; ++k2) a[k1 + R1 * k2] = tmp[k2];
+    for (int k2 = 0; k2 < R2; ++k2) a[k1 + R1 * k2] = out[k2];
   }
 }
 
