@@ -1060,7 +1060,10 @@ static hipError_t launch_blu_t(const cd *in, cd *out, int64_t n, int64_t batch, 
   // M = 8192 / 16384: 32 points per thread (three passes, two exchanges, one
   // twiddle stage fewer; 254 VGPRs, 2 waves per SIMD) beat 16 (four passes,
   // 124 VGPRs, 4 waves per SIMD): chirp-z 3000 3.44 against 3.56 ms, primes
-  // 4099..8191 (M = 16384) 2-5 % (GDSP_BLU_E16=1 to compare)
+  // 4099..8191 (M = 16384) 2-5 % (GDSP_BLU_E16=1 to compare). The 32 points
+  // alone hold 128 VGPRs, so a third wave per SIMD is out of reach: with the
+  // exchange through half-size buffers (34 KiB of LDS) and 168 VGPRs the
+  // kernel spills 206 registers, 6.20 against 2.62 ms (scripts/gpu_r03_occ.sh)
   if constexpr (LOG2M == 13 || LOG2M == 14) {
     static const bool e32 = dev_switch("GDSP_BLU_E16") == nullptr;
     if (e32) {
