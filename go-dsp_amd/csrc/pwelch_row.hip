@@ -40,6 +40,12 @@ namespace gdsp {
 // stage as FMAs (w_j z_j +- w_(j+8) z_(j+8): 16 fewer FP64 instructions per
 // thread and pair), 2.92 against 2.74 ms — the weights stay live in 32 more
 // registers through the first DFT.
+// And for a third wave per SIMD (scripts/gpu_r03_occ.sh): the exchange through
+// a buffer of half a transform (each component in two rounds, 17 KiB: three
+// workgroups per CU by LDS) with the VGPRs capped at 168 spills 106-186
+// registers, 5.95 ms without the next pair's samples in flight (touching its
+// lines one pair ahead instead), 10.4 with them; without them at two waves,
+// 3.02 against 2.73-2.77 ms.
 template <int LOG2F, int LOG2E = 4, bool REGTW = true, int LAYOUT = 2>
 __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_row_kernel(
     const double *__restrict__ x, int64_t seg_begin, int64_t seg_end, int64_t pairs_per_worker,
