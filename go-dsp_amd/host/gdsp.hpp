@@ -294,6 +294,21 @@ inline std::vector<complex> FFTBatchMulti(const std::vector<complex> &x, size_t 
   return r;
 }
 
+// How the split calls went (gdsp_multi_stats).
+struct MultiStats {
+  int64_t batch_calls = 0, pwelch_calls = 0, rccl_reduces = 0, host_reduces = 0;
+};
+inline MultiStats GetMultiStats() {
+  MultiStats m;
+  check(gdsp_multi_stats(&m.batch_calls, &m.pwelch_calls, &m.rccl_reduces, &m.host_reduces),
+        "MultiStats");
+  return m;
+}
+
+// Algorithm selection (gdsp_fft.h GDSP_ALGO_*; no reference equivalent).
+inline void SetAlgorithm(unsigned flags) { check(gdsp_set_algorithm(flags), "SetAlgorithm"); }
+inline unsigned Algorithm() { return gdsp_get_algorithm(); }
+
 inline void SetWorkerPoolSize(int n) { gdsp_set_worker_pool_size(n); }  // fft.go:95-101
 inline void EnsureRadix2Factors(int input_len) {                        // radix2.go:35-37
   check(gdsp_ensure_plan(input_len), "EnsureRadix2Factors");

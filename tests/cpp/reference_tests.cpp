@@ -45,6 +45,11 @@ int main(int argc, char **argv) {
     std::cerr << "usage: reference_tests vectors.txt\n";
     return 2;
   }
+  // the additive entries: algorithm selection round trip, split-call counters
+  fft::SetAlgorithm(GDSP_ALGO_CHIRPZ_POW2);
+  EXPECT(fft::Algorithm() == GDSP_ALGO_CHIRPZ_POW2, "SetAlgorithm");
+  fft::SetAlgorithm(GDSP_ALGO_DEFAULT);
+  EXPECT(fft::GetMultiStats().batch_calls >= 0, "MultiStats");
   std::ifstream f(argv[1]);
   std::string line;
   while (std::getline(f, line)) {

@@ -175,3 +175,31 @@ def test_ifft2_of_empty_rows_panics(gdsp):
     assert L.gdsp_fft2(p, p, 3, 0, 0) == gdsp._lib.GDSP_OK
     assert L.gdsp_fft2(p, p, 3, 0, 1) == gdsp._lib.GDSP_ERR_EMPTY
     assert L.gdsp_fft2_real(p, p, 3, 0, 1) == gdsp._lib.GDSP_ERR_EMPTY
+
+
+def test_algorithm_selection_flags(gdsp):
+    """gdsp_set_algorithm: known flags are kept, unknown bits are rejected and
+    leave the selection unchanged (no device needed)."""
+    F = gdsp.fft
+    prev = F.Algorithm()
+    try:
+        F.SetAlgorithm(F.ALGO_GENERIC_MIXED | F.ALGO_CHIRPZ_POW2)
+        assert F.Algorithm() == F.ALGO_GENERIC_MIXED | F.ALGO_CHIRPZ_POW2
+        with pytest.raises(gdsp.GDSPError) as e:
+            F.SetAlgorithm(1 << 20)
+        assert e.value.status == gdsp._lib.GDSP_ERR_INVALID
+        assert F.Algorithm() == F.ALGO_GENERIC_MIXED | F.ALGO_CHIRPZ_POW2
+        F.SetAlgorithm(F.ALGO_DEFAULT)
+        assert F.Algorithm() == 0
+    finally:
+        F.SetAlgorithm(prev)
+
+
+def test_multi_stats_readable_without_gpu(gdsp):
+    """gdsp_multi_stats reads the split-call counters; without a GPU no call
+    can have been split."""
+    s = gdsp.fft.MultiStats()
+    assert set(s) == {"batch_calls", "pwelch_calls", "rccl_reduces", "host_reduces"}
+    assert all(v >= 0 for v in s.values())
+    if gdsp.device_count() == 0:
+        assert all(v == 0 for v in s.values())
