@@ -256,7 +256,8 @@ constexpr int kBluPfShift = 7;  // touch granularity: one load per 2^7 bytes (a 
 // pass 0 of FFT 1 adds no zeros and the last pass of FFT 2 forms only the
 // outputs below KN T (0: KN = E/2, what n <= M/2 guarantees for any n).
 template <int LOG2M, bool INV, bool SPLIT, int LOG2E = 4, bool PARTS = false, int KN = 0>
-__global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG)) void bluestein_kernel(
+__global__ __launch_bounds__((Geo<LOG2M, LOG2E>::WG))
+__attribute__((amdgpu_waves_per_eu(LOG2M >= 13 && LOG2E == 4 ? 4 : 1))) void bluestein_kernel(
     const cd *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
     const cd *__restrict__ twm, const cd *__restrict__ chirp, const cd *__restrict__ bhat,
     double scale, int64_t kpart, int nparts) {
@@ -1060,7 +1061,10 @@ static hipError_t launch_blu_t(const cd *in, cd *out, int64_t n, int64_t batch, 
   // M = 8192 / 16384: 32 points per thread (three passes, two exchanges, one
   // twiddle stage fewer; 254 VGPRs, 2 waves per SIMD) beat 16 (four passes,
   // 124 VGPRs, 4 waves per SIMD): chirp-z 3000 3.44 against 3.56 ms, primes
-  // 4099..8191 (M = 16384) 2-5 % (GDSP_BLU_E16=1 to compare). The 32 points
+  // 4099..8191 (M = 16384) 2-5 % (GDSP_BLU_E16=1 to compare); round 3, with
+  // the 16-point kernel held to 128 VGPRs (amdgpu_waves_per_eu: at 130 it ran
+  // one 512-thread block per CU, 4.37 ms) and n-aware pruning (KN = 6):
+  // 3.27-3.34 against 2.80 ms (scripts/gpu_r03_e16.sh). The 32 points
   // alone hold 128 VGPRs, so a third wave per SIMD is out of reach: with the
   // exchange through half-size buffers (34 KiB of LDS) and 168 VGPRs the
   // kernel spills 206 registers, 6.20 against 2.62 ms (scripts/gpu_r03_occ.sh)
