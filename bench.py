@@ -14,7 +14,7 @@ The default run also times the other BASELINE configs and nests them under
 rows sharded with two RCCL all-to-alls at N > 1) and pwelch (configs[4]; one
 RCCL all-reduce of the PSD accumulators). --workload X runs one alone.
 bluestein3000 is fft.FFT of N = 3000 through the production dispatch (the
-mixed-radix 8*5*5*5*3 kernel); chirpz3000 times the same workload through the
+compiled mixed-radix 25*15*8 kernel); chirpz3000 times the same workload through the
 reference's algorithm (forced Bluestein plan, gdsp_plan_create_chirpz).
 
 roofline.achieved = algorithmic bytes of one launch (32 B/sample: 16 B read +
@@ -140,7 +140,7 @@ def setup(w: str, c: Ctx, weak: bool = False) -> dict:
             D.fft_batch(x, y, stream=stream, chirpz=chirpz)
 
         algo = {1: "Stockham radix-16 (one kernel)", 3: "Bluestein chirp-z (fused, M=8192)",
-                5: "mixed-radix Stockham 8*5*5*5*3 (one kernel)"}.get(kind, str(kind))
+                5: "mixed-radix Stockham 25*15*8 (one compiled kernel)"}.get(kind, str(kind))
         kernel = {1: "fft_lds_kernel<12>", 3: "bluestein_kernel<13>",
                   5: "fft_mixed_fixed_kernel<25,15,8>"}.get(kind, str(kind))
         return dict(step=step, x=x, y=y, total_samples=total * n, rank_samples=(hi - lo) * n,
