@@ -685,8 +685,18 @@ __global__ void reduce_partials_l1(const double *__restrict__ partial, int64_t n
   if (k >= F) return;
   const int64_t w0 = c * kReduceChunk;
   const int64_t w1 = w0 + kReduceChunk < nworkers ? w0 + kReduceChunk : nworkers;
+  const double *p = partial + w0 * F + k;
   double s = 0.0;
-  for (int64_t w = w0; w < w1; ++w) s += partial[w * F + k];
+  if (w1 - w0 == kReduceChunk) {
+    // a full chunk: every load in flight at once, the sum in the same order
+    double v[kReduceChunk];
+#pragma unroll
+    for (int i = 0; i < kReduceChunk; ++i) v[i] = p[i * F];
+#pragma unroll
+    for (int i = 0; i < kReduceChunk; ++i) s += v[i];
+  } else {
+    for (int64_t w = w0; w < w1; ++w, p += F) s += *p;
+  }
   chunk_sums[c * F + k] = s;
 }
 
@@ -695,7 +705,15 @@ __global__ void reduce_partials_l2(const double *__restrict__ chunk_sums, int64_
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= F) return;
   double s = 0.0;
-  for (int64_t c = 0; c < nchunks; ++c) s += chunk_sums[c * F + k];
+  int64_t c = 0;
+  for (; c + 8 <= nchunks; c += 8) {  // eight loads in flight, summed in order
+    double v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = chunk_sums[(c + i) * F + k];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += v[i];
+  }
+  for (; c < nchunks; ++c) s += chunk_sums[c * F + k];
   acc[k] += s;
 }
 
