@@ -503,8 +503,14 @@ __device__ __forceinline__ cd opaque_cd(cd w) {
 // WPRE: the butterflies' twiddle bases come in wpre[b] (loaded by the caller
 // a pass ahead: fft_regs PREW) instead of being read here
 // PASS: this pass's index (selects a RegTw's base)
+// CHEB: the powers w^3 .. w^(R-1) by the three-term recurrence
+// w^(r+2) = 2 cos(2 theta) w^r - w^(r-2) (two FMAs each) instead of complex
+// products (four instructions each); its error grows with the chain length
+// (numpy model, largest over the bases: 2.3e-15 at R = 8, 4-10e-15 at
+// R = 16, 2e-14 at R = 32 against 1-3e-15 for the products), so callers ask
+// for it up to radix 16
 template <int N, int E, int T, int R, int NS, int ZIN = 0, class EPI = NoEpi,
-          bool WPRE = false, int PASS = 0, class TWP = const cd *>
+          bool WPRE = false, int PASS = 0, class TWP = const cd *, bool CHEB = false>
 __device__ __forceinline__ void pass_compute(cd (&v)[E], int t, TWP tw,
                                              const EPI &epi = EPI(), const cd *wpre = nullptr) {
   constexpr int B = E / R;
@@ -530,7 +536,27 @@ __device__ __forceinline__ void pass_compute(cd (&v)[E], int t, TWP tw,
         w = tw.base[PASS];
       } else w = pass_base<N, R, NS>(tw, j);
       u[1] = cmul(u[1], w);
-      if constexpr (R > 2) {
+      if constexpr (R > 2 && CHEB) {
+        const cd w2 = cmul(w, w);
+        u[2] = cmul(u[2], w2);
+        const double c2 = w2.x + w2.x;
+        cd om = conjg(w), o = w;      // odd powers: w^(r-2), w^r
+        cd em = {1.0, 0.0}, e = w2;   // even powers
+#pragma unroll
+        for (int r = 3; r < R; ++r) {
+          if (r & 1) {
+            const cd n = {fma(c2, o.x, -om.x), fma(c2, o.y, -om.y)};
+            om = o;
+            o = n;
+            u[r] = cmul(u[r], o);
+          } else {
+            const cd n = {fma(c2, e.x, -em.x), fma(c2, e.y, -em.y)};
+            em = e;
+            e = n;
+            u[r] = cmul(u[r], e);
+          }
+        }
+      } else if constexpr (R > 2) {
         const cd w2 = cmul(w, w);
         cd wo = w, we = w2;
         u[2] = cmul(u[2], w2);
@@ -735,13 +761,15 @@ using RegArr = cd[Geo<LOG2N, LOG2E>::E];
 // entry (pass 0 prunes one radix-2 stage and the additions of zeros;
 // pass_compute)
 // EPI: the last pass's epilogue (pass_compute)
+// CHEBR: passes of radix <= CHEBR take their twiddle powers by the
+// three-term recurrence (pass_compute CHEB; 0: none)
 // PREW: each pass's twiddle bases are read before the previous pass's
 // arithmetic and exchange (wpre carries them down), so their L1/L2 or LDS
 // latency hides behind that work instead of opening the pass; only for
 // passes with at most PREW bases per thread (0: off)
 template <int LOG2N, bool SPLIT, int OPAQUE = 0, int LOG2E = 4, int ILV = 0, int P = 0,
           class TWP = const cd *, int LINEAR = 0, int HALF_IN = 0, class EPI = NoEpi,
-          int PREW = 0>
+          int PREW = 0, int CHEBR = 0>
 __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw, double *lre,
                                          double *lim, bool first_exchange = true,
                                          const EPI &epi = EPI(), const cd *wpre = nullptr) {
@@ -770,13 +798,14 @@ __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw,
       for (int b = 0; b < BN; ++b) wn[b] = pass_base<G::N, RN, NSN>(tw, t + b * G::T);
     }
     constexpr bool USE_PRE = PREW >= G::E / R && P > 0 && NS > 1;
+    constexpr bool CH = R <= CHEBR;
     if constexpr (P == G::NPASS - 1)
-      pass_compute<G::N, G::E, G::T, R, NS, P == 0 ? HALF_IN : 0, EPI, USE_PRE, P, TWP>(v, t, tw, epi,
-                                                                                    wpre);
+      pass_compute<G::N, G::E, G::T, R, NS, P == 0 ? HALF_IN : 0, EPI, USE_PRE, P, TWP, CH>(
+          v, t, tw, epi, wpre);
     else
-      pass_compute<G::N, G::E, G::T, R, NS, P == 0 ? HALF_IN : 0, NoEpi, USE_PRE, P, TWP>(
+      pass_compute<G::N, G::E, G::T, R, NS, P == 0 ? HALF_IN : 0, NoEpi, USE_PRE, P, TWP, CH>(
           v, t, tw, NoEpi(), wpre);
-    fft_regs<LOG2N, SPLIT, 0, LOG2E, ILV, P + 1, TWP, LINEAR, false, EPI, PREW>(
+    fft_regs<LOG2N, SPLIT, 0, LOG2E, ILV, P + 1, TWP, LINEAR, false, EPI, PREW, CHEBR>(
         v, t, tw, lre, lim, first_exchange, epi, PRE_NEXT ? wn : nullptr);
   }
 }

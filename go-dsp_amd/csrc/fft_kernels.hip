@@ -248,6 +248,12 @@ __host__ __device__ constexpr int blu_epi_mode(int log2m, int log2e) {
 // touch the same slot's row kBluPf blocks on: primes 13..1021 10-22 %
 // faster (scripts/dev/blu_pfall_ab.sh)
 constexpr int kBluPf = 16;
+// Twiddle powers of the radix-8 passes by the three-term recurrence
+// (pass_compute CHEB; one transform per workgroup): chirpz3000 2.65-2.67
+// against 2.71-2.74 ms, parity 1.58e-15 against 1.56e-15 vs the oracle. The
+// radix-32 passes keep complex products: the recurrence there bought 0.3 %
+// for 5.5e-15 (scripts/gpu_r03_cheb.sh)
+constexpr int kBluChebR = 8;
 constexpr int kBluPf14 = 4;     // M = 16384, one block per CU: 2-4 % faster than 8 or 16
 constexpr int kBluPfParts = 2;  // PARTS: the row's part-0 block touches 2 rows on
 constexpr int kBluPfShift = 7;  // touch granularity: one load per 2^7 bytes (a line)
@@ -335,12 +341,13 @@ __attribute__((amdgpu_waves_per_eu(LOG2M >= 13 && LOG2E == 4 ? 4 : 1))) void blu
     }
     const BhatBufEpi<G::T> be{make_rsrc(bhat, (int64_t)G::N * 16), off};
     fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, ZIN, BhatBufEpi<G::T>,
-             blu_prew(LOG2M)>(v, t, twm, lre, lim, true, be);
+             blu_prew(LOG2M), kBluChebR>(v, t, twm, lre, lim, true, be);
     const ChirpOutBufEpi<G::T, KH, INV> oe{make_rsrc(opaque_ptr(chirp), rowb),
                                            make_rsrc(out + gu * n, rowb), (uint32_t)opaque_int(t) * 16u,
                                            scale};
     fft_regs<LOG2M, SPLIT, true, LOG2E, 0, 0, const cd *, true, false,
-             ChirpOutBufEpi<G::T, KH, INV>, blu_prew(LOG2M)>(v, t, twm, lre, lim, false, oe);
+             ChirpOutBufEpi<G::T, KH, INV>, blu_prew(LOG2M), kBluChebR>(v, t, twm, lre,
+                                                                                 lim, false, oe);
     return;
   }
   const cd *src = in + g * n;

@@ -27,6 +27,9 @@ namespace gdsp {
 //    powers from an LDS table instead of each pair's chain measured slower
 //    (2.99-3.01 against 2.86-2.87 ms: LDS, not the vector unit, is the
 //    scarcer resource here);
+//  - the twiddle powers of both twiddled passes by the three-term recurrence
+//    (pass_compute CHEB: two FMAs per power instead of a complex product):
+//    2.70-2.72 against 2.75-2.82 ms, parity 1.58e-15 against 1.16e-15;
 //  - LAYOUT 2 exchange slots (fft_device.hpp): every LDS address a per-thread
 //    base plus a compile-time offset (2.81-2.84 against 2.94-2.97 ms with
 //    XOR-swizzled slots throughout).
@@ -121,7 +124,8 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_row_kernel(
 #pragma unroll
     for (int k = 0; k < E; ++k) v[k] = {v[k].x * wv[k], v[k].y * wv[k]};
     if constexpr (REGTW)
-      fft_regs<LOG2F, true, 2, LOG2E, 0, 0, RT, LAYOUT, false, NoEpi, 0>(v, tt, rl, lx, lx, first);
+      fft_regs<LOG2F, true, 2, LOG2E, 0, 0, RT, LAYOUT, false, NoEpi, 0, 16>(v, tt, rl, lx, lx,
+                                                                          first);
     else
       fft_regs<LOG2F, true, 1, LOG2E, 0, 0, const cd *, LAYOUT>(v, tt, tw, lx, lx, first);
 #pragma unroll
