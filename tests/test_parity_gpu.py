@@ -352,7 +352,9 @@ def test_mixed_radix_vs_oracle(gdsp, oracle, n):
     assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
 
 
-@pytest.mark.parametrize("n", [3, 5, 100, 3000, 4097, 10000])
+# 2049 .. 3072: M = 8192 with the n-aware pruning (n <= 12 T), 3073 and 4093
+# the same M without it
+@pytest.mark.parametrize("n", [3, 5, 100, 2049, 3000, 3072, 3073, 4093, 4097, 10000])
 def test_chirpz_plan_vs_oracle(gdsp, oracle, n):
     # the reference's own algorithm (Bluestein) on the device API, against the
     # oracle and against the default plan for the same length
