@@ -53,6 +53,9 @@ unsigned algo_flags();
 
 hipError_t launch_fft_lds(int log2n, bool inv, int load, bool split, const void *in, cd *out,
                           int64_t batch, const cd *tw, double scale, hipStream_t s);
+// the N = 4096 case of launch_fft_lds (fft_lds12.hip)
+hipError_t launch_fft_lds12(bool inv, int load, bool split, const void *in, cd *out, int64_t batch,
+                            const cd *tw, double scale, hipStream_t s);
 // fused Pwelch over a mixed-radix segment length d.n = max(pad, nfft) with
 // d.npass >= 2 (fft_mixed.hip); same partial layout as launch_pwelch
 hipError_t launch_pwelch_mixed(const MixedDesc &d, const double *x, int64_t nfft, int64_t stride,
