@@ -43,7 +43,7 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (tools/fp64peak.hip measures 
 # kernels whose FP64 work is taken from the committed SQ counter passes
 # (profiles/r02/sq_counters.json: 64 x (2 FMA + ADD + MUL) F64 instructions)
 SQ_KERNELS = {"radix4096": ["fft_lds_kernel<12"], "bluestein3000": ["fft_mixed_fixed_kernel"],
-              "chirpz3000": ["bluestein_kernel<13"], "pwelch": ["pwelch_row_kernel<12"],
+              "chirpz3000": ["chirpz6k_kernel"], "pwelch": ["pwelch_row_kernel<12"],
               "fft2_8192": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"],
               "fft2_dist": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"]}
 SQ_ROUNDS = ("r03", "r02")  # SQ counter passes quoted: the newest round that has the kernel
@@ -134,7 +134,8 @@ def setup(w: str, c: Ctx, weak: bool = False) -> dict:
         x = torch.empty((hi - lo, n), dtype=torch.complex128, device=dev)
         y = torch.empty_like(x)
         D.fill_uniform(x, SEED, offset=lo * n * 2, stream=stream)
-        kind = D.plan(n, chirpz).kind
+        p = D.plan(n, chirpz)
+        kind = p.kind
 
         def step():
             D.fft_batch(x, y, stream=stream, chirpz=chirpz)
@@ -143,6 +144,11 @@ def setup(w: str, c: Ctx, weak: bool = False) -> dict:
                 5: "mixed-radix Stockham 25*15*8 (one compiled kernel)"}.get(kind, str(kind))
         kernel = {1: "fft_lds_kernel<12>", 3: "bluestein_kernel<13>",
                   5: "fft_mixed_fixed_kernel<25,15,8>"}.get(kind, str(kind))
+        if kind == 3 and p.m == 6144:
+            # 2049 <= n <= 3072: the convolution on M = 6144 (chirpz6k.hip);
+            # bluestein.go:70 pads to 8192 (GDSP_ALGO_CHIRPZ_POW2 keeps it)
+            algo = "Bluestein chirp-z (fused, M=6144=16*24*16; the reference pads to 8192)"
+            kernel = "chirpz6k_kernel"
         return dict(step=step, x=x, y=y, total_samples=total * n, rank_samples=(hi - lo) * n,
                     alg_bytes=32 * (hi - lo) * n, kernel=kernel, metric=HEADLINE_METRIC,
                     scaling="weak" if weak else "strong",
@@ -513,7 +519,11 @@ def run(w: str, c: Ctx, weak: bool = False) -> dict:
     pmc = os.path.join(REPO, "profiles", f"pmc_{w}.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
-            t = json.load(f).get("hbm_bytes_per_launch")
+            pj = json.load(f)
+        t = pj.get("hbm_bytes_per_launch")
+        pk = pj.get("kernel")
+        if isinstance(pk, str) and not wl["kernel"].startswith(pk):
+            t = None  # profiled on another kernel than the one timed here
         traffic = None if t is None else int(round(t * share))
     out = {
         "metric": wl["metric"],
@@ -533,6 +543,25 @@ def run(w: str, c: Ctx, weak: bool = False) -> dict:
         "cpu_baseline": None,  # filled in by main() after every GPU measurement
         "parity": check,
     }
+    if w == "chirpz3000" and not weak and wl["kernel"] == "chirpz6k_kernel":
+        # the same workload on the reference's convolution length M = 8192
+        # (bluestein.go:70; GDSP_ALGO_CHIRPZ_POW2), timed the same way
+        F = c.gdsp.fft
+        del wl
+        F.SetAlgorithm(F.ALGO_CHIRPZ_POW2)
+        try:
+            w8 = setup(w, c)
+            m8 = measure(w8, c)
+        finally:
+            F.SetAlgorithm(F.ALGO_DEFAULT)
+        out["reference_m8192"] = {
+            "kernel": w8["kernel"], "algorithm": w8["cfg"]["algorithm"],
+            "ms_per_step": round(m8["elapsed"] / args.steps * 1e3, 4),
+            "avg_launch_ms": round(m8["avg_launch_s"] * 1e3, 4),
+            "frac": round(w8["alg_bytes"] / m8["avg_launch_s"] / 1e9 / HBM_PEAK_GBS, 4)}
+        del w8
+        c.torch.cuda.empty_cache()
+        return out
     if c.rank == 0 and w == "fft_2p20":
         # fft.FFT on a host vector, the way BenchmarkFFT calls it: H2D +
         # transform + D2H through the C ABI's pinned staging (PCIe-inclusive;

@@ -342,6 +342,10 @@ struct gdsp_plan {
   // NextPowerOf2(2n-1) = 32768 exceeds one kernel runs as `parts` fused
   // convolutions of M = 16384, each giving kpart outputs; bhat holds parts * M
   int parts = 1;
+  // fused chirp-z on M = 6144 = 16*24*16 (chirpz6k.hip, 2049 <= n <= 3072,
+  // where bluestein.go:70 pads to 8192); tw6k: its pass twiddle bases
+  bool c6k = false;
+  cd *tw6k = nullptr;
   // composed chirp-z without its fused transposes (GDSP_ALGO_CHIRPZ_UNFUSED)
   bool unfused = false;
   int64_t kpart = 0;
@@ -743,6 +747,22 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
         break;
       }
     }
+  }
+  bool c6k_ok = !(gdsp::algo_flags() & GDSP_ALGO_CHIRPZ_POW2);
+#ifdef GDSP_DEV_BUILD
+  // the rejected M = 8192 / 2048 Q kernels, when switched on, keep their M
+  if (wave_chirpz_enabled() || shfl_chirpz_enabled()) c6k_ok = false;
+#endif
+  if (p->kind == KIND_BLUESTEIN && p->parts == 1 && gdsp::chirpz6k_fits(n) && c6k_ok) {
+    // 2049 <= n <= 3072: bluestein.go:70 pads the convolution to 8192; the
+    // smallest M >= 2n - 1 with a three-pass 16-point-per-thread split, 6144,
+    // gives the same linear convolution (and DFT) with a quarter fewer points
+    // at three waves per SIMD (chirpz6k.hip). GDSP_ALGO_CHIRPZ_POW2 keeps 8192.
+    p->m = 6144;
+    p->log2m = 0;
+    p->c6k = true;
+    gdsp::MixedDesc d6{};
+    STCHK(make_mixed_desc(dev, 6144, {16, 24, 16}, d6, &p->tw6k));
   }
   if (!p->mplan) STCHK(get_plan_locked(dev, p->m, &p->mplan));
   std::vector<cd> w((size_t)n), chirp((size_t)n),
@@ -1153,6 +1173,11 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
         HIPCHK(gdsp::launch_bluestein_parts(p->log2m, inv, src, out, p->n, batch, p->parts,
                                             p->kpart, p->mplan->tw, p->chirp, p->bhat, scale,
                                             s));
+        return GDSP_OK;
+      }
+      if (p->kind == KIND_BLUESTEIN && p->c6k) {
+        HIPCHK(gdsp::launch_chirpz6k(inv, src, out, p->n, batch, p->tw6k, p->chirp, p->bhat, scale,
+                                     s));
         return GDSP_OK;
       }
       if (p->kind == KIND_BLUESTEIN) {

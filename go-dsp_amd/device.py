@@ -62,7 +62,8 @@ _plans: dict = {}
 
 def plan(n: int, chirpz: bool = False) -> Plan:
     torch = _torch()
-    key = (torch.cuda.current_device(), int(n), bool(chirpz))
+    # the library caches plans per (device, n, algorithm flags): so does this
+    key = (torch.cuda.current_device(), int(n), bool(chirpz), int(lib().gdsp_get_algorithm()))
     if key not in _plans:
         _plans[key] = Plan(n, chirpz)
     return _plans[key]

@@ -352,8 +352,9 @@ def test_mixed_radix_vs_oracle(gdsp, oracle, n):
     assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
 
 
-# 2049 .. 3072: M = 8192 with the n-aware pruning (n <= 12 T), 3073 and 4093
-# the same M without it
+# 2049 .. 3072: the fused chirp-z on M = 6144 (chirpz6k.hip; with
+# GDSP_ALGO_CHIRPZ_POW2, M = 8192 with the n-aware pruning, n <= 12 T), 3073
+# and 4093 M = 8192 without pruning
 @pytest.mark.parametrize("n", [3, 5, 100, 2049, 3000, 3072, 3073, 4093, 4097, 10000])
 def test_chirpz_plan_vs_oracle(gdsp, oracle, n):
     # the reference's own algorithm (Bluestein) on the device API, against the
@@ -369,6 +370,65 @@ def test_chirpz_plan_vs_oracle(gdsp, oracle, n):
     assert row_nrel(yc, ref) < TOL and row_nrel(yd, ref) < TOL
     yci = D.fft_batch(xt, inverse=True, chirpz=True).cpu().numpy()
     assert row_nrel(yci, oracle.ifft_rows(x)) < TOL
+
+
+# M = 6144 (16 * 24 * 16) where bluestein.go:70 pads to 8192: the range's
+# ends, primes across it, and a length that is smooth (3072 = 2^10 * 3, the
+# mixed-radix kernel by default, chirp-z only when forced)
+C6K = [2049, 2053, 2307, 2729, 3000, 3001, 3067, 3071, 3072]
+
+
+@pytest.mark.parametrize("n", C6K)
+def test_chirpz6k_vs_oracle(gdsp, oracle, n):
+    import torch
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    F = __import__("importlib").import_module("go-dsp_amd.fft")
+    pc = D.plan(n, chirpz=True)
+    assert (pc.kind, pc.m) == (3, 6144), (n, pc.kind, pc.m)
+    rng = np.random.default_rng(6144 + n)
+    for batch in (1, 5):
+        x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
+        xt = torch.from_numpy(x).cuda()
+        ref = oracle.fft_rows(x)
+        assert row_nrel(D.fft_batch(xt, chirpz=True).cpu().numpy(), ref) < TOL
+        yi = D.fft_batch(xt, inverse=True, chirpz=True).cpu().numpy()
+        assert row_nrel(yi, oracle.ifft_rows(x)) < TOL
+    # host API (default plan: chirp-z for the primes, mixed radix when smooth)
+    x = rng.uniform(-1, 1, (3, n)) + 1j * rng.uniform(-1, 1, (3, n))
+    assert row_nrel(gdsp.fft.FFTBatch(x), oracle.fft_rows(x)) < TOL
+    xr = rng.uniform(-1, 1, (3, n))
+    assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
+    # the reference's M = 8192 on request (GDSP_ALGO_CHIRPZ_POW2), same results
+    F.SetAlgorithm(F.ALGO_CHIRPZ_POW2)
+    try:
+        assert D.plan(n, chirpz=True).m == 8192
+        y8 = D.fft_batch(xt, chirpz=True).cpu().numpy()
+    finally:
+        F.SetAlgorithm(0)
+    assert row_nrel(y8, ref) < TOL
+
+
+def test_chirpz6k_large_batch_properties(gdsp):
+    """A full-occupancy grid (65 536 rows of n = 3000, the BASELINE shape):
+    linearity and the forward/inverse round trip on every row, and eight rows
+    against a float64 direct DFT (numpy)."""
+    import torch
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    n, batch = 3000, 65536
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.complex(torch.rand(batch, n, dtype=torch.float64, device="cuda", generator=g) - 0.5,
+                      torch.rand(batch, n, dtype=torch.float64, device="cuda", generator=g) - 0.5)
+    y = D.fft_batch(x, chirpz=True)
+    z = D.fft_batch(y, inverse=True, chirpz=True)
+    err = ((z - x).abs().amax(dim=1) / x.abs().amax(dim=1)).max().item()
+    assert err < 1e-12, err
+    y2 = D.fft_batch(2.0 * x[:64] - 1j * x[64:128], chirpz=True)
+    lin = ((y2 - (2.0 * y[:64] - 1j * y[64:128])).abs().max() / y[:128].abs().max()).item()
+    assert lin < 1e-13, lin
+    rows = [0, 1, 777, 4096, 30000, 65534, 65535, 12345]
+    xs = x[rows].cpu().numpy()
+    ref = np.fft.fft(xs, axis=1)
+    assert row_nrel(y[rows].cpu().numpy(), ref) < TOL
 
 
 # smooth lengths beyond one kernel: four-step over one-kernel factors
