@@ -77,8 +77,9 @@ enum {
   /* primes in (8192, 14563] on the composed chirp-z instead of the
    * output-split fused kernel */
   GDSP_ALGO_NO_CHIRPZ_PARTS = 2,
-  /* the composed chirp-z on the reference's M = NextPowerOf2(2n-1)
-   * (fft/bluestein.go:70) instead of a smaller smooth M */
+  /* chirp-z on the reference's M = NextPowerOf2(2n-1) (fft/bluestein.go:70)
+   * instead of a smaller smooth M: the composed chirp-z, and the fused one
+   * for 2049 <= n <= 3072 (M = 6144 by default) */
   GDSP_ALGO_CHIRPZ_POW2 = 4,
   /* the composed chirp-z without its fused transposes */
   GDSP_ALGO_CHIRPZ_UNFUSED = 8
