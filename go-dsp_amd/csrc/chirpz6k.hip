@@ -221,9 +221,11 @@ __device__ __forceinline__ void c6_fft(cd (&v)[16], int t, const cd *__restrict_
 // beside the first's 2-2-1-1 placement and the kernel ran 3.13 against
 // 2.43 ms (profiles/r03/chirpz6k_ab.txt)
 // KN: n <= 384 KN (inputs and wanted outputs at r < KN)
-template <bool INV, int KN>
+// REAL: float64 input rows (fft.FFTReal, fft/fft.go:25-27), read directly
+// (no complex copy of the input first)
+template <bool INV, int KN, bool REAL = false>
 __global__ __launch_bounds__(kC6T) __attribute__((amdgpu_waves_per_eu(4))) void chirpz6k_kernel(
-    const cd *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
+    const void *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
     const cd *__restrict__ tw, const cd *__restrict__ chirp, const cd *__restrict__ bhat,
     double scale) {
   static_assert(KN >= 1 && KN <= 8, "n <= M/2");
@@ -233,14 +235,19 @@ __global__ __launch_bounds__(kC6T) __attribute__((amdgpu_waves_per_eu(4))) void 
   if (g >= batch) return;  // (grid = batch: never taken)
   const uint32_t off = (uint32_t)t * 16u;
   const int64_t rowb = n * 16;
-  const rsrc_t rin = make_rsrc(in + g * n, rowb);
+  const rsrc_t rin =
+      REAL ? make_rsrc(static_cast<const double *>(in) + g * n, n * 8)
+           : make_rsrc(static_cast<const cd *>(in) + g * n, rowb);
   const rsrc_t rch = make_rsrc(chirp, rowb);
   cd v[16];
   {
     cd xv[KN], cv[KN];
 #pragma unroll
     for (int r = 0; r < KN; ++r) {
-      xv[r] = buf_ld(rin, off + (uint32_t)(r * kC6T * 16));
+      if constexpr (REAL)
+        xv[r] = {buf_ld1(rin, (uint32_t)t * 8u + (uint32_t)(r * kC6T * 8)), 0.0};
+      else
+        xv[r] = buf_ld(rin, off + (uint32_t)(r * kC6T * 16));
       cv[r] = buf_ld(rch, off + (uint32_t)(r * kC6T * 16));
     }
 #pragma unroll
@@ -266,13 +273,17 @@ __global__ __launch_bounds__(kC6T) __attribute__((amdgpu_waves_per_eu(4))) void 
 
 bool chirpz6k_fits(int64_t n) { return n >= 2049 && 2 * n - 1 <= kC6M; }
 
-hipError_t launch_chirpz6k(bool inv, const cd *in, cd *out, int64_t n, int64_t batch,
+hipError_t launch_chirpz6k(bool inv, int load, const void *in, cd *out, int64_t n, int64_t batch,
                            const cd *tw, const cd *chirp, const cd *bhat, double scale,
                            hipStream_t s) {
-  if (!chirpz6k_fits(n) || batch < 0 || batch > 0x7fffffff) return hipErrorInvalidValue;
+  if (!chirpz6k_fits(n) || batch < 0 || batch > 0x7fffffff || (inv && load == LOAD_REAL))
+    return hipErrorInvalidValue;
   if (batch == 0) return hipSuccess;
   const dim3 grid((unsigned)batch), block(kC6T);
-  if (inv)
+  if (load == LOAD_REAL)
+    hipLaunchKernelGGL((chirpz6k_kernel<false, 8, true>), grid, block, 0, s, in, out, n, batch,
+                       tw, chirp, bhat, scale);
+  else if (inv)
     hipLaunchKernelGGL((chirpz6k_kernel<true, 8>), grid, block, 0, s, in, out, n, batch, tw, chirp,
                        bhat, scale);
   else

@@ -1140,6 +1140,12 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
       return exec_global(p, in, out, batch, inv, load, s);
     case KIND_BLUESTEIN:
     case KIND_BLUESTEIN_COMPOSED: {
+      if (p->kind == KIND_BLUESTEIN && p->c6k) {
+        // real input read by the kernel itself (no complex copy first)
+        HIPCHK(gdsp::launch_chirpz6k(inv, load, in, out, p->n, batch, p->tw6k, p->chirp, p->bhat,
+                                     scale, s));
+        return GDSP_OK;
+      }
       const cd *src = (const cd *)in;
       DevBuf tmp;
       if (load == gdsp::LOAD_REAL) {
@@ -1173,11 +1179,6 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
         HIPCHK(gdsp::launch_bluestein_parts(p->log2m, inv, src, out, p->n, batch, p->parts,
                                             p->kpart, p->mplan->tw, p->chirp, p->bhat, scale,
                                             s));
-        return GDSP_OK;
-      }
-      if (p->kind == KIND_BLUESTEIN && p->c6k) {
-        HIPCHK(gdsp::launch_chirpz6k(inv, src, out, p->n, batch, p->tw6k, p->chirp, p->bhat, scale,
-                                     s));
         return GDSP_OK;
       }
       if (p->kind == KIND_BLUESTEIN) {
