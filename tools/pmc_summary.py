@@ -13,7 +13,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {"radix4096": "fft_lds_kernel<12", "bluestein3000": "fft_mixed_fixed_kernel",
-           "chirpz3000": "bluestein_kernel<13",
+           "chirpz3000": "chirpz6k_kernel",
            "pwelch": "pwelch_row_kernel<12",
            # one FFT2 step = row pass + the two column-tile launches: summed
            "fft2_8192": ["fft_lds_kernel<13", "colfft_tile_kernel<7", "colfft_tile_kernel<6"],
