@@ -1,19 +1,21 @@
 // chirpz6k.hip — fused chirp-z (Bluestein, fft/bluestein.go:68-94) on the
-// convolution length M = 6144 = 16 * 24 * 16 for 2049 <= n <= 3072.
+// convolution length M = 16 * RB * 16 = 3 * 2^k: M = 6144 (RB = 24) for
+// 2049 <= n <= 3072 and M = 3072 (RB = 12) for 1025 <= n <= 1536.
 //
-// bluestein.go:70 pads the circular convolution to NextPowerOf2(2n - 1) =
-// 8192 for these n because its FFT is radix 2. Any M >= 2n - 1 gives the
-// same linear convolution, hence the same DFT; 6144 = 3 * 2^11 is a quarter
-// fewer points, and its exchange buffer (6144 doubles, 48 KiB) and a
-// 16-point-per-thread register set let two 384-thread workgroups share a CU
-// at three waves per SIMD, where the M = 8192 kernel (bluestein_kernel<13>,
-// 32 points per thread, 256 VGPRs) runs two.
+// bluestein.go:70 pads the circular convolution to NextPowerOf2(2n - 1)
+// (8192, 4096) for these n because its FFT is radix 2. Any M >= 2n - 1 gives
+// the same linear convolution, hence the same DFT; 3 * 2^k is a quarter fewer
+// points. At M = 6144 the exchange buffer (48 KiB) and a 16-point-per-thread
+// register set let two 384-thread workgroups share a CU at 128 VGPRs, where
+// the M = 8192 kernel (bluestein_kernel<13>, 32 points per thread, 256 VGPRs)
+// runs two 256-thread ones.
 //
-// One workgroup per transform, 384 threads (thread t):
-//   premultiply  a[t + 384 r] = x * conj(w), r < KN (n <= 384 KN; rest zero)
-//   FFT 1        pass A  R = 16, NS = 1:   DFT_16 of t + 384 r (pruned input)
-//                pass B  R = 24, NS = 16:  t < 256, inputs t + 256 r
-//                pass C  R = 16, NS = 384: outputs t + 384 r (natural order)
+// One workgroup per transform, T = max(M / 16, 256) threads (thread t):
+//   premultiply  a[t + NA r] = x * conj(w), r < KN (n <= NA KN; rest zero),
+//                NA = M / 16 (pass A and C butterflies)
+//   FFT 1        pass A  R = 16, NS = 1:      DFT_16 of t + NA r (pruned input)
+//                pass B  R = RB, NS = 16:     t < 256, inputs t + 256 r
+//                pass C  R = 16, NS = 16 RB:  outputs t + NA r (natural order)
 //   middle       v = conj(A * bhat) in registers: pass C's outputs are pass
 //                A's inputs of FFT 2, so no exchange between the two FFTs
 //   FFT 2        pass A, B, C again; the outputs r < KN are the wanted ones:
@@ -32,7 +34,13 @@ namespace gdsp {
 
 // (kernel and helpers outside an anonymous namespace, so profiler kernel
 // names read gdsp::chirpz6k_kernel<...>)
-constexpr int kC6M = 6144, kC6T = 384, kC6B = 256;  // points, threads, pass-B butterflies
+constexpr int kC6B = 256;  // pass-B butterflies (both sizes)
+template <int RB>
+struct C6Geo {
+  static constexpr int M = 256 * RB;               // points
+  static constexpr int NA = M / 16;                // pass A / C butterflies
+  static constexpr int T = NA > kC6B ? NA : kC6B;  // threads
+};
 
 // x * W_24^q (q a compile-time constant after unrolling)
 #define GDSP_C24 0.96592582628906828675  // cos(pi/12)
@@ -63,28 +71,30 @@ __device__ __forceinline__ cd rot24(cd x, int q) {
   return {fma(x.x, c, x.y * s), fma(x.y, c, -(x.x * s))};
 }
 
-// DFT_24 = DFT_8 over n1 (n = 3 n1 + n2), twiddles W_24^(n2 k1), DFT_3 over
-// n2 (k = k1 + 8 k2)
-__device__ __forceinline__ void dft24(cd (&a)[24]) {
-  cd y[3][8];
+// DFT_R, R = 3 Q (Q = 8: 24, Q = 4: 12): DFT_Q over n1 (n = 3 n1 + n2),
+// twiddles W_R^(n2 k1) (= W_24^((24 / R) n2 k1)), DFT_3 over n2 (k = k1 + Q k2)
+template <int R>
+__device__ __forceinline__ void dft3x(cd (&a)[R]) {
+  constexpr int Q = R / 3, S = 24 / R;
+  cd y[3][Q];
 #pragma unroll
   for (int n2 = 0; n2 < 3; ++n2) {
-    cd tmp[8];
+    cd tmp[Q];
 #pragma unroll
-    for (int n1 = 0; n1 < 8; ++n1) tmp[n1] = a[3 * n1 + n2];
-    Dft<8>::run(tmp);
+    for (int n1 = 0; n1 < Q; ++n1) tmp[n1] = a[3 * n1 + n2];
+    Dft<Q>::run(tmp);
 #pragma unroll
-    for (int k1 = 0; k1 < 8; ++k1) y[n2][k1] = tmp[k1];
+    for (int k1 = 0; k1 < Q; ++k1) y[n2][k1] = tmp[k1];
   }
 #pragma unroll
-  for (int k1 = 0; k1 < 8; ++k1) {
-    const cd a0 = y[0][k1], a1 = rot24(y[1][k1], k1), a2 = rot24(y[2][k1], 2 * k1);
+  for (int k1 = 0; k1 < Q; ++k1) {
+    const cd a0 = y[0][k1], a1 = rot24(y[1][k1], S * k1), a2 = rot24(y[2][k1], 2 * S * k1);
     // DFT_3: X1 = a0 - (a1 + a2)/2 - i sin(2 pi/3) (a1 - a2), X2 its mirror
     const cd s = a1 + a2, d = a1 - a2;
     const cd m = {fma(-0.5, s.x, a0.x), fma(-0.5, s.y, a0.y)};
     a[k1] = a0 + s;
-    a[k1 + 8] = {fma(GDSP_C12, d.y, m.x), fma(-GDSP_C12, d.x, m.y)};
-    a[k1 + 16] = {fma(-GDSP_C12, d.y, m.x), fma(GDSP_C12, d.x, m.y)};
+    a[k1 + Q] = {fma(GDSP_C12, d.y, m.x), fma(-GDSP_C12, d.x, m.y)};
+    a[k1 + 2 * Q] = {fma(-GDSP_C12, d.y, m.x), fma(GDSP_C12, d.x, m.y)};
   }
 }
 
@@ -122,133 +132,153 @@ __device__ __forceinline__ void c6_twiddle(cd (&v)[R], cd w) {
 // postmultiply and store (issue: the loads, apply: the arithmetic). Issued
 // before the pass-C twiddles or the last exchange's reads instead, the loads
 // push the kernel past 128 VGPRs into spills: 2.43 against 2.37 ms.
+template <int RB>
 struct C6Bhat {
+  using G = C6Geo<RB>;
   rsrc_t rb;
   uint32_t off;
   cd f[16];
   __device__ __forceinline__ void issue() {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) f[r] = buf_ld(rb, off + (uint32_t)(r * kC6T * 16));
+    for (int r = 0; r < 16; ++r) f[r] = buf_ld(rb, off + (uint32_t)(r * G::NA * 16));
   }
   __device__ __forceinline__ void apply(cd (&v)[16]) const {
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = conjg(cmul(v[r], f[r]));
   }
 };
-template <int KN, bool INV>
+template <int RB, int KN, bool INV>
 struct C6Out {
+  using G = C6Geo<RB>;
   rsrc_t rch, rout;
   uint32_t off;
   double scale;
   cd f[KN];
   __device__ __forceinline__ void issue() {
 #pragma unroll
-    for (int r = 0; r < KN; ++r) f[r] = buf_ld(rch, off + (uint32_t)(r * kC6T * 16));
+    for (int r = 0; r < KN; ++r) f[r] = buf_ld(rch, off + (uint32_t)(r * G::NA * 16));
   }
   __device__ __forceinline__ void apply(cd (&v)[16]) const {
 #pragma unroll
     for (int r = 0; r < KN; ++r) {
       cd y = cmul(conjg(v[r]), f[r]);
       if constexpr (INV) y = {y.x * scale, -y.y * scale};
-      buf_st_nt(rout, off + (uint32_t)(r * kC6T * 16), y);
+      buf_st_nt(rout, off + (uint32_t)(r * G::NA * 16), y);
     }
   }
 };
 
-// One FFT_6144 of the thread's registers v[r] = element t + 384 r, in place
+// One FFT_M of the thread's registers v[r] = element t + NA r, in place
 // (natural order in and out), then epi. ZIN: inputs r >= ZIN are zero (pass
 // A pruned); first: no exchange precedes this one in the kernel. tw: the pass
-// twiddle bases, W_384^k (k < 16, pass B) then W_6144^k (k < 384, pass C).
-template <int ZIN, class EPI>
+// twiddle bases, W_{16 RB}^k (k < 16, pass B) then W_M^k (k < NA, pass C).
+// Threads t >= NA (M = 6144: none) sit out passes A and C, threads t >= 256
+// (M = 3072: none) pass B; all take part in the barriers.
+template <int RB, int ZIN, class EPI>
 __device__ __forceinline__ void c6_fft(cd (&v)[16], int t, const cd *__restrict__ tw, double *lds,
                                        bool first, EPI &epi) {
+  using G = C6Geo<RB>;
+  const bool pa = G::NA == G::T || t < G::NA;
+  const bool pb = kC6B == G::T || t < kC6B;
+  // pass A
+  if (pa) {
+    if constexpr (ZIN > 0 && ZIN <= 8) dft_half_in<16, ZIN>(v);
+    else Dft<16>::run(v);
+  }
+  // exchange 1: write 16 t + r, read t + 256 r (t < 256)
   // (the twiddle bases are read where they are used: read a pass ahead,
   // 3.2-3.3 against 2.37 ms)
-  // pass A
-  if constexpr (ZIN > 0 && ZIN <= 8) dft_half_in<16, ZIN>(v);
-  else Dft<16>::run(v);
-  // exchange 1: write 16 t + r, read t + 256 r (t < 256)
-  const bool pb = t < kC6B;
   const int wa = 16 * t, ma = t & 15;
   const int ra = t ^ ((t >> 4) & 15);
-  cd u[24];
+  cd u[RB];
   if (!first) __syncthreads();
+  if (pa) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) lds[wa + (r ^ ma)] = v[r].x;
+    for (int r = 0; r < 16; ++r) lds[wa + (r ^ ma)] = v[r].x;
+  }
   __syncthreads();
   if (pb) {
 #pragma unroll
-    for (int r = 0; r < 24; ++r) u[r].x = lds[ra + kC6B * r];
+    for (int r = 0; r < RB; ++r) u[r].x = lds[ra + kC6B * r];
   }
   __syncthreads();
+  if (pa) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) lds[wa + (r ^ ma)] = v[r].y;
+    for (int r = 0; r < 16; ++r) lds[wa + (r ^ ma)] = v[r].y;
+  }
   __syncthreads();
-  // pass B (waves 0-3; waves 4-5 only take part in the barriers)
-  const int wbo = (t >> 4) * 384 + (t & 15);
+  // pass B
+  const int wbo = (t >> 4) * (16 * RB) + (t & 15);
   if (pb) {
 #pragma unroll
-    for (int r = 0; r < 24; ++r) u[r].y = lds[ra + kC6B * r];
-    c6_twiddle<24>(u, tw[t & 15]);
-    dft24(u);
+    for (int r = 0; r < RB; ++r) u[r].y = lds[ra + kC6B * r];
+    c6_twiddle<RB>(u, tw[t & 15]);
+    dft3x<RB>(u);
   }
   __syncthreads();
-  // exchange 2: write (t / 16) 384 + t % 16 + 16 r, read t + 384 r
+  // exchange 2: write (t / 16) 16 RB + t % 16 + 16 r, read t + NA r
   if (pb) {
 #pragma unroll
-    for (int r = 0; r < 24; ++r) lds[wbo + 16 * r] = u[r].x;
+    for (int r = 0; r < RB; ++r) lds[wbo + 16 * r] = u[r].x;
   }
   __syncthreads();
+  if (pa) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) v[r].x = lds[t + kC6T * r];
+    for (int r = 0; r < 16; ++r) v[r].x = lds[t + G::NA * r];
+  }
   __syncthreads();
   if (pb) {
 #pragma unroll
-    for (int r = 0; r < 24; ++r) lds[wbo + 16 * r] = u[r].y;
+    for (int r = 0; r < RB; ++r) lds[wbo + 16 * r] = u[r].y;
   }
   __syncthreads();
+  if (pa) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) v[r].y = lds[t + kC6T * r];
-  // pass C: twiddle W_6144^(t r), DFT_16, the epilogue
-  c6_twiddle<16>(v, tw[16 + t]);
-  Dft<16>::run(v);
-  epi.issue();
-  epi.apply(v);
+    for (int r = 0; r < 16; ++r) v[r].y = lds[t + G::NA * r];
+    // pass C: twiddle W_M^(t r), DFT_16, the epilogue
+    c6_twiddle<16>(v, tw[16 + t]);
+    Dft<16>::run(v);
+    epi.issue();
+    epi.apply(v);
+  }
 }
 
-// Two workgroups of 6 waves share a CU. Held to 128 VGPRs (4 waves per SIMD
-// of room): at 144 (3 per SIMD) the second workgroup's waves did not fit
-// beside the first's 2-2-1-1 placement and the kernel ran 3.13 against
-// 2.43 ms (profiles/r03/chirpz6k_ab.txt)
-// KN: n <= 384 KN (inputs and wanted outputs at r < KN)
+// M = 6144: two workgroups of 6 waves share a CU. Held to 128 VGPRs (4 waves
+// per SIMD of room): at 144 (3 per SIMD) the second workgroup's waves did not
+// fit beside the first's 2-2-1-1 placement and the kernel ran 3.13 against
+// 2.43 ms (profiles/r03/chirpz6k_ab.txt). M = 3072 (4-wave workgroups, one
+// wave per SIMD each) takes its natural 144-146 VGPRs, three per SIMD: at 128
+// it spills 54-78.
+// KN: n <= NA KN (inputs and wanted outputs at r < KN)
 // REAL: float64 input rows (fft.FFTReal, fft/fft.go:25-27), read directly
 // (no complex copy of the input first)
-template <bool INV, int KN, bool REAL = false>
-__global__ __launch_bounds__(kC6T) __attribute__((amdgpu_waves_per_eu(4))) void chirpz6k_kernel(
+template <int RB, bool INV, int KN, bool REAL = false>
+__global__ __launch_bounds__(C6Geo<RB>::T) __attribute__((amdgpu_waves_per_eu(RB == 24 ? 4 : 3))) void chirpz6k_kernel(
     const void *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
     const cd *__restrict__ tw, const cd *__restrict__ chirp, const cd *__restrict__ bhat,
     double scale) {
+  using G = C6Geo<RB>;
   static_assert(KN >= 1 && KN <= 8, "n <= M/2");
-  __shared__ double lds[kC6M];
+  __shared__ double lds[G::M];
   const int t = (int)threadIdx.x;
   const int64_t g = xcd_remap(blockIdx.x, gridDim.x);
   if (g >= batch) return;  // (grid = batch: never taken)
   const uint32_t off = (uint32_t)t * 16u;
   const int64_t rowb = n * 16;
-  const rsrc_t rin =
-      REAL ? make_rsrc(static_cast<const double *>(in) + g * n, n * 8)
-           : make_rsrc(static_cast<const cd *>(in) + g * n, rowb);
-  const rsrc_t rch = make_rsrc(chirp, rowb);
   cd v[16];
-  {
+  if (G::NA == G::T || t < G::NA) {
+    const rsrc_t rin =
+        REAL ? make_rsrc(static_cast<const double *>(in) + g * n, n * 8)
+             : make_rsrc(static_cast<const cd *>(in) + g * n, rowb);
+    const rsrc_t rch = make_rsrc(chirp, rowb);
     cd xv[KN], cv[KN];
 #pragma unroll
     for (int r = 0; r < KN; ++r) {
       if constexpr (REAL)
-        xv[r] = {buf_ld1(rin, (uint32_t)t * 8u + (uint32_t)(r * kC6T * 8)), 0.0};
+        xv[r] = {buf_ld1(rin, (uint32_t)t * 8u + (uint32_t)(r * G::NA * 8)), 0.0};
       else
-        xv[r] = buf_ld(rin, off + (uint32_t)(r * kC6T * 16));
-      cv[r] = buf_ld(rch, off + (uint32_t)(r * kC6T * 16));
+        xv[r] = buf_ld(rin, off + (uint32_t)(r * G::NA * 16));
+      cv[r] = buf_ld(rch, off + (uint32_t)(r * G::NA * 16));
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -261,35 +291,48 @@ __global__ __launch_bounds__(kC6T) __attribute__((amdgpu_waves_per_eu(4))) void 
       }
     }
   }
-  C6Bhat be{make_rsrc(bhat, (int64_t)kC6M * 16), off, {}};
-  c6_fft<KN>(v, t, tw, lds, true, be);
+  C6Bhat<RB> be{make_rsrc(bhat, (int64_t)G::M * 16), off, {}};
+  c6_fft<RB, KN>(v, t, tw, lds, true, be);
   // the second FFT must not share the first one's addresses (opaque copies:
   // otherwise the compiler keeps them live across both)
   const int t2 = opaque_int(t);
-  C6Out<KN, INV> oe{make_rsrc(opaque_ptr(chirp), rowb), make_rsrc(out + g * n, rowb),
-                    (uint32_t)t2 * 16u, scale, {}};
-  c6_fft<0>(v, t2, opaque_ptr(tw), lds, false, oe);
+  C6Out<RB, KN, INV> oe{make_rsrc(opaque_ptr(chirp), rowb), make_rsrc(out + g * n, rowb),
+                        (uint32_t)t2 * 16u, scale, {}};
+  c6_fft<RB, 0>(v, t2, opaque_ptr(tw), lds, false, oe);
 }
 
-bool chirpz6k_fits(int64_t n) { return n >= 2049 && 2 * n - 1 <= kC6M; }
+// The convolution length for n (0: neither size applies)
+int chirpz6k_m(int64_t n) {
+  if (n >= 2049 && 2 * n - 1 <= 6144) return 6144;
+  if (n >= 1025 && 2 * n - 1 <= 3072) return 3072;
+  return 0;
+}
 
-hipError_t launch_chirpz6k(bool inv, int load, const void *in, cd *out, int64_t n, int64_t batch,
-                           const cd *tw, const cd *chirp, const cd *bhat, double scale,
-                           hipStream_t s) {
-  if (!chirpz6k_fits(n) || batch < 0 || batch > 0x7fffffff || (inv && load == LOAD_REAL))
-    return hipErrorInvalidValue;
-  if (batch == 0) return hipSuccess;
-  const dim3 grid((unsigned)batch), block(kC6T);
+template <int RB>
+static hipError_t launch_c6(bool inv, int load, const void *in, cd *out, int64_t n, int64_t batch,
+                            const cd *tw, const cd *chirp, const cd *bhat, double scale,
+                            hipStream_t s) {
+  const dim3 grid((unsigned)batch), block(C6Geo<RB>::T);
   if (load == LOAD_REAL)
-    hipLaunchKernelGGL((chirpz6k_kernel<false, 8, true>), grid, block, 0, s, in, out, n, batch,
+    hipLaunchKernelGGL((chirpz6k_kernel<RB, false, 8, true>), grid, block, 0, s, in, out, n, batch,
                        tw, chirp, bhat, scale);
   else if (inv)
-    hipLaunchKernelGGL((chirpz6k_kernel<true, 8>), grid, block, 0, s, in, out, n, batch, tw, chirp,
-                       bhat, scale);
+    hipLaunchKernelGGL((chirpz6k_kernel<RB, true, 8>), grid, block, 0, s, in, out, n, batch, tw,
+                       chirp, bhat, scale);
   else
-    hipLaunchKernelGGL((chirpz6k_kernel<false, 8>), grid, block, 0, s, in, out, n, batch, tw,
+    hipLaunchKernelGGL((chirpz6k_kernel<RB, false, 8>), grid, block, 0, s, in, out, n, batch, tw,
                        chirp, bhat, scale);
   return hipGetLastError();
+}
+
+hipError_t launch_chirpz6k(int64_t m, bool inv, int load, const void *in, cd *out, int64_t n,
+                           int64_t batch, const cd *tw, const cd *chirp, const cd *bhat,
+                           double scale, hipStream_t s) {
+  if (chirpz6k_m(n) != m || batch < 0 || batch > 0x7fffffff || (inv && load == LOAD_REAL))
+    return hipErrorInvalidValue;
+  if (batch == 0) return hipSuccess;
+  if (m == 6144) return launch_c6<24>(inv, load, in, out, n, batch, tw, chirp, bhat, scale, s);
+  return launch_c6<12>(inv, load, in, out, n, batch, tw, chirp, bhat, scale, s);
 }
 
 }  // namespace gdsp

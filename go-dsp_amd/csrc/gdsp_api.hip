@@ -342,8 +342,9 @@ struct gdsp_plan {
   // NextPowerOf2(2n-1) = 32768 exceeds one kernel runs as `parts` fused
   // convolutions of M = 16384, each giving kpart outputs; bhat holds parts * M
   int parts = 1;
-  // fused chirp-z on M = 6144 = 16*24*16 (chirpz6k.hip, 2049 <= n <= 3072,
-  // where bluestein.go:70 pads to 8192); tw6k: its pass twiddle bases
+  // fused chirp-z on M = 6144 / 3072 (chirpz6k.hip, 2049 <= n <= 3072 /
+  // 1025 <= n <= 1536, where bluestein.go:70 pads to 8192 / 4096); tw6k: its
+  // pass twiddle bases
   bool c6k = false;
   cd *tw6k = nullptr;
   // composed chirp-z without its fused transposes (GDSP_ALGO_CHIRPZ_UNFUSED)
@@ -753,16 +754,16 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   // the rejected M = 8192 / 2048 Q kernels, when switched on, keep their M
   if (wave_chirpz_enabled() || shfl_chirpz_enabled()) c6k_ok = false;
 #endif
-  if (p->kind == KIND_BLUESTEIN && p->parts == 1 && gdsp::chirpz6k_fits(n) && c6k_ok) {
-    // 2049 <= n <= 3072: bluestein.go:70 pads the convolution to 8192; the
-    // smallest M >= 2n - 1 with a three-pass 16-point-per-thread split, 6144,
-    // gives the same linear convolution (and DFT) with a quarter fewer points
-    // at three waves per SIMD (chirpz6k.hip). GDSP_ALGO_CHIRPZ_POW2 keeps 8192.
-    p->m = 6144;
+  if (p->kind == KIND_BLUESTEIN && p->parts == 1 && gdsp::chirpz6k_m(n) && c6k_ok) {
+    // 2049 <= n <= 3072 (1025 <= n <= 1536): bluestein.go:70 pads the
+    // convolution to 8192 (4096); M = 6144 (3072) = 16 * RB * 16 gives the
+    // same linear convolution (and DFT) with a quarter fewer points
+    // (chirpz6k.hip). GDSP_ALGO_CHIRPZ_POW2 keeps the power of 2.
+    p->m = gdsp::chirpz6k_m(n);
     p->log2m = 0;
     p->c6k = true;
     gdsp::MixedDesc d6{};
-    STCHK(make_mixed_desc(dev, 6144, {16, 24, 16}, d6, &p->tw6k));
+    STCHK(make_mixed_desc(dev, p->m, {16, (int)(p->m / 256), 16}, d6, &p->tw6k));
   }
   if (!p->mplan) STCHK(get_plan_locked(dev, p->m, &p->mplan));
   std::vector<cd> w((size_t)n), chirp((size_t)n),
@@ -1142,8 +1143,8 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
     case KIND_BLUESTEIN_COMPOSED: {
       if (p->kind == KIND_BLUESTEIN && p->c6k) {
         // real input read by the kernel itself (no complex copy first)
-        HIPCHK(gdsp::launch_chirpz6k(inv, load, in, out, p->n, batch, p->tw6k, p->chirp, p->bhat,
-                                     scale, s));
+        HIPCHK(gdsp::launch_chirpz6k(p->m, inv, load, in, out, p->n, batch, p->tw6k, p->chirp,
+                                     p->bhat, scale, s));
         return GDSP_OK;
       }
       const cd *src = (const cd *)in;

@@ -91,13 +91,14 @@ hipError_t launch_fft_mixed(const MixedDesc &d, bool inv, int load, const void *
 hipError_t launch_bluestein(int log2m, bool inv, const cd *in, cd *out, int64_t n,
                             int64_t batch, const cd *twm, const cd *chirp, const cd *bhat,
                             double scale, hipStream_t s);
-// fused chirp-z on M = 6144 = 16*24*16 (chirpz6k.hip) for 2049 <= n <= 3072:
-// tw = W_384^k (k < 16) then W_6144^k (k < 384), bhat = FFT_6144(b)/6144;
-// load LOAD_REAL: float64 rows (forward only)
-bool chirpz6k_fits(int64_t n);
-hipError_t launch_chirpz6k(bool inv, int load, const void *in, cd *out, int64_t n, int64_t batch,
-                           const cd *tw, const cd *chirp, const cd *bhat, double scale,
-                           hipStream_t s);
+// fused chirp-z on M = 16 * RB * 16 (chirpz6k.hip): 6144 for 2049 <= n <=
+// 3072, 3072 for 1025 <= n <= 1536 (chirpz6k_m; 0 otherwise). tw = W_{M/16}^k
+// (k < 16) then W_M^k (k < M/16), bhat = FFT_M(b)/M; load LOAD_REAL: float64
+// rows (forward only)
+int chirpz6k_m(int64_t n);
+hipError_t launch_chirpz6k(int64_t m, bool inv, int load, const void *in, cd *out, int64_t n,
+                           int64_t batch, const cd *tw, const cd *chirp, const cd *bhat,
+                           double scale, hipStream_t s);
 // output-split chirp-z on M = 2^log2m (13 or 14): parts * kpart >= n outputs,
 // n + kpart - 1 <= M, bhat = parts tables of M, twm = T_M
 hipError_t launch_bluestein_parts(int log2m, bool inv, const cd *in, cd *out, int64_t n,

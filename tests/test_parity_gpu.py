@@ -372,10 +372,12 @@ def test_chirpz_plan_vs_oracle(gdsp, oracle, n):
     assert row_nrel(yci, oracle.ifft_rows(x)) < TOL
 
 
-# M = 6144 (16 * 24 * 16) where bluestein.go:70 pads to 8192: the range's
-# ends, primes across it, and a length that is smooth (3072 = 2^10 * 3, the
-# mixed-radix kernel by default, chirp-z only when forced)
-C6K = [2049, 2053, 2307, 2729, 3000, 3001, 3067, 3071, 3072]
+# M = 6144 (16 * 24 * 16) where bluestein.go:70 pads to 8192, M = 3072
+# (16 * 12 * 16) where it pads to 4096: the ranges' ends, primes across them,
+# and lengths that are smooth (3072 = 2^10 * 3, 1500, 1536: the mixed-radix
+# kernel by default, chirp-z only when forced)
+C6K = [2049, 2053, 2307, 2729, 3000, 3001, 3067, 3071, 3072,
+       1025, 1031, 1201, 1500, 1531, 1536]
 
 
 @pytest.mark.parametrize("n", C6K)
@@ -384,7 +386,8 @@ def test_chirpz6k_vs_oracle(gdsp, oracle, n):
     D = __import__("importlib").import_module("go-dsp_amd.device")
     F = __import__("importlib").import_module("go-dsp_amd.fft")
     pc = D.plan(n, chirpz=True)
-    assert (pc.kind, pc.m) == (3, 6144), (n, pc.kind, pc.m)
+    m, m_ref = (6144, 8192) if n > 2048 else (3072, 4096)
+    assert (pc.kind, pc.m) == (3, m), (n, pc.kind, pc.m)
     rng = np.random.default_rng(6144 + n)
     for batch in (1, 5):
         x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
@@ -398,10 +401,10 @@ def test_chirpz6k_vs_oracle(gdsp, oracle, n):
     assert row_nrel(gdsp.fft.FFTBatch(x), oracle.fft_rows(x)) < TOL
     xr = rng.uniform(-1, 1, (3, n))
     assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
-    # the reference's M = 8192 on request (GDSP_ALGO_CHIRPZ_POW2), same results
+    # the reference's M on request (GDSP_ALGO_CHIRPZ_POW2), same results
     F.SetAlgorithm(F.ALGO_CHIRPZ_POW2)
     try:
-        assert D.plan(n, chirpz=True).m == 8192
+        assert D.plan(n, chirpz=True).m == m_ref
         y8 = D.fft_batch(xt, chirpz=True).cpu().numpy()
     finally:
         F.SetAlgorithm(0)
