@@ -734,7 +734,8 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
     // power of 2; the convolution, hence the DFT, is the same. Only where it
     // measured faster: M <= 0.55 of a power of 2 <= 2^16 (8209: 19.5 vs 22.1
     // ms, 16411: 19.4 vs 21.3; 10007, 65537, 100003 were slower). The forced
-    // chirp-z plan keeps the reference's M.
+    // chirp-z plan keeps the reference's M for the composed chirp-z (the
+    // fused one at 1025..1536 / 2049..3072 takes M = 3072 / 6144 below).
     for (int64_t m = 2 * n - 1; p->m <= 65536 && m <= (p->m * 11) / 20; ++m) {
       int64_t r = 0, c = 0;
       if (pow2col_split(m, r, c) || radixcol_split(m, r, c)) {
