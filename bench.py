@@ -15,7 +15,9 @@ rows sharded with two RCCL all-to-alls at N > 1) and pwelch (configs[4]; one
 RCCL all-reduce of the PSD accumulators). --workload X runs one alone.
 bluestein3000 is fft.FFT of N = 3000 through the production dispatch (the
 compiled mixed-radix 25*15*8 kernel); chirpz3000 times the same workload through the
-reference's algorithm (forced Bluestein plan, gdsp_plan_create_chirpz).
+reference's algorithm (forced Bluestein plan, gdsp_plan_create_chirpz), whose
+convolution runs on M = 6144 (chirpz6k.hip); the same line carries the time on the
+reference's M = 8192 (GDSP_ALGO_CHIRPZ_POW2) as "reference_m8192".
 
 roofline.achieved = algorithmic bytes of one launch (32 B/sample: 16 B read +
 16 B written) / the launch's average duration, measured with
