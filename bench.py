@@ -4,7 +4,11 @@
 
 A step = one batched transform over one HBM-resident batch of synthetic
 input (configs[1]: N = 4096 complex128 x 65536 rows). Multi-GPU: one process
-per GPU (torch.distributed.run); the 65536 rows are split over the ranks
+per GPU, started either by torch.distributed.run (WORLD_SIZE must then equal
+--gpus) or, for a plain `python bench.py --gpus N`, by this script itself (N
+rank processes spawned before anything touches a GPU; with the nccl backend it
+exits non-zero when the node has fewer than N GPUs, GDSP_DIST_BACKEND=gloo
+rehearses N ranks on one GPU); the 65536 rows are split over the ranks
 (strong scaling; no data-path collective: the rows are
 independent). value = 2^28 samples / max-over-ranks wall time; at N > 1 a
 weak-scaling figure (65536 rows per rank) is added as "weak_scaling".
@@ -101,7 +105,11 @@ class Ctx:
         # one GPU (RCCL refuses two ranks per device); production runs use nccl=RCCL
         self.backend = os.environ.get("GDSP_DIST_BACKEND", "nccl")
         if self.world > 1:
-            torch.cuda.set_device(local % torch.cuda.device_count())
+            ndev = torch.cuda.device_count()
+            if self.backend == "nccl" and ndev < self.world:
+                raise SystemExit(f"bench.py: {self.world} ranks over nccl (RCCL) need "
+                                 f"{self.world} GPUs, this node has {ndev}")
+            torch.cuda.set_device(local % ndev)
             if self.backend == "nccl":
                 dist.init_process_group("nccl", device_id=torch.device("cuda", local))
             else:
@@ -584,8 +592,98 @@ def run(w: str, c: Ctx, weak: bool = False) -> dict:
     return out
 
 
+def launch_plan(gpus: int, env: dict, device_count) -> tuple:
+    """What `bench.py --gpus N` does before anything touches a GPU.
+
+    Returns ("run", None) when this process is a rank (WORLD_SIZE set by
+    torch.distributed.run or by launch(), or N = 1), ("spawn", [env per rank])
+    when it must start N rank processes itself, or ("error", message).
+    device_count() is only called for a spawn with the nccl backend (RCCL
+    needs one GPU per rank); the gloo rehearsal (GDSP_DIST_BACKEND=gloo) may
+    put several ranks on one GPU."""
+    if gpus < 1:
+        return "error", f"--gpus must be >= 1 (got {gpus})"
+    ws = env.get("WORLD_SIZE")
+    backend = env.get("GDSP_DIST_BACKEND", "nccl")
+    if ws is not None:
+        if int(ws) != gpus:
+            return "error", (f"WORLD_SIZE={ws} (set by the launcher) but --gpus {gpus}: "
+                             "the two must agree")
+        return "run", None
+    if gpus == 1:
+        return "run", None
+    if backend == "nccl":
+        have = device_count()
+        if have < gpus:
+            return "error", (f"--gpus {gpus} with the nccl (RCCL) backend needs {gpus} GPUs, "
+                             f"this node has {have}; GDSP_DIST_BACKEND=gloo rehearses the "
+                             "multi-rank path with ranks sharing a GPU")
+    port = env.get("MASTER_PORT") or str(_free_port())
+    ranks = []
+    for r in range(gpus):
+        e = dict(env)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(gpus),
+                  "LOCAL_WORLD_SIZE": str(gpus), "GROUP_RANK": "0",
+                  "MASTER_ADDR": env.get("MASTER_ADDR", "127.0.0.1"), "MASTER_PORT": port})
+        ranks.append(e)
+    return "spawn", ranks
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(cmd: list, ranks: list, poll_s: float = 0.2) -> int:
+    """Start one child per rank (cmd with that rank's environment) and wait.
+    The children inherit stdout/stderr: only rank 0 prints the JSON line. The
+    first child to fail ends the others (their exact PIDs), and its exit
+    status is returned. This process makes no GPU call."""
+    import subprocess
+    procs = [subprocess.Popen(cmd, env=e) for e in ranks]
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                r = p.poll()
+                if r is None:
+                    continue
+                procs.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r
+                    for q in procs:
+                        q.terminate()
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        deadline = time.time() + 20
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    return rc if rc >= 0 else 128 - rc  # a signalled child: 128 + signal number
+
+
+def _device_count() -> int:
+    # counting devices does not initialise the GPU (no HIP context is made)
+    import torch
+    return torch.cuda.device_count()
+
+
 def main():
     args = parse()
+    what, info = launch_plan(args.gpus, dict(os.environ), _device_count)
+    if what == "error":
+        print(f"bench.py: {info}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if what == "spawn":
+        sys.exit(launch([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], info))
     c = Ctx(args)
     w = "radix4096" if args.workload == "default" else args.workload
     head = run(w, c)

@@ -15,6 +15,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # GDSP_LIB: an alternate build of the same library (A/B builds in experiments)
 LIB_PATH = os.environ.get("GDSP_LIB") or os.path.join(_HERE, "lib", "libgdspfft.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gdsp_fft.h")
+# queries only the development build (go-dsp_amd/lib_dev) exports
+DEV_HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gdsp_fft_dev.h")
 
 GDSP_OK = 0
 GDSP_ERR_INVALID = 1
@@ -64,8 +66,6 @@ SIGNATURES = {
     "gdsp_plan_create_chirpz": (_I, [_I64, ctypes.POINTER(_P)]),
     "gdsp_plan_destroy": (_I, [_P]),
     "gdsp_plan_kind": (_I, [_P]),
-    "gdsp_plan_wave_q": (_I, [_P]),
-    "gdsp_plan_shfl": (_I, [_P]),
     "gdsp_plan_parts": (_I, [_P]),
     "gdsp_plan_info": (_I, [_P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64),
                             ctypes.POINTER(_I64), ctypes.POINTER(_I)]),
@@ -90,6 +90,13 @@ SIGNATURES = {
                                ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
 }
 
+# include/gdsp_fft_dev.h: bound only when the loaded library is the
+# development build (the product library does not export them)
+DEV_SIGNATURES = {
+    "gdsp_plan_wave_q": (_I, [_P]),
+    "gdsp_plan_shfl": (_I, [_P]),
+}
+
 _lib = None
 
 
@@ -108,9 +115,9 @@ class Panic(GDSPError):
 _PANIC_STATUSES = {GDSP_ERR_UNEQUAL, GDSP_ERR_EMPTY, GDSP_ERR_RAGGED, GDSP_ERR_DIVIDE_BY_ZERO}
 
 
-def header_functions() -> list[str]:
-    """Every function name declared in include/gdsp_fft.h."""
-    src = open(HEADER_PATH).read()
+def header_functions(path: str = HEADER_PATH) -> list[str]:
+    """Every function name declared in include/gdsp_fft.h (or another header)."""
+    src = open(path).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(gdsp_[a-z0-9_]+)\s*\(", src)))
 
@@ -143,6 +150,11 @@ def lib() -> ctypes.CDLL:
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
+        for name, (res, args) in DEV_SIGNATURES.items():
+            if hasattr(L, name):
+                f = getattr(L, name)
+                f.restype = res
+                f.argtypes = args
         _lib = L
     return _lib
 
@@ -156,6 +168,11 @@ def check(status: int, what: str = "") -> None:
     if status in _PANIC_STATUSES:
         raise Panic(status, msg)
     raise GDSPError(status, f"{what}: {msg} ({detail})")
+
+
+def is_dev_build() -> bool:
+    """True when the loaded library is the development build."""
+    return hasattr(lib(), "gdsp_plan_wave_q")
 
 
 def device_count() -> int:

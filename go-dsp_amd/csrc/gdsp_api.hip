@@ -19,6 +19,9 @@
 
 #include "fft_device.hpp"
 #include "gdsp_fft.h"
+#ifdef GDSP_DEV_BUILD
+#include "gdsp_fft_dev.h"
+#endif
 #include "launch.hpp"
 #include "api_internal.hpp"
 
@@ -486,8 +489,17 @@ int build_mixed(int dev, int64_t n, const std::vector<int> &rad, gdsp_plan *p) {
 // P <= 8 with n + ceil(n/P) - 1 <= 16384 where NextPowerOf2(2n-1) exceeds
 // one kernel, else 0 (composed chirp-z). P = 8 (n <= 14563) measured 10.8
 // against 11.5 ms for the composed chirp-z per 2^27 samples, P = 2 4x faster.
+// The algorithm flags a plan is built under: read once by the outermost
+// get_plan_locked of a thread (the cache key) and used by every decision of
+// that build and of the sub-plans it fetches, so a concurrent
+// gdsp_set_algorithm cannot leave a plan built under mixed flags in the
+// cache (plans are built under g_plan_mu; the snapshot is per thread).
+thread_local int t_build_depth = 0;
+thread_local unsigned t_build_flags = 0;
+unsigned plan_flags() { return t_build_depth > 0 ? t_build_flags : gdsp::algo_flags(); }
+
 int chirpz_parts(int64_t n) {
-  const bool off = (gdsp::algo_flags() & GDSP_ALGO_NO_CHIRPZ_PARTS) != 0;
+  const bool off = (plan_flags() & GDSP_ALGO_NO_CHIRPZ_PARTS) != 0;
   const int64_t mk = (int64_t)1 << gdsp::kMaxLdsLog2;
   if (off || next_pow2_ref(2 * n - 1) <= mk) return 0;
   for (int parts = 2; parts <= 8; ++parts)
@@ -725,9 +737,9 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
       p->kpart = (n + parts - 1) / parts;
     }
   }
-  p->unfused = (gdsp::algo_flags() & GDSP_ALGO_CHIRPZ_UNFUSED) != 0;
+  p->unfused = (plan_flags() & GDSP_ALGO_CHIRPZ_UNFUSED) != 0;
   if (p->kind == KIND_BLUESTEIN_COMPOSED && !chirpz &&
-      !(gdsp::algo_flags() & GDSP_ALGO_CHIRPZ_POW2)) {
+      !(plan_flags() & GDSP_ALGO_CHIRPZ_POW2)) {
     // The composed chirp-z is HBM-bound, so its cost follows M: take the
     // smallest M >= 2n - 1 with a three-pass split (power-of-2 or
     // single-radix columns, one-kernel rows) instead of bluestein.go:70's
@@ -750,7 +762,7 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
       }
     }
   }
-  bool c6k_ok = !(gdsp::algo_flags() & GDSP_ALGO_CHIRPZ_POW2);
+  bool c6k_ok = !(plan_flags() & GDSP_ALGO_CHIRPZ_POW2);
 #ifdef GDSP_DEV_BUILD
   // the rejected M = 8192 / 2048 Q kernels, when switched on, keep their M
   if (wave_chirpz_enabled() || shfl_chirpz_enabled()) c6k_ok = false;
@@ -824,14 +836,24 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
 
 int get_plan_locked(int dev, int64_t n, gdsp_plan **out, bool chirpz = false) {
   auto &cache = chirpz ? g_chirpz_plans : g_plans;
-  auto key = std::make_tuple(dev, n, gdsp::algo_flags());
+  auto key = std::make_tuple(dev, n, plan_flags());
   auto it = cache.find(key);
   if (it != cache.end()) {
     *out = it->second;
     return GDSP_OK;
   }
   gdsp_plan *p = new gdsp_plan();
-  int st = build_plan(dev, n, p, chirpz);
+  struct Depth {  // leaves the snapshot on every exit, exceptions included
+    explicit Depth(unsigned f) {
+      if (t_build_depth++ == 0) t_build_flags = f;
+    }
+    ~Depth() { --t_build_depth; }
+  };
+  int st;
+  {
+    Depth d(std::get<2>(key));
+    st = build_plan(dev, n, p, chirpz);
+  }
   if (st != GDSP_OK) {
     delete p;  // device tables of a failed plan are leaked deliberately (rare)
     return st;
@@ -1650,9 +1672,11 @@ int gdsp_plan_create_chirpz(int64_t n, gdsp_plan **plan) {
 int gdsp_plan_destroy(gdsp_plan *) { return GDSP_OK; }
 
 int gdsp_plan_kind(const gdsp_plan *plan) { return plan ? plan->kind : -1; }
+#ifdef GDSP_DEV_BUILD
+// include/gdsp_fft_dev.h: queries of the development build's kernels only
 int gdsp_plan_wave_q(const gdsp_plan *plan) { return plan ? plan->wq : 0; }
-
 int gdsp_plan_shfl(const gdsp_plan *plan) { return plan && plan->bhats ? 1 : 0; }
+#endif
 int gdsp_plan_parts(const gdsp_plan *plan) { return plan ? plan->parts : 0; }
 
 int gdsp_plan_info(const gdsp_plan *plan, int64_t *n, int64_t *m, int64_t *n1, int64_t *n2,

@@ -150,8 +150,12 @@ class Pool {
   }
 
   // f(i) on worker i for i < n, concurrently; the first failing shard's
-  // status and message become the caller's.
-  int run(int n, const std::function<int(int)> &f) {
+  // status and message become the caller's. When every shard succeeded,
+  // after() runs on the calling thread while the call still holds the pool
+  // (the collective step of a call: no other multi-device call can touch
+  // the workers' streams or an RCCL clique in between).
+  int run(int n, const std::function<int(int)> &f,
+          const std::function<int()> &after = nullptr) {
     std::lock_guard<std::mutex> call(run_mu_);
     while ((int)ws_.size() < n) {
       ws_.emplace_back(new W);
@@ -183,7 +187,13 @@ class Pool {
         msg = w->msg;
       }
     }
-    return st == GDSP_OK ? GDSP_OK : set_error(st, msg);
+    if (st != GDSP_OK) return set_error(st, msg);
+    if (!after) return GDSP_OK;
+    try {
+      return after();
+    } catch (...) {  // nothing may throw past the C ABI
+      return set_error(GDSP_ERR_NOMEM, "exception in a multi-device call");
+    }
   }
 
  private:
@@ -232,6 +242,7 @@ struct Rccl {
   decltype(&ncclGroupStart) group_start = nullptr;
   decltype(&ncclGroupEnd) group_end = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
+  decltype(&ncclCommAbort) comm_abort = nullptr;
   std::string why;  // empty when loaded
 };
 
@@ -251,8 +262,10 @@ const Rccl &rccl() {
     x.group_start = (decltype(x.group_start))dlsym(h, "ncclGroupStart");
     x.group_end = (decltype(x.group_end))dlsym(h, "ncclGroupEnd");
     x.error_string = (decltype(x.error_string))dlsym(h, "ncclGetErrorString");
-    if (!x.init_all || !x.reduce || !x.group_start || !x.group_end || !x.error_string)
-      x.why = "librccl.so.1 lacks an ncclCommInitAll/ncclReduce/ncclGroup* symbol";
+    x.comm_abort = (decltype(x.comm_abort))dlsym(h, "ncclCommAbort");
+    if (!x.init_all || !x.reduce || !x.group_start || !x.group_end || !x.error_string ||
+        !x.comm_abort)
+      x.why = "librccl.so.1 lacks an ncclCommInitAll/ncclReduce/ncclGroup*/ncclCommAbort symbol";
     return x;
   }();
   return r;
@@ -262,10 +275,14 @@ int nccl_fail(const Rccl &r, ncclResult_t e, const char *what) {
   return set_error(GDSP_ERR_HIP, std::string(what) + ": " + r.error_string(e));
 }
 
-// One clique per device list, built once (ncclCommInitAll) and kept.
+// One clique per device list, built once (ncclCommInitAll) and kept until
+// a collective on it fails (drop_comms).
+std::mutex g_comms_mu;
+std::map<std::vector<int>, std::vector<ncclComm_t>> g_comms;
+
 int comms_for(const std::vector<int> &devs, std::vector<ncclComm_t> **out) {
-  static std::mutex mu;
-  static std::map<std::vector<int>, std::vector<ncclComm_t>> cache;
+  auto &mu = g_comms_mu;
+  auto &cache = g_comms;
   const Rccl &r = rccl();
   if (!r.why.empty()) return set_error(GDSP_ERR_UNSUPPORTED, r.why);
   std::lock_guard<std::mutex> lk(mu);
@@ -278,6 +295,17 @@ int comms_for(const std::vector<int> &devs, std::vector<ncclComm_t> **out) {
   }
   *out = &it->second;
   return GDSP_OK;
+}
+
+// After a failed collective: abort every communicator of the clique (so no
+// rank is left inside it) and forget it; the next call builds a new one.
+void drop_comms(const std::vector<int> &devs) {
+  const Rccl &r = rccl();
+  std::lock_guard<std::mutex> lk(g_comms_mu);
+  auto it = g_comms.find(devs);
+  if (it == g_comms.end()) return;
+  for (ncclComm_t c : it->second) (void)r.comm_abort(c);
+  g_comms.erase(it);
 }
 
 // ---- shard geometry ----------------------------------------------------------------
@@ -344,34 +372,19 @@ int fft_batch_multi(const void *x, size_t in_elem_bytes, double *out, int64_t n,
   });
 }
 
-// All workers of one Pool::run meet here between accumulating and reducing:
-// the collective starts only when every shard has its accumulator, so a
-// failing shard cannot leave the others waiting inside it.
-class Rendezvous {
- public:
-  explicit Rendezvous(int n) : n_(n) {}
-  // true when every worker arrived without failing
-  bool arrive(bool ok) {
-    std::unique_lock<std::mutex> lk(mu_);
-    if (!ok) failed_ = true;
-    if (++arrived_ == n_) cv_.notify_all();
-    else cv_.wait(lk, [this] { return arrived_ == n_; });
-    return !failed_;
-  }
-
- private:
-  std::mutex mu_;
-  std::condition_variable cv_;
-  int n_, arrived_ = 0;
-  bool failed_ = false;
-};
-
 // Device buffer owned by one call (the accumulators the reduce reads: never
-// a worker's shared scratch, which the next call would reuse).
+// a worker's shared scratch, which the next call would reuse), freed on its
+// own device.
 struct CallBuf {
   void *p = nullptr;
+  int dev = -1;
   ~CallBuf() {
-    if (p) (void)hipFree(p);
+    if (!p) return;
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(dev);
+    (void)hipFree(p);
+    if (cur >= 0) (void)hipSetDevice(cur);
   }
 };
 
@@ -422,61 +435,96 @@ int pwelch_multi(const double *x, int64_t n, double fs, int64_t nfft, int64_t pa
     std::vector<int> sorted(devs);
     std::sort(sorted.begin(), sorted.end());
     const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-    std::vector<ncclComm_t> *comms = nullptr;
-    const bool use_rccl = distinct && comms_for(devs, &comms) == GDSP_OK;
-    std::vector<std::vector<double>> part(use_rccl ? 1 : D);
-    Rendezvous meet(D);
+    const bool use_rccl = distinct && rccl().why.empty();
+    bool reduced_by_rccl = false;
+    std::vector<std::vector<double>> part((size_t)D);
+    std::vector<CallBuf> dacc((size_t)D);
+    std::vector<hipStream_t> streams((size_t)D, nullptr);
     ++g_pwelch_calls;
+    // Phase 1, on the workers: every shard accumulates into its own
+    // call-owned device buffer (a failing shard reports its own status and
+    // message; the others return GDSP_OK and their work is dropped).
+    auto accumulate = [&](int i) -> int {
+      MHIPCHK(hipSetDevice(devs[i]));
+      hipStream_t s = stream_for(devs[i]);
+      if (!s) return set_error(GDSP_ERR_HIP, "stream creation failed");
+      streams[(size_t)i] = s;
+      int64_t seg_lo, seg_hi, x_lo, x_hi;
+      pwelch_shard(nsegs, nfft, noverlap, D, i, &seg_lo, &seg_hi, &x_lo, &x_hi);
+      void *dx = nullptr, *dw = nullptr;
+      const int64_t len = x_hi - x_lo;
+      CallBuf &a = dacc[(size_t)i];
+      a.dev = devs[i];
+      MHIPCHK(hipMalloc(&a.p, (size_t)flen * sizeof(double)));
+      MSTCHK(scratch((size_t)(len > 0 ? len : 1) * sizeof(double), s, SCRATCH_SIGNAL, &dx));
+      MSTCHK(scratch((size_t)flen * sizeof(double), s, SCRATCH_WINDOW, &dw));
+      MHIPCHK(hipMemsetAsync(a.p, 0, (size_t)flen * sizeof(double), s));
+      if (len > 0) {
+        const int64_t have = (x_hi < n ? x_hi : n) - x_lo;  // past n: ZeroPadF's zeros
+        if (have < len) MHIPCHK(hipMemsetAsync(dx, 0, (size_t)len * sizeof(double), s));
+        if (have > 0) MSTCHK(h2d(dx, x + x_lo, (size_t)have * sizeof(double), s));
+        MSTCHK(h2d(dw, win_seg, (size_t)flen * sizeof(double), s));
+        MSTCHK(gdsp_pwelch_accumulate_device((const double *)dx, len, nfft, pad, noverlap, 0,
+                                             seg_hi - seg_lo, (const double *)dw,
+                                             (double *)a.p, s));
+      }
+      if (use_rccl) return GDSP_OK;  // the reduce reads it on the same stream
+      part[(size_t)i].resize((size_t)flen);
+      return d2h(part[(size_t)i].data(), a.p, (size_t)flen * sizeof(double), s);
+    };
+    // Phase 2, on the calling thread once every shard succeeded, still inside
+    // the pool's call: one grouped RCCL reduce over the clique (a single
+    // thread driving several devices must group its calls), each rank on the
+    // stream that produced its accumulator; root 0 receives the sum. A failed
+    // group aborts the clique, so no rank stays inside the collective.
+    auto reduce = [&]() -> int {
+      const Rccl &r = rccl();
+      std::vector<ncclComm_t> *comms = nullptr;
+      if (comms_for(devs, &comms) != GDSP_OK) {
+        // no clique for this set (e.g. ncclCommInitAll refused it): the
+        // accumulators come back to the host and are summed there
+        for (int i = 0; i < D; ++i) {
+          MHIPCHK(hipSetDevice(devs[i]));
+          part[(size_t)i].resize((size_t)flen);
+          MSTCHK(d2h(part[(size_t)i].data(), dacc[(size_t)i].p, (size_t)flen * sizeof(double),
+                     streams[(size_t)i]));
+        }
+        return GDSP_OK;
+      }
+      ncclResult_t e = r.group_start();
+      if (e != ncclSuccess) return nccl_fail(r, e, "ncclGroupStart");
+      ncclResult_t first = ncclSuccess;
+      for (int i = 0; i < D && first == ncclSuccess; ++i) {
+        if (hipSetDevice(devs[i]) != hipSuccess) {
+          first = ncclUnhandledCudaError;
+          break;
+        }
+        double *da = (double *)dacc[(size_t)i].p;
+        first = r.reduce(da, da, (size_t)flen, ncclFloat64, ncclSum, 0, (*comms)[i],
+                         streams[(size_t)i]);
+      }
+      e = r.group_end();
+      if (first == ncclSuccess) first = e;
+      if (first != ncclSuccess) {
+        const int st = nccl_fail(r, first, "ncclReduce (grouped)");
+        drop_comms(devs);
+        return st;
+      }
+      MHIPCHK(hipSetDevice(devs[0]));
+      part[0].resize((size_t)flen);
+      MSTCHK(d2h(part[0].data(), dacc[0].p, (size_t)flen * sizeof(double), streams[0]));
+      for (int i = 1; i < D; ++i) {
+        MHIPCHK(hipSetDevice(devs[i]));
+        MHIPCHK(hipStreamSynchronize(streams[(size_t)i]));
+      }
+      reduced_by_rccl = true;
+      return GDSP_OK;
+    };
     // one Pool::run holds the whole call (accumulate, reduce, copy back), so
     // concurrent calls from other host threads queue behind it and never
     // share its accumulators, streams or clique
-    MSTCHK(Pool::get().run(D, [&](int i) -> int {
-      CallBuf dacc;
-      hipStream_t s = nullptr;
-      auto accumulate = [&]() -> int {
-        MHIPCHK(hipSetDevice(devs[i]));
-        s = stream_for(devs[i]);
-        if (!s) return set_error(GDSP_ERR_HIP, "stream creation failed");
-        int64_t seg_lo, seg_hi, x_lo, x_hi;
-        pwelch_shard(nsegs, nfft, noverlap, D, i, &seg_lo, &seg_hi, &x_lo, &x_hi);
-        void *dx = nullptr, *dw = nullptr;
-        const int64_t len = x_hi - x_lo;
-        MHIPCHK(hipMalloc(&dacc.p, (size_t)flen * sizeof(double)));
-        MSTCHK(scratch((size_t)(len > 0 ? len : 1) * sizeof(double), s, SCRATCH_SIGNAL, &dx));
-        MSTCHK(scratch((size_t)flen * sizeof(double), s, SCRATCH_WINDOW, &dw));
-        MHIPCHK(hipMemsetAsync(dacc.p, 0, (size_t)flen * sizeof(double), s));
-        if (len > 0) {
-          const int64_t have = (x_hi < n ? x_hi : n) - x_lo;  // past n: ZeroPadF's zeros
-          if (have < len) MHIPCHK(hipMemsetAsync(dx, 0, (size_t)len * sizeof(double), s));
-          if (have > 0) MSTCHK(h2d(dx, x + x_lo, (size_t)have * sizeof(double), s));
-          MSTCHK(h2d(dw, win_seg, (size_t)flen * sizeof(double), s));
-          MSTCHK(gdsp_pwelch_accumulate_device((const double *)dx, len, nfft, pad, noverlap, 0,
-                                               seg_hi - seg_lo, (const double *)dw,
-                                               (double *)dacc.p, s));
-        }
-        return GDSP_OK;
-      };
-      const int st = accumulate();
-      if (!meet.arrive(st == GDSP_OK)) return st != GDSP_OK ? st : GDSP_ERR_HIP;
-      double *da = (double *)dacc.p;
-      if (use_rccl) {
-        // every worker issues its rank's reduce on the stream that produced
-        // its accumulator; root 0 receives the sum
-        const Rccl &r = rccl();
-        const ncclResult_t e =
-            r.reduce(da, da, (size_t)flen, ncclFloat64, ncclSum, 0, (*comms)[i], s);
-        if (e != ncclSuccess) return nccl_fail(r, e, "ncclReduce");
-        if (i == 0) {
-          part[0].resize((size_t)flen);
-          return d2h(part[0].data(), da, (size_t)flen * sizeof(double), s);
-        }
-        MHIPCHK(hipStreamSynchronize(s));
-        return GDSP_OK;
-      }
-      part[i].resize((size_t)flen);
-      return d2h(part[i].data(), da, (size_t)flen * sizeof(double), s);
-    }));
-    if (use_rccl) {
+    MSTCHK(Pool::get().run(D, accumulate, use_rccl ? std::function<int()>(reduce) : nullptr));
+    if (reduced_by_rccl) {
       acc.swap(part[0]);
       ++g_rccl_reduces;
     } else {

@@ -263,17 +263,6 @@ int gdsp_plan_kind(const gdsp_plan *plan);
  * runtime-compiled specialisation backs it (1) or not (0). 0 where n/a. */
 int gdsp_plan_info(const gdsp_plan *plan, int64_t *n, int64_t *m, int64_t *n1, int64_t *n2,
                    int *runtime_compiled);
-/* Waves per transform of the wave-resident chirp-z kernel (fft_wave.hip:
- * one 64-lane wavefront per 2048-point sub-transform, M = 2048 * waves) that a
- * kind-3 plan with 512 < n <= 4096 runs, or 0 for any other kernel. That
- * kernel is in the development build only (GDSP_BLU_WAVE=1 there): the
- * default library always returns 0. */
-int gdsp_plan_wave_q(const gdsp_plan *plan);
-/* 1 when a kind-3 plan (M = 8192, 2049 <= n <= 4096) runs the chirp-z kernel
- * whose FFTs keep one of their two exchanges inside the wavefront
- * (bluestein_shfl.hip; development build only, GDSP_BLU_SHFL=1 there), else
- * 0 (always 0 in the default library). */
-int gdsp_plan_shfl(const gdsp_plan *plan);
 /* Output parts of a kind-3 plan: 1 for the one-convolution chirp-z of
  * bluestein.go:68-94; P > 1 when n in (8192, 14563] (NextPowerOf2(2n-1) =
  * 32768, beyond one kernel) runs as P fused convolutions of M = 16384, each

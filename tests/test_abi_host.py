@@ -5,11 +5,19 @@ mirror (windows, dsputils, Segment, Pwelch finalisation) matches the
 reference's tables and the oracle."""
 import ctypes
 import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
 
-from conftest import nrel
+from conftest import REPO, nrel
+
+
+def _exported(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True,
+                         check=True).stdout
+    return {l.split()[-1] for l in out.splitlines() if l.strip()}
 
 
 def test_library_exports_every_header_symbol(gdsp):
@@ -19,6 +27,28 @@ def test_library_exports_every_header_symbol(gdsp):
     for n in names:
         assert hasattr(L, n), n
         assert n in gdsp._lib.SIGNATURES, n
+
+
+def test_product_library_exports_no_dev_query(gdsp):
+    # include/gdsp_fft_dev.h's queries belong to the development build only
+    dev_names = gdsp._lib.header_functions(gdsp._lib.DEV_HEADER_PATH)
+    assert sorted(dev_names) == sorted(gdsp._lib.DEV_SIGNATURES)
+    prod = _exported(os.path.join(REPO, "go-dsp_amd", "lib", "libgdspfft.so"))
+    public = {n for n in prod if n.startswith("gdsp_")}
+    assert public == set(gdsp._lib.header_functions()), public ^ set(gdsp._lib.header_functions())
+    assert not public & set(dev_names)
+
+
+def test_dev_library_exports_both_headers():
+    path = os.path.join(REPO, "go-dsp_amd", "lib_dev", "libgdspfft.so")
+    if not os.path.exists(path):
+        pytest.skip("development build not built")
+    sys.path.insert(0, REPO)
+    import importlib
+    _lib = importlib.import_module("go-dsp_amd._lib")
+    have = _exported(path)
+    for n in _lib.header_functions() + _lib.header_functions(_lib.DEV_HEADER_PATH):
+        assert n in have, n
 
 
 def test_version_and_status_strings(gdsp):

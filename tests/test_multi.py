@@ -180,6 +180,33 @@ def test_shards_on_one_device_vs_oracle(gdsp, oracle):
     assert st1["host_reduces"] == st0["host_reduces"] + 3
 
 
+@pytest.mark.gpu
+def test_pwelch_eight_shards_on_one_device_vs_oracle(gdsp, oracle):
+    """BASELINE configs[4]'s split — the 2^30-sample Pwelch over 8 GPUs —
+    rehearsed on the one-GPU box: gdsp_pwelch_multi with devices [0]*8 runs 8
+    segment shards (each with its 2048-sample halo) side by side on device 0,
+    at 2^24 samples of the bench's stream, NFFT 4096, 50 % overlap, Hann;
+    against the reference restatement (spectral/pwelch.go:74-145), and the
+    same call on one shard."""
+    n = 1 << 24
+    x = oracle.fill_uniform(n, 0x5EED)
+    o = gdsp.spectral.PwelchOptions(NFFT=4096, Noverlap=2048)
+    st0 = gdsp.fft.MultiStats()
+    p, f = gdsp.spectral.PwelchMulti(x, 1.0, o, devices=[0] * 8)
+    st1 = gdsp.fft.MultiStats()
+    assert st1["pwelch_calls"] == st0["pwelch_calls"] + 1
+    assert st1["host_reduces"] == st0["host_reduces"] + 1  # repeated device: host sum
+    pr, fr = oracle.pwelch(x, 1.0, 4096, 0, 2048)
+    assert p.size == 2049 and nrel(p, pr) < 1e-9 and nrel(f, fr) < 1e-15
+    p1, _ = gdsp.spectral.PwelchMulti(x, 1.0, o, devices=[0])
+    assert nrel(p, p1) < 1e-13
+    # the shards tile the 8191 segments exactly (configs[4]'s 8-way split)
+    S = gdsp.spectral.segment_count(n, 4096, 2048)
+    bounds = [gdsp.spectral.pwelch_shard(S, 4096, 2048, 8, i) for i in range(8)]
+    assert bounds[0][0] == 0 and bounds[-1][1] == S
+    assert all(a[1] == b[0] for a, b in zip(bounds, bounds[1:]))
+
+
 _ROUTE = r"""
 import importlib, os, sys
 sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
