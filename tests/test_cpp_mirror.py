@@ -214,3 +214,51 @@ print("ok", g._lib.jit_stats())
     assert runs[0]["built"] == 2 and runs[0]["cached"] == 0 and runs[0]["failed"] == 0, runs
     assert runs[1]["built"] == 0 and runs[1]["cached"] == 2 and runs[1]["failed"] == 0, runs
     assert len(list((tmp_path / "cache").glob("*.co"))) == 2
+
+
+SHIM_BIN = os.path.join(REPO, "tests", "cpp", "bin", "shim_replay")
+GO = os.path.join(REPO, "go")
+
+
+def test_go_shim_covers_the_reference_api():
+    """go/ holds the cgo shim as source: every exported function of
+    fft/fft.go:25-162 and spectral/pwelch.go:28,74 (and
+    wav.go:138's ReadFloats) is defined there, under the gdspgpu build tag,
+    and every C function it calls is declared in include/gdsp_fft.h."""
+    import re
+    import importlib
+    lib = importlib.import_module("go-dsp_amd._lib")
+    declared = set(lib.header_functions())
+    want = {"fft/fft_gpu.go": {"FFT", "FFTReal", "IFFT", "IFFTReal", "Convolve", "FFT2",
+                               "FFT2Real", "IFFT2", "IFFT2Real", "FFTN", "IFFTN",
+                               "SetWorkerPoolSize", "EnsurePlan"},
+            "spectral/pwelch_gpu.go": {"Pwelch"},
+            "wav/wav_gpu.go": {"ReadFloats"}}
+    for rel, names in want.items():
+        src = open(os.path.join(GO, rel)).read()
+        assert src.startswith("//go:build gdspgpu\n"), rel
+        assert "#cgo LDFLAGS: -lgdspfft" in src and '#include "gdsp_fft.h"' in src, rel
+        defined = set(re.findall(r"^func (?:\([^)]*\) )?([A-Z]\w*)\(", src, flags=re.M))
+        assert names <= defined, (rel, names - defined)
+        called = set(re.findall(r"\bC\.(gdsp_\w+)\(", src))
+        assert called and called <= declared, (rel, called - declared)
+    pw = open(os.path.join(GO, "spectral/pwelch_gpu.go")).read()
+    for field in ("NFFT      int", "Window    func(int) []float64", "Pad       int",
+                  "Noverlap  int", "Scale_off bool"):  # pwelch.go:28-65
+        assert field in pw, field
+
+
+def test_shim_replay_built():
+    assert os.path.exists(SHIM_BIN), "tests/cpp/bin/shim_replay missing: run __graft_entry__.build()"
+
+
+@pytest.mark.gpu
+def test_shim_replay(refvec, tmp_path):
+    """The cgo shim's call sequences (go/, replayed in C++) on the GPU: every
+    function against the oracle on both sides of the small-n policy, the
+    reference's tables and every panic."""
+    vec = tmp_path / "vectors.txt"
+    _write_vectors(refvec, vec)
+    r = subprocess.run([SHIM_BIN, str(vec)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "failures 0" in r.stdout
