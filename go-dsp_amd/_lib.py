@@ -70,6 +70,7 @@ SIGNATURES = {
     "gdsp_plan_info": (_I, [_P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64),
                             ctypes.POINTER(_I64), ctypes.POINTER(_I)]),
     "gdsp_fft_batch_device": (_I, [_P, _P, _P, _I64, _I, _P]),
+    "gdsp_fft_real_batch_device": (_I, [_P, _P, _P, _I64, _I, _P]),
     "gdsp_fft2_device": (_I, [_P, _P, _I64, _I64, _I, _P, _P]),
     "gdsp_pwelch_accumulate_device": (_I, [_P, _I64, _I64, _I64, _I64, _I64, _I64, _P, _P, _P]),
     "gdsp_pwelch_finalize": (_I, [_P, _I64, _I64, _I64, _I64, _P, _D, _I, _P, _P]),

@@ -1698,6 +1698,18 @@ int gdsp_fft_batch_device(const gdsp_plan *plan, const void *d_in, void *d_out, 
                    (hipStream_t)stream);
 }
 
+int gdsp_fft_real_batch_device(const gdsp_plan *plan, const double *d_in, void *d_out,
+                               int64_t batch, int inverse, void *stream) {
+  if (!plan || batch < 0) return fail(GDSP_ERR_INVALID, "bad argument");
+  if (plan->n == 0 && inverse) return fail(GDSP_ERR_EMPTY, "IFFT of an empty slice");
+  const size_t in_bytes = (size_t)batch * (size_t)plan->n * sizeof(double);
+  const char *i0 = (const char *)d_in, *o0 = (const char *)d_out;
+  if (batch > 0 && plan->n > 0 && i0 < o0 + 2 * in_bytes && o0 < i0 + in_bytes)
+    return fail(GDSP_ERR_INVALID, "real input overlaps the complex output");
+  return exec_plan(plan, d_in, (cd *)d_out, batch, inverse != 0, gdsp::LOAD_REAL,
+                   (hipStream_t)stream);
+}
+
 int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, int64_t pad,
                                   int64_t noverlap, int64_t seg_begin, int64_t seg_end,
                                   const double *d_win_seg, double *d_acc, void *stream) {

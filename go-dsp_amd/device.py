@@ -86,6 +86,23 @@ def fft_batch(x, out=None, inverse: bool = False, stream=None, chirpz: bool = Fa
     return out
 
 
+def fft_real_batch(x, out=None, inverse: bool = False, stream=None, chirpz: bool = False):
+    """fft.FFTReal / IFFTReal of the rows of a (batch, n) float64 CUDA tensor
+    into a complex128 tensor (gdsp_fft_real_batch_device: the kernels read the
+    real rows themselves)."""
+    torch = _torch()
+    assert x.is_cuda and x.dtype == torch.float64 and x.dim() == 2 and x.is_contiguous()
+    if out is None:
+        out = torch.empty(x.shape, dtype=torch.complex128, device=x.device)
+    assert out.shape == x.shape and out.dtype == torch.complex128 and out.is_contiguous()
+    with torch.cuda.device(x.device):
+        p = plan(x.shape[1], chirpz)
+        check(lib().gdsp_fft_real_batch_device(p.handle, _ptr(x), _ptr(out), x.shape[0],
+                                               int(inverse), _stream_ptr(stream, x.device)),
+              "fft_real_batch_device")
+    return out
+
+
 def fft2(x, out=None, inverse: bool = False, work=None, stream=None):
     """FFT2/IFFT2 of a (rows, cols) complex128 CUDA tensor."""
     torch = _torch()

@@ -275,6 +275,13 @@ int gdsp_plan_parts(const gdsp_plan *plan);
 int gdsp_fft_batch_device(const gdsp_plan *plan, const void *d_in, void *d_out,
                           int64_t batch, int inverse, void *stream);
 
+/* fft.FFTReal / fft.IFFTReal — fft/fft.go:25-32 — over `batch` device rows:
+ * d_in holds batch*n float64 (read as they are: no ToComplex copy), d_out
+ * batch*n complex128 and must not overlap d_in. inverse != 0 → IFFTReal
+ * semantics (an empty plan is then GDSP_ERR_EMPTY, like IFFT). */
+int gdsp_fft_real_batch_device(const gdsp_plan *plan, const double *d_in, void *d_out,
+                               int64_t batch, int inverse, void *stream);
+
 /* FFT2/IFFT2 on a device rows×cols complex128 matrix. d_work: scratch of
  * rows*cols complex128 (may be NULL: the library allocates stream-ordered). */
 int gdsp_fft2_device(const void *d_in, void *d_out, int64_t rows, int64_t cols,
