@@ -52,7 +52,11 @@ SQ_KERNELS = {"radix4096": ["fft_lds_kernel<12"], "bluestein3000": ["fft_mixed_f
               "chirpz3000": ["chirpz6k_kernel"], "pwelch": ["pwelch_row_kernel<12"],
               "fft2_8192": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"],
               "fft2_dist": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"]}
-SQ_ROUNDS = ("r03", "r02")  # SQ counter passes quoted: the newest round that has the kernel
+SQ_ROUNDS = ("r04", "r03", "r02")  # SQ counter passes quoted: the newest round that has the kernel
+# rocprofv3 --kernel-trace --stats summaries quoted beside the event timing
+# (profiles/<round>/<workload>_kernel_stats.csv, the closing session's runs of
+# `bench.py --workload <w>`): the newest round that has the workload
+STATS_ROUNDS = ("r04", "r03", "r02")
 SEED = 0x5EED
 # algorithmic bytes of one launch in the N=1 full-size configuration the
 # committed PMC (profiles/pmc_*.json) and SQ (profiles/r02/sq_counters.json)
@@ -549,7 +553,8 @@ def run(w: str, c: Ctx, weak: bool = False) -> dict:
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "frac_vs_copy": round(achieved / HBM_COPY_GBS, 4),
                      "avg_launch_ms": round(avg_launch_s * 1e3, 4),
-                     "alg_bytes_per_launch": wl["alg_bytes"], "traffic": traffic},
+                     "alg_bytes_per_launch": wl["alg_bytes"], "traffic": traffic,
+                     "rocprof": rocprof_info(w, wl["alg_bytes"], share)},
         "fp64": fp64_info(w, avg_launch_s, share),
         "cpu_baseline": None,  # filled in by main() after every GPU measurement
         "parity": check,
@@ -750,6 +755,42 @@ def fp64_info(workload: str, launch_s: float, share: float = 1.0):
         return {"flop_per_launch": flop, "achieved_tflops": round(tf, 2),
                 "peak_tflops": FP64_PEAK_TFLOPS, "frac": round(tf / FP64_PEAK_TFLOPS, 4),
                 "source": f"profiles/{rnd}/sq_counters.json (SQ_INSTS_VALU_{{FMA,ADD,MUL}}_F64)"}
+    return None
+
+
+def rocprof_info(workload: str, alg_bytes: int, share: float = 1.0):
+    """The dominant kernel's duration from the committed rocprofv3
+    --kernel-trace --stats summary of this workload (newest round; FFT2: its
+    launches summed), and roofline.frac recomputed from that average: the
+    profiler's figure quoted beside the HIP-event one. The summary was taken
+    at the N=1 full-size configuration; share scales it to this launch."""
+    w = "fft2_8192" if workload == "fft2_dist" else workload
+    ks = SQ_KERNELS.get(w)
+    if not ks:
+        return None
+    import csv
+    for rnd in STATS_ROUNDS:
+        path = os.path.join(REPO, "profiles", rnd, f"{w}_kernel_stats.csv")
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            rows = list(csv.DictReader(f))
+        avg = mn = 0.0
+        calls = []
+        for k in ks:
+            hit = [r for r in rows if k in r["Name"]]
+            if not hit:
+                break
+            r = max(hit, key=lambda r: int(r["Calls"]))  # the timed template
+            avg += float(r["AverageNs"])
+            mn += float(r["MinNs"])
+            calls.append(int(r["Calls"]))
+        else:
+            avg_s = avg * 1e-9 * share
+            ach = alg_bytes / avg_s / 1e9
+            return {"avg_launch_ms": round(avg_s * 1e3, 4), "min_launch_ms": round(mn * 1e-6 * share, 4),
+                    "calls": calls, "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                    "source": f"profiles/{rnd}/{w}_kernel_stats.csv"}
     return None
 
 

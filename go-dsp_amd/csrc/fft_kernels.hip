@@ -1101,6 +1101,10 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
       // GDSP_PW_SHFL=1) and round 2's pwelch_half_kernel (GDSP_PW_HALF=1)
       if (const char *e = dev_switch("GDSP_PW_SHFL"); e && e[0] == '1')
         return launch_pwelch4096_shfl(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
+      // round-4 occupancy variants (pwelch_rowx.hip; the Hann ones ignore win)
+      if (const char *e = dev_switch("GDSP_PW_ROWX"); e && e[0] >= '1' && e[0] <= '9')
+        return launch_pwelch_rowx4096(e[0] - '0', x, seg_begin, seg_end, ppw, nworkers, win, tw,
+                                      partial, s);
       if (const char *e = dev_switch("GDSP_PW_HALF"); e && e[0] == '1')
         return launch_pwh_t<12, 2, 1, 4, true, true>(x, seg_begin, seg_end, ppw, nworkers, win, tw,
                                                      partial, s);

@@ -136,6 +136,13 @@ hipError_t launch_pwelch(int log2f, const double *x, int64_t nfft, int64_t strid
 hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int64_t seg_end,
                               int64_t ppw, int64_t nworkers, const double *win, const cd *tw,
                               double *partial, hipStream_t s);
+#ifdef GDSP_DEV_BUILD
+// round-4 occupancy variants of the row kernel (pwelch_rowx.hip, dev build)
+hipError_t launch_pwelch_rowx4096(int variant, const double *x, int64_t seg_begin,
+                                  int64_t seg_end, int64_t ppw, int64_t nworkers,
+                                  const double *win, const cd *tw, double *partial,
+                                  hipStream_t s);
+#endif
 // the row kernel (pwelch_row.hip) behind launch_pwelch_half(12, ...)
 hipError_t launch_pwelch_row4096(const double *x, int64_t seg_begin, int64_t seg_end, int64_t ppw,
                                  int64_t nworkers, const double *win, const cd *tw,
