@@ -30,6 +30,9 @@
 #include "launch.hpp"
 #include "mixed_core.hpp"
 
+#ifndef GDSP_C6_TOUCH
+#define GDSP_C6_TOUCH 1
+#endif
 namespace gdsp {
 
 // (kernel and helpers outside an anonymous namespace, so profiler kernel
@@ -132,7 +135,7 @@ __device__ __forceinline__ void c6_twiddle(cd (&v)[R], cd w) {
 // postmultiply and store (issue: the loads, apply: the arithmetic). Issued
 // before the pass-C twiddles or the last exchange's reads instead, the loads
 // push the kernel past 128 VGPRs into spills: 2.43 against 2.37 ms.
-template <int RB>
+template <int RB, int ABL = 0>
 struct C6Bhat {
   using G = C6Geo<RB>;
   rsrc_t rb;
@@ -140,14 +143,15 @@ struct C6Bhat {
   cd f[16];
   __device__ __forceinline__ void issue() {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) f[r] = buf_ld(rb, off + (uint32_t)(r * G::NA * 16));
+    for (int r = 0; r < 16; ++r)
+      f[r] = (ABL & 2) ? cd{1.0 + 1e-3 * r, (double)off * 1e-9} : buf_ld(rb, off + (uint32_t)(r * G::NA * 16));
   }
   __device__ __forceinline__ void apply(cd (&v)[16]) const {
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = conjg(cmul(v[r], f[r]));
   }
 };
-template <int RB, int KN, bool INV>
+template <int RB, int KN, bool INV, int ABL = 0>
 struct C6Out {
   using G = C6Geo<RB>;
   rsrc_t rch, rout;
@@ -156,7 +160,8 @@ struct C6Out {
   cd f[KN];
   __device__ __forceinline__ void issue() {
 #pragma unroll
-    for (int r = 0; r < KN; ++r) f[r] = buf_ld(rch, off + (uint32_t)(r * G::NA * 16));
+    for (int r = 0; r < KN; ++r)
+      f[r] = (ABL & 4) ? cd{1.0 - 1e-3 * r, (double)off * 1e-9} : buf_ld(rch, off + (uint32_t)(r * G::NA * 16));
   }
   __device__ __forceinline__ void apply(cd (&v)[16]) const {
 #pragma unroll
@@ -174,7 +179,14 @@ struct C6Out {
 // twiddle bases, W_{16 RB}^k (k < 16, pass B) then W_M^k (k < NA, pass C).
 // Threads t >= NA (M = 6144: none) sit out passes A and C, threads t >= 256
 // (M = 3072: none) pass B; all take part in the barriers.
-template <int RB, int ZIN, class EPI>
+// ABL (development ablations, results wrong): bit 3 drops the exchanges'
+// barriers (a race, timing only)
+template <int ABL>
+__device__ __forceinline__ void c6_sync() {
+  if constexpr (!(ABL & 8)) __syncthreads();
+}
+
+template <int RB, int ZIN, class EPI, int ABL = 0>
 __device__ __forceinline__ void c6_fft(cd (&v)[16], int t, const cd *__restrict__ tw, double *lds,
                                        bool first, EPI &epi) {
   using G = C6Geo<RB>;
@@ -191,22 +203,22 @@ __device__ __forceinline__ void c6_fft(cd (&v)[16], int t, const cd *__restrict_
   const int wa = 16 * t, ma = t & 15;
   const int ra = t ^ ((t >> 4) & 15);
   cd u[RB];
-  if (!first) __syncthreads();
+  if (!first) c6_sync<ABL>();
   if (pa) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) lds[wa + (r ^ ma)] = v[r].x;
   }
-  __syncthreads();
+  c6_sync<ABL>();
   if (pb) {
 #pragma unroll
     for (int r = 0; r < RB; ++r) u[r].x = lds[ra + kC6B * r];
   }
-  __syncthreads();
+  c6_sync<ABL>();
   if (pa) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) lds[wa + (r ^ ma)] = v[r].y;
   }
-  __syncthreads();
+  c6_sync<ABL>();
   // pass B
   const int wbo = (t >> 4) * (16 * RB) + (t & 15);
   if (pb) {
@@ -215,23 +227,23 @@ __device__ __forceinline__ void c6_fft(cd (&v)[16], int t, const cd *__restrict_
     c6_twiddle<RB>(u, tw[t & 15]);
     dft3x<RB>(u);
   }
-  __syncthreads();
+  c6_sync<ABL>();
   // exchange 2: write (t / 16) 16 RB + t % 16 + 16 r, read t + NA r
   if (pb) {
 #pragma unroll
     for (int r = 0; r < RB; ++r) lds[wbo + 16 * r] = u[r].x;
   }
-  __syncthreads();
+  c6_sync<ABL>();
   if (pa) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r].x = lds[t + G::NA * r];
   }
-  __syncthreads();
+  c6_sync<ABL>();
   if (pb) {
 #pragma unroll
     for (int r = 0; r < RB; ++r) lds[wbo + 16 * r] = u[r].y;
   }
-  __syncthreads();
+  c6_sync<ABL>();
   if (pa) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r].y = lds[t + G::NA * r];
@@ -252,33 +264,54 @@ __device__ __forceinline__ void c6_fft(cd (&v)[16], int t, const cd *__restrict_
 // KN: n <= NA KN (inputs and wanted outputs at r < KN)
 // REAL: float64 input rows (fft.FFTReal, fft/fft.go:25-27), read directly
 // (no complex copy of the input first)
-template <int RB, bool INV, int KN, bool REAL = false>
-__global__ __launch_bounds__(C6Geo<RB>::T) __attribute__((amdgpu_waves_per_eu(RB == 24 ? 4 : 3))) void chirpz6k_kernel(
-    const void *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
-    const cd *__restrict__ tw, const cd *__restrict__ chirp, const cd *__restrict__ bhat,
-    double scale) {
+// ABL: development ablations (timing only, results wrong; 0 in the product):
+// 1 = x and chirp premultiply loads replaced by constants, 2 = bhat loads,
+// 4 = the output chirp loads, 8 = no exchange barriers, 16 = x only, 32 = the
+// premultiply chirp only
+//
+// One transform (row g) of the workgroup: premultiply, FFT 1, bhat, FFT 2,
+// postmultiply and store. first: no exchange of this workgroup precedes it.
+// touch (persistent kernel): the next row's bytes, one 128-B line per thread,
+// loaded into L2 right after this row's loads issue (its result is held in one
+// register to the end of the transform, so no wait ever lands on it early).
+template <int RB, bool INV, int KN, bool REAL, int ABL>
+__device__ __forceinline__ void c6_transform(const void *__restrict__ in, cd *__restrict__ out,
+                                             int64_t n, int64_t g, int t, const cd *tw,
+                                             const cd *chirp, const cd *bhat, double scale,
+                                             double *lds, bool first, int64_t touch_row) {
   using G = C6Geo<RB>;
-  static_assert(KN >= 1 && KN <= 8, "n <= M/2");
-  __shared__ double lds[G::M];
-  const int t = (int)threadIdx.x;
-  const int64_t g = xcd_remap(blockIdx.x, gridDim.x);
-  if (g >= batch) return;  // (grid = batch: never taken)
   const uint32_t off = (uint32_t)t * 16u;
   const int64_t rowb = n * 16;
+  const int64_t inb = REAL ? n * 8 : rowb;
   cd v[16];
+  unsigned touched = 0u;
   if (G::NA == G::T || t < G::NA) {
     const rsrc_t rin =
-        REAL ? make_rsrc(static_cast<const double *>(in) + g * n, n * 8)
-             : make_rsrc(static_cast<const cd *>(in) + g * n, rowb);
+        make_rsrc(static_cast<const char *>(in) + g * inb, inb);
     const rsrc_t rch = make_rsrc(chirp, rowb);
     cd xv[KN], cv[KN];
 #pragma unroll
     for (int r = 0; r < KN; ++r) {
-      if constexpr (REAL)
-        xv[r] = {buf_ld1(rin, (uint32_t)t * 8u + (uint32_t)(r * G::NA * 8)), 0.0};
-      else
+      if constexpr (ABL & 1) {
+        xv[r] = {(double)(off + r) * 1e-7, (double)g * 1e-9};
+        cv[r] = {1.0 - 1e-4 * r, 1e-5 * r};
+      } else if constexpr (ABL & 16) {
+        xv[r] = {(double)(off + r) * 1e-7, (double)g * 1e-9};
+        cv[r] = buf_ld(rch, off + (uint32_t)(r * G::NA * 16));
+      } else if constexpr (ABL & 32) {
         xv[r] = buf_ld(rin, off + (uint32_t)(r * G::NA * 16));
-      cv[r] = buf_ld(rch, off + (uint32_t)(r * G::NA * 16));
+        cv[r] = {1.0 - 1e-4 * r, 1e-5 * r};
+      } else {
+        if constexpr (REAL)
+          xv[r] = {buf_ld1(rin, (uint32_t)t * 8u + (uint32_t)(r * G::NA * 8)), 0.0};
+        else
+          xv[r] = buf_ld(rin, off + (uint32_t)(r * G::NA * 16));
+        cv[r] = buf_ld(rch, off + (uint32_t)(r * G::NA * 16));
+      }
+    }
+    if (touch_row >= 0) {
+      const rsrc_t rnx = make_rsrc(static_cast<const char *>(in) + touch_row * inb, inb);
+      touched = __builtin_amdgcn_raw_buffer_load_b32(rnx, (uint32_t)t * 128u, 0, 0);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -291,14 +324,61 @@ __global__ __launch_bounds__(C6Geo<RB>::T) __attribute__((amdgpu_waves_per_eu(RB
       }
     }
   }
-  C6Bhat<RB> be{make_rsrc(bhat, (int64_t)G::M * 16), off, {}};
-  c6_fft<RB, KN>(v, t, tw, lds, true, be);
+  C6Bhat<RB, ABL> be{make_rsrc(bhat, (int64_t)G::M * 16), off, {}};
+  c6_fft<RB, KN, C6Bhat<RB, ABL>, ABL>(v, t, tw, lds, first, be);
   // the second FFT must not share the first one's addresses (opaque copies:
   // otherwise the compiler keeps them live across both)
   const int t2 = opaque_int(t);
-  C6Out<RB, KN, INV> oe{make_rsrc(opaque_ptr(chirp), rowb), make_rsrc(out + g * n, rowb),
-                        (uint32_t)t2 * 16u, scale, {}};
-  c6_fft<RB, 0>(v, t2, opaque_ptr(tw), lds, false, oe);
+  C6Out<RB, KN, INV, ABL> oe{make_rsrc(opaque_ptr(chirp), rowb), make_rsrc(out + g * n, rowb),
+                             (uint32_t)t2 * 16u, scale, {}};
+  c6_fft<RB, 0, C6Out<RB, KN, INV, ABL>, ABL>(v, t2, opaque_ptr(tw), lds, false, oe);
+  if (touch_row >= 0) asm volatile("" ::"v"(touched));
+}
+
+// TA: touch into L2 the row of the block TA places later in dispatch order
+// (the same XCD when TA is a multiple of 8; it should start after this block
+// ends, so TA >= the resident blocks, 2 per CU)
+template <int RB, bool INV, int KN, bool REAL = false, int ABL = 0, int TA = 0>
+__global__ __launch_bounds__(C6Geo<RB>::T) __attribute__((amdgpu_waves_per_eu(RB == 24 ? 4 : 3))) void chirpz6k_kernel(
+    const void *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
+    const cd *__restrict__ tw, const cd *__restrict__ chirp, const cd *__restrict__ bhat,
+    double scale) {
+  using G = C6Geo<RB>;
+  static_assert(KN >= 1 && KN <= 8, "n <= M/2");
+  __shared__ double lds[G::M];
+  const int64_t g = xcd_remap(blockIdx.x, gridDim.x);
+  if (g >= batch) return;  // (grid = batch: never taken)
+  int64_t touch = -1;
+  if constexpr (TA > 0) {
+    const int64_t bn = (int64_t)blockIdx.x + TA;
+    if (bn < (int64_t)gridDim.x) touch = xcd_remap(bn, gridDim.x);
+  }
+  c6_transform<RB, INV, KN, REAL, ABL>(in, out, n, g, (int)threadIdx.x, tw, chirp, bhat, scale,
+                                       lds, true, touch);
+}
+
+// Persistent form: one workgroup per resident slot, each over a contiguous
+// run of rows, touching its next row into L2 while the current one runs (the
+// one-transform-per-workgroup kernel waits on each row's HBM loads with
+// nothing else to do: 16 % of its time, profiles/r04/chirpz6k_ablation.txt).
+template <int RB, bool INV, int KN, bool REAL = false>
+__global__ __launch_bounds__(C6Geo<RB>::T) __attribute__((amdgpu_waves_per_eu(RB == 24 ? 4 : 3))) void chirpz6k_persist_kernel(
+    const void *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
+    int64_t rows_per_wg, const cd *__restrict__ tw, const cd *__restrict__ chirp,
+    const cd *__restrict__ bhat, double scale) {
+  using G = C6Geo<RB>;
+  static_assert(KN >= 1 && KN <= 8, "n <= M/2");
+  __shared__ double lds[G::M];
+  const int64_t g0 = (int64_t)blockIdx.x * rows_per_wg;
+  const int64_t g1 = g0 + rows_per_wg < batch ? g0 + rows_per_wg : batch;
+  for (int64_t g = g0; g < g1; ++g) {
+    // laundered per row: nothing address-like is hoisted out of the loop and
+    // kept live across it (the compiler would, 59 spilled VGPRs at 128)
+    c6_transform<RB, INV, KN, REAL, 0>(opaque_ptr(in), opaque_ptr(out), n, g,
+                                       opaque_int((int)threadIdx.x), opaque_ptr(tw),
+                                       opaque_ptr(chirp), opaque_ptr(bhat), scale, lds, g == g0,
+                                       GDSP_C6_TOUCH ? (g + 1 < g1 ? g + 1 : -1) : -1);
+  }
 }
 
 // The convolution length for n (0: neither size applies)
@@ -313,6 +393,64 @@ static hipError_t launch_c6(bool inv, int load, const void *in, cd *out, int64_t
                             const cd *tw, const cd *chirp, const cd *bhat, double scale,
                             hipStream_t s) {
   const dim3 grid((unsigned)batch), block(C6Geo<RB>::T);
+#ifdef GDSP_DEV_BUILD
+  if constexpr (RB == 24) {
+    // ablation timings (GDSP_C6_ABL = 1..15, forward complex only; wrong results)
+    if (const char *e = dev_switch("GDSP_C6_ABL"); e && !inv && load != LOAD_REAL) {
+      switch (atoi(e)) {
+#define GDSP_C6A(A)                                                                              \
+  case A:                                                                                        \
+    hipLaunchKernelGGL((chirpz6k_kernel<24, false, 8, false, A>), grid, block, 0, s, in, out, n, \
+                       batch, tw, chirp, bhat, scale);                                           \
+    return hipGetLastError();
+        GDSP_C6A(1) GDSP_C6A(2) GDSP_C6A(4) GDSP_C6A(7) GDSP_C6A(8) GDSP_C6A(15) GDSP_C6A(16) GDSP_C6A(32)
+#undef GDSP_C6A
+        default: break;
+      }
+    }
+  }
+#endif
+#ifdef GDSP_DEV_BUILD
+  if (const char *e = dev_switch("GDSP_C6_TA"); e && !inv && load != LOAD_REAL) {
+    switch (atoi(e)) {
+#define GDSP_C6T(D)                                                                             \
+  case D:                                                                                       \
+    hipLaunchKernelGGL((chirpz6k_kernel<RB, false, 8, false, 0, D>), grid, block, 0, s, in, out, \
+                       n, batch, tw, chirp, bhat, scale);                                       \
+    return hipGetLastError();
+      GDSP_C6T(256) GDSP_C6T(512) GDSP_C6T(768) GDSP_C6T(1024) GDSP_C6T(2048)
+#undef GDSP_C6T
+      default: break;
+    }
+  }
+  if (const char *e = dev_switch("GDSP_C6_PERSIST"); e && e[0] == '1') {
+    // one workgroup per resident slot (occupancy x CUs of the current device)
+    static int slots_per_cu = 0, cus = 0;
+    if (!slots_per_cu) {
+      int dev = 0, nb = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &nb, reinterpret_cast<const void *>(&chirpz6k_persist_kernel<RB, false, 8>),
+          C6Geo<RB>::T, 0);
+      slots_per_cu = nb > 0 ? nb : 1;
+    }
+    const int64_t slots = (int64_t)slots_per_cu * (cus > 0 ? cus : 1);
+    const int64_t nwg = batch < slots ? batch : slots;
+    const int64_t rpw = (batch + nwg - 1) / nwg;
+    const dim3 pg((unsigned)((batch + rpw - 1) / rpw));
+    if (load == LOAD_REAL)
+      hipLaunchKernelGGL((chirpz6k_persist_kernel<RB, false, 8, true>), pg, block, 0, s, in, out, n,
+                         batch, rpw, tw, chirp, bhat, scale);
+    else if (inv)
+      hipLaunchKernelGGL((chirpz6k_persist_kernel<RB, true, 8>), pg, block, 0, s, in, out, n,
+                         batch, rpw, tw, chirp, bhat, scale);
+    else
+      hipLaunchKernelGGL((chirpz6k_persist_kernel<RB, false, 8>), pg, block, 0, s, in, out, n,
+                         batch, rpw, tw, chirp, bhat, scale);
+    return hipGetLastError();
+  }
+#endif
   if (load == LOAD_REAL)
     hipLaunchKernelGGL((chirpz6k_kernel<RB, false, 8, true>), grid, block, 0, s, in, out, n, batch,
                        tw, chirp, bhat, scale);

@@ -33,7 +33,9 @@ struct HannRec {
 // PREF: the next pair's samples loaded into registers during this pair
 // NOCARRY: no samples kept across pairs: each pair loads its 3 rows-blocks
 // (the first one an L2 hit: the previous pair's last block) at its start
-template <int LOG2F, int WIN, bool PREF, int WPE, bool NOCARRY = false>
+// SPLIT: real and imaginary parts through one N-double buffer in turn (four
+// barriers per exchange); false: two buffers, two barriers per exchange
+template <int LOG2F, int WIN, bool PREF, int WPE, bool NOCARRY = false, bool SPLIT = true>
 __global__ __launch_bounds__((Geo<LOG2F, 4>::WG)) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 void pwelch_rowx_kernel(const double *__restrict__ x, int64_t seg_begin, int64_t seg_end,
                         int64_t pairs_per_worker, const double *__restrict__ win,
@@ -42,9 +44,11 @@ void pwelch_rowx_kernel(const double *__restrict__ x, int64_t seg_begin, int64_t
   static_assert(G::TPW == 1, "one worker per workgroup");
   constexpr int E = G::E, H = E / 2, T = G::T;
   constexpr int64_t STRIDE = G::N / 2;
-  __shared__ double lds[G::LDS_DOUBLES + (WIN == 0 ? G::N : 0)];
+  constexpr int XD = SPLIT ? G::LDS_DOUBLES : 2 * G::LDS_DOUBLES;
+  __shared__ double lds[XD + (WIN == 0 ? G::N : 0)];
   double *const lx = lds;
-  double *const wl = lds + G::LDS_DOUBLES;
+  double *const ly = SPLIT ? lds : lds + G::LDS_DOUBLES;
+  double *const wl = lds + XD;
   const int t = threadIdx.x;
   const uint32_t lane = (uint32_t)t;
   HannRec hr{};
@@ -128,7 +132,7 @@ void pwelch_rowx_kernel(const double *__restrict__ x, int64_t seg_begin, int64_t
     }
 #pragma unroll
     for (int k = 0; k < E; ++k) v[k] = {v[k].x * wv[k], v[k].y * wv[k]};
-    fft_regs<LOG2F, true, 2, 4, 0, 0, RT, 2, false, NoEpi, 0, 16>(v, tt, rl, lx, lx, first);
+    fft_regs<LOG2F, SPLIT, 2, 4, 0, 0, RT, 2, false, NoEpi, 0, 16>(v, tt, rl, lx, ly, first);
 #pragma unroll
     for (int k = 0; k < E; ++k) acc[k] = fma(v[k].y, v[k].y, fma(v[k].x, v[k].x, acc[k]));
   };
@@ -140,11 +144,11 @@ void pwelch_rowx_kernel(const double *__restrict__ x, int64_t seg_begin, int64_t
   for (int k = 0; k < E; ++k) dst[t + k * T] = acc[k];
 }
 
-template <int WIN, bool PREF, int WPE, bool NOCARRY = false>
+template <int WIN, bool PREF, int WPE, bool NOCARRY = false, bool SPLIT = true>
 hipError_t launch_rowx(const double *x, int64_t seg_begin, int64_t seg_end, int64_t ppw,
                        int64_t nworkers, const double *win, const cd *tw, double *partial,
                        hipStream_t s) {
-  hipLaunchKernelGGL((pwelch_rowx_kernel<12, WIN, PREF, WPE, NOCARRY>), dim3((unsigned)nworkers),
+  hipLaunchKernelGGL((pwelch_rowx_kernel<12, WIN, PREF, WPE, NOCARRY, SPLIT>), dim3((unsigned)nworkers),
                      dim3(Geo<12>::WG), 0, s, x, seg_begin, seg_end, ppw, win, tw, partial);
   return hipGetLastError();
 }
@@ -152,7 +156,8 @@ hipError_t launch_rowx(const double *x, int64_t seg_begin, int64_t seg_end, int6
 // variant: 1 = Hann in registers + prefetch, 2 waves; 2 = Hann in registers,
 // no prefetch, 3 waves; 3 = LDS window, no prefetch, 2 waves; 4 = Hann in
 // registers + prefetch, 3 waves; 5 / 6 = Hann in registers, no carry, no
-// prefetch, 3 / 2 waves; 7 = LDS window, no carry, no prefetch, 2 waves
+// prefetch, 3 / 2 waves; 7 = LDS window, no carry, no prefetch, 2 waves;
+// 8 = Hann in registers + prefetch, two exchange buffers, 2 waves
 hipError_t launch_pwelch_rowx4096(int variant, const double *x, int64_t seg_begin,
                                   int64_t seg_end, int64_t ppw, int64_t nworkers,
                                   const double *win, const cd *tw, double *partial,
@@ -165,6 +170,7 @@ hipError_t launch_pwelch_rowx4096(int variant, const double *x, int64_t seg_begi
     case 5: return launch_rowx<1, false, 3, true>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
     case 6: return launch_rowx<1, false, 2, true>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
     case 7: return launch_rowx<0, false, 2, true>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
+    case 8: return launch_rowx<1, true, 2, false, false>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
   }
   return hipErrorInvalidValue;
 }
