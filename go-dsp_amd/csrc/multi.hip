@@ -139,9 +139,12 @@ int resolve(const int *devices, int ndev, std::vector<int> &out, bool *configure
 
 // ---- persistent per-shard host workers ----------------------------------------
 
-// Worker i runs shard i of every multi-device call. Workers persist, so their
-// thread-local streams and pinned staging buffers are built once. One
-// multi-device call runs at a time (calls from several host threads queue).
+// One persistent worker per (device, occurrence): the k-th time a device
+// appears in a call's device list, that shard runs on worker (device, k).
+// Workers persist, so their thread-local streams and pinned staging buffers
+// are built once. A call holds the workers it uses for its whole duration
+// (accumulate, collective, copy back), taken in one global order, so calls on
+// disjoint device sets run concurrently and calls sharing a device queue.
 class Pool {
  public:
   static Pool &get() {
@@ -149,27 +152,44 @@ class Pool {
     return *p;
   }
 
-  // f(i) on worker i for i < n, concurrently; the first failing shard's
-  // status and message become the caller's. When every shard succeeded,
-  // after() runs on the calling thread while the call still holds the pool
-  // (the collective step of a call: no other multi-device call can touch
-  // the workers' streams or an RCCL clique in between).
-  int run(int n, const std::function<int(int)> &f,
+  // f(i) for shard i of devs (on worker (devs[i], occurrence)), concurrently;
+  // the first failing shard's status and message become the caller's. When
+  // every shard succeeded, after() runs on the calling thread while the call
+  // still holds its workers (the collective step: no other call can touch
+  // their streams or this device set's RCCL clique in between).
+  int run(const std::vector<int> &devs, const std::function<int(int)> &f,
           const std::function<int()> &after = nullptr) {
-    std::lock_guard<std::mutex> call(run_mu_);
-    while ((int)ws_.size() < n) {
-      ws_.emplace_back(new W);
-      W *w = ws_.back().get();
-      try {
-        w->th = std::thread([w] { loop(w); });
-        w->th.detach();
-      } catch (...) {
-        ws_.pop_back();
-        return set_error(GDSP_ERR_NOMEM, "cannot start a device worker thread");
+    const int n = (int)devs.size();
+    std::vector<W *> ws((size_t)n, nullptr);
+    {
+      std::lock_guard<std::mutex> lk(map_mu_);
+      std::map<int, int> seen;
+      for (int i = 0; i < n; ++i) {
+        const std::pair<int, int> key(devs[i], seen[devs[i]]++);
+        auto it = ws_.find(key);
+        if (it == ws_.end()) {
+          std::unique_ptr<W> w(new W);
+          W *wp = w.get();
+          try {
+            wp->th = std::thread([wp] { loop(wp); });
+            wp->th.detach();
+          } catch (...) {
+            return set_error(GDSP_ERR_NOMEM, "cannot start a device worker thread");
+          }
+          wp->key = key;
+          it = ws_.emplace(key, std::move(w)).first;
+        }
+        ws[(size_t)i] = it->second.get();
       }
     }
+    // the workers' call locks in one global order (map order = key order)
+    std::vector<W *> order(ws);
+    std::sort(order.begin(), order.end(), [](W *a, W *b) { return a->key < b->key; });
+    std::vector<std::unique_lock<std::mutex>> held;
+    held.reserve(order.size());
+    for (W *w : order) held.emplace_back(w->call_mu);
     for (int i = 0; i < n; ++i) {
-      W *w = ws_[i].get();
+      W *w = ws[(size_t)i];
       std::lock_guard<std::mutex> lk(w->mu);
       w->f = &f;
       w->idx = i;
@@ -179,7 +199,7 @@ class Pool {
     int st = GDSP_OK;
     std::string msg;
     for (int i = 0; i < n; ++i) {
-      W *w = ws_[i].get();
+      W *w = ws[(size_t)i];
       std::unique_lock<std::mutex> lk(w->mu);
       w->cv.wait(lk, [w] { return !w->busy; });
       if (st == GDSP_OK && w->st != GDSP_OK) {
@@ -198,7 +218,9 @@ class Pool {
 
  private:
   struct W {
+    std::pair<int, int> key;
     std::thread th;
+    std::mutex call_mu;  // held by the call using this worker
     std::mutex mu;
     std::condition_variable cv;
     const std::function<int(int)> *f = nullptr;
@@ -230,8 +252,8 @@ class Pool {
     }
   }
 
-  std::mutex run_mu_;
-  std::vector<std::unique_ptr<W>> ws_;
+  std::mutex map_mu_;
+  std::map<std::pair<int, int>, std::unique_ptr<W>> ws_;
 };
 
 // ---- RCCL (dlopen) ----------------------------------------------------------------
@@ -362,7 +384,8 @@ int fft_batch_multi(const void *x, size_t in_elem_bytes, double *out, int64_t n,
   if (!x || !out) return set_error(GDSP_ERR_INVALID, "NULL pointer");
   const int parts = (int)std::min<int64_t>((int64_t)devs.size(), batch);
   ++g_batch_calls;
-  return Pool::get().run(parts, [&](int i) -> int {
+  const std::vector<int> used(devs.begin(), devs.begin() + parts);
+  return Pool::get().run(used, [&](int i) -> int {
     int64_t lo, hi;
     shard(batch, parts, i, &lo, &hi);
     MHIPCHK(hipSetDevice(devs[i]));
@@ -520,10 +543,11 @@ int pwelch_multi(const double *x, int64_t n, double fs, int64_t nfft, int64_t pa
       reduced_by_rccl = true;
       return GDSP_OK;
     };
-    // one Pool::run holds the whole call (accumulate, reduce, copy back), so
-    // concurrent calls from other host threads queue behind it and never
-    // share its accumulators, streams or clique
-    MSTCHK(Pool::get().run(D, accumulate, use_rccl ? std::function<int()>(reduce) : nullptr));
+    // one Pool::run holds the call's workers for the whole call (accumulate,
+    // reduce, copy back): a concurrent call on an overlapping device set
+    // queues behind it and never shares its accumulators, streams or clique;
+    // one on a disjoint set runs beside it
+    MSTCHK(Pool::get().run(devs, accumulate, use_rccl ? std::function<int()>(reduce) : nullptr));
     if (reduced_by_rccl) {
       acc.swap(part[0]);
       ++g_rccl_reduces;
