@@ -487,6 +487,11 @@ def run_fftreal1024(c: Ctx) -> dict:
         "fp64": None,
         "cpu_baseline": None,
         "parity": check,
+        "drop_in_policy": {
+            "gpu_min_n": 4096, "source": "go/fft/fft_gpu.go (GPUMinN)",
+            "note": "a one-vector fft.FFTReal shorter than GPUMinN stays on the reference's own "
+                    "pure-Go radix2FFT/bluesteinFFT in the drop-in (this line times the GPU call "
+                    "itself); small_n.first_n_gpu_faster is where the GPU call wins"},
     }
 
 
