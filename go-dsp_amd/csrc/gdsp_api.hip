@@ -669,6 +669,27 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   }
   std::vector<int> rad;
   int fr[16], fnp = 0;
+#ifdef GDSP_DEV_BUILD
+  // experiment: GDSP_JIT_RADICES="10,15,20" compiles that radix list (hipRTC)
+  // for the n it multiplies to, compiled specialisation or not
+  if (const char *e = gdsp::dev_switch("GDSP_JIT_RADICES"); e && !chirpz && gdsp::jit_enabled()) {
+    int jr[5], jnp = 0;
+    int64_t prod = 1;
+    for (const char *q = e; *q && jnp < 5;) {
+      char *end = nullptr;
+      const long v = strtol(q, &end, 10);
+      if (end == q) break;
+      jr[jnp++] = (int)v;
+      prod *= v;
+      q = *end == ',' ? end + 1 : end;
+    }
+    if (jnp >= 2 && prod == n)
+      if (gdsp::JitSpec *j = gdsp::jit_spec_build(dev, jr, jnp, (int)n)) {
+        p->jit = j;
+        return build_mixed(dev, n, std::vector<int>(jr, jr + jnp), p);
+      }
+  }
+#endif
   if (!chirpz && n <= gdsp::kMixedSpecMax && !gdsp::mixed_fixed_radices((int)n, fr, &fnp) &&
       gdsp::jit_enabled()) {
     // smooth length without a compiled specialisation: compile one (hipRTC);
