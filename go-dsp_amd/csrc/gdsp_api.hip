@@ -670,7 +670,7 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   std::vector<int> rad;
   int fr[16], fnp = 0;
 #ifdef GDSP_DEV_BUILD
-  // experiment: GDSP_JIT_RADICES="10,15,20" compiles that radix list (hipRTC)
+  // experiment: GDSP_JIT_RADICES="10x15x20" compiles that radix list (hipRTC)
   // for the n it multiplies to, compiled specialisation or not
   if (const char *e = gdsp::dev_switch("GDSP_JIT_RADICES"); e && !chirpz && gdsp::jit_enabled()) {
     int jr[5], jnp = 0;
@@ -681,7 +681,7 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
       if (end == q) break;
       jr[jnp++] = (int)v;
       prod *= v;
-      q = *end == ',' ? end + 1 : end;
+      q = *end ? end + 1 : end;  // any one separator character
     }
     if (jnp >= 2 && prod == n)
       if (gdsp::JitSpec *j = gdsp::jit_spec_build(dev, jr, jnp, (int)n)) {
@@ -1727,8 +1727,14 @@ int gdsp_fft_real_batch_device(const gdsp_plan *plan, const double *d_in, void *
   const char *i0 = (const char *)d_in, *o0 = (const char *)d_out;
   if (batch > 0 && plan->n > 0 && i0 < o0 + 2 * in_bytes && o0 < i0 + in_bytes)
     return fail(GDSP_ERR_INVALID, "real input overlaps the complex output");
-  return exec_plan(plan, d_in, (cd *)d_out, batch, inverse != 0, gdsp::LOAD_REAL,
-                   (hipStream_t)stream);
+  hipStream_t s = (hipStream_t)stream;
+  if (inverse && batch > 0 && plan->n > 0) {
+    // IFFTReal (fft.go:30-32 = IFFT(ToComplex(x))): the kernels read real rows
+    // in the forward direction only, so widen into d_out and transform there
+    HIPCHK(gdsp::launch_real_to_complex(d_in, (cd *)d_out, batch * plan->n, s));
+    return exec_plan(plan, d_out, (cd *)d_out, batch, true, gdsp::LOAD_COMPLEX, s);
+  }
+  return exec_plan(plan, d_in, (cd *)d_out, batch, inverse != 0, gdsp::LOAD_REAL, s);
 }
 
 int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, int64_t pad,

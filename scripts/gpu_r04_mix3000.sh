@@ -2,4 +2,4 @@
 # (dev switch GDSP_JIT_RADICES) against the compiled 25*15*8 specialisation
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
-bash scripts/gpu_ab_env.sh bluestein3000 "GDSP_JIT_RADICES=25,15,8 GDSP_JIT_RADICES=10,15,20 GDSP_JIT_RADICES=20,15,10 GDSP_JIT_RADICES=12,10,25 GDSP_JIT_RADICES=8,15,25 GDSP_JIT_RADICES=24,5,25 GDSP_JIT_RADICES=6,20,25" 2
+bash scripts/gpu_ab_env.sh bluestein3000 "GDSP_JIT_RADICES=25x15x8 GDSP_JIT_RADICES=10x15x20 GDSP_JIT_RADICES=20x15x10 GDSP_JIT_RADICES=12x10x25 GDSP_JIT_RADICES=8x15x25 GDSP_JIT_RADICES=24x5x25 GDSP_JIT_RADICES=6x20x25" 2
