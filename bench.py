@@ -58,6 +58,7 @@ SQ_ROUNDS = ("r04", "r03", "r02")  # SQ counter passes quoted: the newest round 
 # `bench.py --workload <w>`): the newest round that has the workload
 STATS_ROUNDS = ("r04", "r03", "r02")
 SEED = 0x5EED
+WARM_S = 0.06  # untimed GPU work before the timed steps (steady clocks; measure())
 # algorithmic bytes of one launch in the N=1 full-size configuration the
 # committed PMC (profiles/pmc_*.json) and SQ (profiles/r02/sq_counters.json)
 # summaries were measured on
@@ -290,6 +291,26 @@ def measure(wl: dict, c: Ctx) -> dict:
     for _ in range(args.warmup):
         wl["step"]()
     torch.cuda.synchronize()
+    # Steady state: the first launches of a run are up to 30 % slower while
+    # the chip's clocks ramp (rocprofv3 per-launch traces, profiles/r04/
+    # *_kernel_trace.json: chirp-z 2.64-3.00 ms for the first launches, 2.28-2.33
+    # from the tenth on). After the W warm-up steps, further untimed steps run
+    # until about WARM_S of GPU work has passed since the start (the same count
+    # on every rank: collectives run inside some steps). Reported as
+    # "warmup_steps_run".
+    t1 = time.perf_counter()
+    wl["step"]()
+    torch.cuda.synchronize()
+    est = max(time.perf_counter() - t1, 1e-6)
+    extra = min(200, max(0, int(WARM_S / est) - args.warmup - 1))
+    if c.world > 1:
+        t = torch.tensor([extra], dtype=torch.int64, device=c.dev if c.backend == "nccl" else "cpu")
+        c.dist.all_reduce(t, op=c.dist.ReduceOp.MAX)
+        extra = int(t.item())
+    for _ in range(extra):
+        wl["step"]()
+    torch.cuda.synchronize()
+    wl["warmup_steps_run"] = args.warmup + 1 + extra
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     c.barrier()
@@ -550,6 +571,7 @@ def run(w: str, c: Ctx, weak: bool = False) -> dict:
         "value": round(value, 3),
         "unit": "Gsamples/s",
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "warmup_steps_run": wl.get("warmup_steps_run"),
         "scaling": wl["scaling"],
         "dtype": wl.get("dtype", "f64 (complex128)"),
         "config": wl["cfg"],
@@ -701,6 +723,7 @@ def main():
     line = {"metric": head["metric"], "value": head["value"], "unit": "Gsamples/s",
             "n_gpus": c.world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": head["ms_per_step"], "higher_is_better": True,
+            "warmup_steps_run": head.get("warmup_steps_run"),
             "scaling": head["scaling"], "vs_baseline": None, "dtype": head["dtype"],
             "data": "synthetic (splitmix64 uniform[-1,1), generated in HBM)"}
     line.update({k: head[k] for k in ("config", "roofline", "fp64", "cpu_baseline", "parity")})
@@ -775,6 +798,32 @@ def rocprof_info(workload: str, alg_bytes: int, share: float = 1.0):
         return None
     import csv
     for rnd in STATS_ROUNDS:
+        # per-launch trace: the average over the launches that run timed
+        # (the last timed_last; the earlier ones are the run's warm-up)
+        tpath = os.path.join(REPO, "profiles", rnd, f"{w}_kernel_trace.json")
+        if os.path.exists(tpath):
+            with open(tpath) as f:
+                tr = json.load(f)
+            last = tr["timed_last"]
+            avg = mn = 0.0
+            calls = []
+            for k in ks:
+                hit = [v for name, v in tr["kernels"].items() if k in name]
+                if not hit:
+                    break
+                d = max(hit, key=len)[-last:]
+                avg += sum(d) / len(d)
+                mn += min(d)
+                calls.append(len(d))
+            else:
+                avg_s = avg * 1e-9 * share
+                ach = alg_bytes / avg_s / 1e9
+                return {"avg_launch_ms": round(avg_s * 1e3, 4),
+                        "min_launch_ms": round(mn * 1e-6 * share, 4), "calls": calls,
+                        "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                        "over": "the timed launches of the profiled run (its last "
+                                f"{last}; warm-up excluded)",
+                        "source": f"profiles/{rnd}/{w}_kernel_trace.json"}
         path = os.path.join(REPO, "profiles", rnd, f"{w}_kernel_stats.csv")
         if not os.path.exists(path):
             continue

@@ -8,4 +8,5 @@ for W in radix4096 bluestein3000 chirpz3000 fft2_8192 pwelch; do
   cp gpurun_out/prof_$W/run_kernel_stats.csv profiles/r04/${W}_kernel_stats.csv
 done
 python3 tools/pmc_summary.py r04 radix4096 bluestein3000 chirpz3000 fft2_8192 pwelch
+python3 tools/trace_summary.py r04 20 radix4096 bluestein3000 chirpz3000 fft2_8192 pwelch
 python3 tools/sq_summary.py r04 radix4096 bluestein3000 chirpz3000 pwelch fft2_8192
