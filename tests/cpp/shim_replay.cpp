@@ -233,6 +233,11 @@ std::vector<complex128> FFTRealBatch(const std::vector<double> &x, int n) {
   return r;
 }
 
+void SetDevices(const std::vector<int> &ids) {
+  std::vector<int> c(ids.begin(), ids.end());
+  check(gdsp_set_devices(c.empty() ? nullptr : c.data(), (int)c.size()));
+}
+
 std::vector<complex128> FFTBatchMulti(const std::vector<complex128> &x, int n, bool inverse) {
   if (n <= 0 || x.size() % (size_t)n != 0) throw GoPanic("arrays not of equal size");
   std::vector<complex128> r(x.size());
@@ -586,6 +591,13 @@ int main(int argc, char **argv) {
     EXPECT(e < 1e-9 && ei < 1e-9 && er < 1e-9, "FFTBatch/FFTBatchMulti/FFTRealBatch");
   }
   goshim::EnsurePlan(1 << 20);
+  {
+    goshim::SetDevices({0});
+    int d[4] = {-1, -1, -1, -1};
+    EXPECT(gdsp_get_devices(d, 4) == 1 && d[0] == 0, "SetDevices([0])");
+    goshim::SetDevices({});  // back to the calling thread's current device
+    EXPECT(panics([] { goshim::SetDevices({999}); }).find("gdspfft:") == 0, "SetDevices bad id");
+  }
   goshim::SetWorkerPoolSize(-3);
   EXPECT(gdsp_worker_pool_size() == 0, "SetWorkerPoolSize(-3) records 0");
   goshim::SetWorkerPoolSize(6);

@@ -262,3 +262,40 @@ def test_shim_replay(refvec, tmp_path):
     r = subprocess.run([SHIM_BIN, str(vec)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "failures 0" in r.stdout
+
+
+def _bodies(src, lang):
+    """name -> body text of each top-level function (Go: func Name(...);
+    C++: the goshim namespace's functions)."""
+    import re
+    out = {}
+    if lang == "go":
+        pat = re.compile(r"^func (?:\([^)]*\) )?(\w+)\(.*?\{\s*$|^func (?:\([^)]*\) )?(\w+)\(.*?\{ ", re.M)
+    else:
+        pat = re.compile(r"^(?:static )?[\w:<>, ]+?[ *&](\w+)\([^;{]*\)\s*(?:const\s*)?\{", re.M)
+    ms = list(pat.finditer(src))
+    for i, m in enumerate(ms):
+        name = m.group(1) or (m.group(2) if m.lastindex and m.lastindex >= 2 else None)
+        end = ms[i + 1].start() if i + 1 < len(ms) else len(src)
+        out[name] = src[m.start():end]
+    return out
+
+
+def test_shim_replay_matches_go_call_sequences():
+    """tests/cpp/shim_replay.cpp replays go/'s functions call for call: for
+    every exported Go function (and the helpers they delegate to), the
+    ordered libgdspfft calls in its body equal those of its C++ namesake."""
+    import re
+    cpp = open(os.path.join(REPO, "tests", "cpp", "shim_replay.cpp")).read()
+    cpp = cpp[cpp.index("namespace goshim {"):cpp.index("}  // namespace goshim")]
+    cb = _bodies(cpp, "cpp")
+    checked = 0
+    for rel in ("fft/fft_gpu.go", "spectral/pwelch_gpu.go", "wav/wav_gpu.go"):
+        gb = _bodies(open(os.path.join(GO, rel)).read(), "go")
+        for name, body in gb.items():
+            calls = re.findall(r"\bC\.(gdsp_\w+)\(", body)
+            if not calls or name not in cb:
+                continue
+            assert re.findall(r"\b(gdsp_\w+)\(", cb[name]) == calls, (rel, name)
+            checked += 1
+    assert checked >= 15, checked
