@@ -274,7 +274,11 @@ __device__ __forceinline__ void c6_fft(cd (&v)[16], int t, const cd *__restrict_
 // touch (persistent kernel): the next row's bytes, one 128-B line per thread,
 // loaded into L2 right after this row's loads issue (its result is held in one
 // register to the end of the transform, so no wait ever lands on it early).
-template <int RB, bool INV, int KN, bool REAL, int ABL>
+// XD: the row comes in by LDS-DMA (buffer_load ... lds) into the exchange
+// buffer, idle at the transform's start, and is read from there (an
+// all-DMA prologue: MI355X_MICROARCH.md's prologue-burst row, ~12-13 against
+// ~11 B/cycle/CU for register loads); bytes past the row land as zeros.
+template <int RB, bool INV, int KN, bool REAL, int ABL, bool XD = false>
 __device__ __forceinline__ void c6_transform(const void *__restrict__ in, cd *__restrict__ out,
                                              int64_t n, int64_t g, int t, const cd *tw,
                                              const cd *chirp, const cd *bhat, double scale,
@@ -285,7 +289,45 @@ __device__ __forceinline__ void c6_transform(const void *__restrict__ in, cd *__
   const int64_t inb = REAL ? n * 8 : rowb;
   cd v[16];
   unsigned touched = 0u;
-  if (G::NA == G::T || t < G::NA) {
+  if constexpr (XD) {
+    constexpr int NW = G::T / 64;            // waves
+    constexpr int PIECES = G::M * 8 / 1024;  // 1-KiB pieces of the buffer
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const rsrc_t rin = make_rsrc(static_cast<const char *>(in) + g * inb, inb);
+    const uint32_t lane16 = (uint32_t)(t & 63) * 16u;
+    if (!first) __syncthreads();  // the previous transform's last exchange reads are done
+#pragma unroll
+    for (int i = 0; i < (PIECES + NW - 1) / NW; ++i) {
+      const int p = w + i * NW;
+      if (p < PIECES)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rin, (__attribute__((address_space(3))) void *)((char *)lds + p * 1024), 16,
+            (uint32_t)p * 1024u + lane16, 0, 0, 0);
+    }
+    cd cv[KN];
+    if (G::NA == G::T || t < G::NA) {
+      const rsrc_t rch = make_rsrc(chirp, rowb);
+#pragma unroll
+      for (int r = 0; r < KN; ++r) cv[r] = buf_ld(rch, off + (uint32_t)(r * G::NA * 16));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (G::NA == G::T || t < G::NA) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (r < KN) {
+          cd x;
+          if constexpr (REAL) x = {lds[t + r * G::NA], 0.0};
+          else x = reinterpret_cast<const cd *>(lds)[t + r * G::NA];
+          if constexpr (INV) x.y = -x.y;
+          v[r] = cmul(x, cv[r]);
+        } else {
+          v[r] = {0.0, 0.0};
+        }
+      }
+    }
+    first = false;  // the exchange below must wait for every read of the row
+  } else if (G::NA == G::T || t < G::NA) {
     const rsrc_t rin =
         make_rsrc(static_cast<const char *>(in) + g * inb, inb);
     const rsrc_t rch = make_rsrc(chirp, rowb);
@@ -338,7 +380,7 @@ __device__ __forceinline__ void c6_transform(const void *__restrict__ in, cd *__
 // TA: touch into L2 the row of the block TA places later in dispatch order
 // (the same XCD when TA is a multiple of 8; it should start after this block
 // ends, so TA >= the resident blocks, 2 per CU)
-template <int RB, bool INV, int KN, bool REAL = false, int ABL = 0, int TA = 0>
+template <int RB, bool INV, int KN, bool REAL = false, int ABL = 0, int TA = 0, bool XD = false>
 __global__ __launch_bounds__(C6Geo<RB>::T) __attribute__((amdgpu_waves_per_eu(RB == 24 ? 4 : 3))) void chirpz6k_kernel(
     const void *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
     const cd *__restrict__ tw, const cd *__restrict__ chirp, const cd *__restrict__ bhat,
@@ -353,8 +395,8 @@ __global__ __launch_bounds__(C6Geo<RB>::T) __attribute__((amdgpu_waves_per_eu(RB
     const int64_t bn = (int64_t)blockIdx.x + TA;
     if (bn < (int64_t)gridDim.x) touch = xcd_remap(bn, gridDim.x);
   }
-  c6_transform<RB, INV, KN, REAL, ABL>(in, out, n, g, (int)threadIdx.x, tw, chirp, bhat, scale,
-                                       lds, true, touch);
+  c6_transform<RB, INV, KN, REAL, ABL, XD>(in, out, n, g, (int)threadIdx.x, tw, chirp, bhat,
+                                           scale, lds, true, touch);
 }
 
 // Persistent form: one workgroup per resident slot, each over a contiguous
@@ -422,6 +464,18 @@ static hipError_t launch_c6(bool inv, int load, const void *in, cd *out, int64_t
 #undef GDSP_C6T
       default: break;
     }
+  }
+  if (const char *e = dev_switch("GDSP_C6_XDMA"); e && e[0] == '1') {
+    if (load == LOAD_REAL)
+      hipLaunchKernelGGL((chirpz6k_kernel<RB, false, 8, true, 0, 0, true>), grid, block, 0, s, in,
+                         out, n, batch, tw, chirp, bhat, scale);
+    else if (inv)
+      hipLaunchKernelGGL((chirpz6k_kernel<RB, true, 8, false, 0, 0, true>), grid, block, 0, s, in,
+                         out, n, batch, tw, chirp, bhat, scale);
+    else
+      hipLaunchKernelGGL((chirpz6k_kernel<RB, false, 8, false, 0, 0, true>), grid, block, 0, s, in,
+                         out, n, batch, tw, chirp, bhat, scale);
+    return hipGetLastError();
   }
   if (const char *e = dev_switch("GDSP_C6_PERSIST"); e && e[0] == '1') {
     // one workgroup per resident slot (occupancy x CUs of the current device)
