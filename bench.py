@@ -671,11 +671,27 @@ def _free_port() -> int:
 
 def launch(cmd: list, ranks: list, poll_s: float = 0.2) -> int:
     """Start one child per rank (cmd with that rank's environment) and wait.
-    The children inherit stdout/stderr: only rank 0 prints the JSON line. The
-    first child to fail ends the others (their exact PIDs), and its exit
-    status is returned. This process makes no GPU call."""
+    Only rank 0's JSON line reaches stdout: every other line a child prints on
+    stdout (e.g. gloo's "[Gloo] Rank 1 is connected to ..." banner) goes to
+    stderr, so the result stays one parseable line. The first child to fail
+    ends the others (their exact PIDs), and its exit status is returned. This
+    process makes no GPU call."""
     import subprocess
-    procs = [subprocess.Popen(cmd, env=e) for e in ranks]
+    import threading
+    procs = [subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE, text=True) for e in ranks]
+
+    def pump(rank: int, stream):
+        for raw in stream:
+            line = raw.rstrip("\n")
+            if rank == 0 and line.startswith("{"):
+                print(line, flush=True)
+            elif line:
+                print(line, file=sys.stderr, flush=True)
+
+    pumps = [threading.Thread(target=pump, args=(i, p.stdout), daemon=True)
+             for i, p in enumerate(procs)]
+    for t in pumps:
+        t.start()
     rc = 0
     try:
         while procs:
@@ -700,6 +716,8 @@ def launch(cmd: list, ranks: list, poll_s: float = 0.2) -> int:
             except subprocess.TimeoutExpired:
                 p.kill()
                 p.wait()
+        for t in pumps:
+            t.join(timeout=5)
     return rc if rc >= 0 else 128 - rc  # a signalled child: 128 + signal number
 
 

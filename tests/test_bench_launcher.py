@@ -72,6 +72,7 @@ def test_bad_gpu_count():
 CHILD = r"""
 import json, os, sys
 r = int(os.environ["RANK"])
+print(f"[Gloo] Rank {r} is connected to 2 peer ranks.", flush=True)  # stdout noise
 if os.environ.get("FAIL_RANK") == str(r):
     sys.exit(3)
 if os.environ.get("HANG_RANK") == str(r):
@@ -100,8 +101,11 @@ def _run_launch(tmp_path, n, extra=None):
 def test_launch_forwards_rank0_line(tmp_path):
     p = _run_launch(tmp_path, 3)
     assert p.returncode == 0, p.stderr
+    # only rank 0's JSON line reaches stdout; the ranks' other stdout lines
+    # go to stderr
     lines = [l for l in p.stdout.splitlines() if l.strip()]
     assert len(lines) == 1 and json.loads(lines[0]) == {"n_gpus": 3, "rank": 0}
+    assert p.stderr.count("[Gloo] Rank") == 3
 
 
 def test_launch_fails_loud_and_ends_the_others(tmp_path):
