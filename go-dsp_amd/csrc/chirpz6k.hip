@@ -181,14 +181,35 @@ struct C6Out {
 // (M = 3072: none) pass B; all take part in the barriers.
 // ABL (development ablations, results wrong): bit 3 drops the exchanges'
 // barriers (a race, timing only)
+// bit 6 (64, not an ablation): a bare s_barrier after the wave's own LDS
+// operations, so an LDS-DMA in flight is not drained (__syncthreads' fence
+// waits vmcnt(0) for it; cdna_hip_programming.md "Pipelining across barriers")
 template <int ABL>
 __device__ __forceinline__ void c6_sync() {
-  if constexpr (!(ABL & 8)) __syncthreads();
+  if constexpr (ABL & 64) {
+    // (sched_barrier: nothing is scheduled across it, as across
+    // __syncthreads; without, 22 VGPRs spill at 128)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  }
+  else if constexpr (!(ABL & 8)) __syncthreads();
 }
 
-template <int RB, int ZIN, class EPI, int ABL = 0>
+// Hooks into c6_fft for the LDS-DMA-prefetching persistent kernel: after the
+// first barrier of exchange 1, and between the last exchange and pass C (pa:
+// this thread takes part in pass C); tw_b / tw_c give the pass twiddle bases
+// (from registers where a load's wait would drain an LDS-DMA in flight).
+struct C6NoHook {
+  __device__ __forceinline__ void after_first() {}
+  __device__ __forceinline__ cd tw_b(const cd *tw, int t) const { return tw[t & 15]; }
+  __device__ __forceinline__ cd tw_c(const cd *tw, int t) const { return tw[16 + t]; }
+  __device__ __forceinline__ void before_c(const cd *, int, bool) {}
+};
+
+template <int RB, int ZIN, class EPI, int ABL = 0, class HOOK = C6NoHook>
 __device__ __forceinline__ void c6_fft(cd (&v)[16], int t, const cd *__restrict__ tw, double *lds,
-                                       bool first, EPI &epi) {
+                                       bool first, EPI &epi, HOOK hk = {}) {
   using G = C6Geo<RB>;
   const bool pa = G::NA == G::T || t < G::NA;
   const bool pb = kC6B == G::T || t < kC6B;
@@ -204,6 +225,7 @@ __device__ __forceinline__ void c6_fft(cd (&v)[16], int t, const cd *__restrict_
   const int ra = t ^ ((t >> 4) & 15);
   cd u[RB];
   if (!first) c6_sync<ABL>();
+  hk.after_first();
   if (pa) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) lds[wa + (r ^ ma)] = v[r].x;
@@ -224,7 +246,7 @@ __device__ __forceinline__ void c6_fft(cd (&v)[16], int t, const cd *__restrict_
   if (pb) {
 #pragma unroll
     for (int r = 0; r < RB; ++r) u[r].y = lds[ra + kC6B * r];
-    c6_twiddle<RB>(u, tw[t & 15]);
+    c6_twiddle<RB>(u, hk.tw_b(tw, t));
     dft3x<RB>(u);
   }
   c6_sync<ABL>();
@@ -247,8 +269,11 @@ __device__ __forceinline__ void c6_fft(cd (&v)[16], int t, const cd *__restrict_
   if (pa) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r].y = lds[t + G::NA * r];
+  }
+  hk.before_c(tw, t, pa);
+  if (pa) {
     // pass C: twiddle W_M^(t r), DFT_16, the epilogue
-    c6_twiddle<16>(v, tw[16 + t]);
+    c6_twiddle<16>(v, hk.tw_c(tw, t));
     Dft<16>::run(v);
     epi.issue();
     epi.apply(v);
@@ -423,6 +448,179 @@ __global__ __launch_bounds__(C6Geo<RB>::T) __attribute__((amdgpu_waves_per_eu(RB
   }
 }
 
+// Two rows per workgroup, straight-line (development build, GDSP_C6_X2=1):
+// row A as the one-shot kernel while its FFTs bring row B in by LDS-DMA, then
+// row B from LDS. Bytes [0, LZ) of row B (the whole row for float64 input)
+// go to a landing zone of their own, issued after FFT 1's pass A of row A
+// (the zone is idle), bytes [LZ, 16 n) to the same offsets of the exchange
+// buffer, issued after FFT 2's last exchange (the buffer is idle from there
+// to row B). While a DMA is in flight the compiler waits vmcnt(0) at the next
+// use of any ordinary load (cdna_hip_programming.md, "Pipelining across
+// barriers"), so row A's barriers fence LDS only (c6_sync<64>) and the pass
+// twiddle bases come from an LDS copy (ds_read: lgkmcnt) — the first waits
+// on a DMA are then FFT 1's bhat (part 1) and FFT 2's output chirp (part 2).
+// Held in registers instead, the bases cost 38 spilled VGPRs at the 128 two
+// workgroups per CU need; a persistent loop over rows spilled 27-112 (the
+// compiler keeps loop-invariant addresses live across the loop), so this is
+// two rows, not a loop. LDS per workgroup: 48 KiB exchange + 6.25 KiB
+// twiddles + 24 KiB landing zone (dynamic, so the compiler's LDS occupancy
+// model keeps the 4-waves register cap): two per CU.
+template <int RB>
+struct C6Dma {
+  using G = C6Geo<RB>;
+  static constexpr int LZ = G::M * 4;      // landing zone bytes (half the buffer)
+  static constexpr int NTW = 16 + G::NA;   // twiddle bases in LDS
+  static constexpr int DYN = NTW * 16 + LZ;
+  static constexpr int NW = G::T / 64;
+  // bytes [b0, b0 + 1024 P) of the row to dst + b0 - d0
+  template <int P>
+  __device__ __forceinline__ static void part(rsrc_t rin, char *dst, uint32_t b0, int w,
+                                              uint32_t lane16) {
+#pragma unroll
+    for (int i = 0; i < (P + NW - 1) / NW; ++i) {
+      const int p = w + i * NW;
+      if (p < P)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rin, (__attribute__((address_space(3))) void *)(dst + p * 1024), 16, lane16,
+            __builtin_amdgcn_readfirstlane(b0 + p * 1024), 0, 0);
+    }
+  }
+};
+struct C6LdsTw {  // twiddle bases from the LDS copy
+  const cd *ltw;
+  __device__ __forceinline__ void after_first() {}
+  __device__ __forceinline__ cd tw_b(const cd *, int t) const { return ltw[t & 15]; }
+  __device__ __forceinline__ cd tw_c(const cd *, int t) const { return ltw[16 + t]; }
+  __device__ __forceinline__ void before_c(const cd *, int, bool) {}
+};
+template <int RB>
+struct C6DmaHook1 : C6LdsTw {  // FFT 1: row B's bytes [0, LZ) into the landing zone
+  rsrc_t rnx;
+  char *lz;
+  int w;
+  uint32_t lane16;
+  bool go;
+  __device__ __forceinline__ void after_first() {
+    __builtin_amdgcn_sched_barrier(0);  // pass A (every use of row A's loads) stays before
+    if (go) C6Dma<RB>::template part<C6Dma<RB>::LZ / 1024>(rnx, lz, 0u, w, lane16);
+  }
+};
+template <int RB, bool REAL>
+struct C6DmaHook2 : C6LdsTw {  // FFT 2: the rest of row B into the exchange buffer
+  rsrc_t rnx;
+  char *xb;
+  int w;
+  uint32_t lane16;
+  bool go;
+  __device__ __forceinline__ void before_c(const cd *, int, bool) {
+    if constexpr (!REAL) {
+      c6_sync<64>();  // every read of the exchange buffer is done
+      constexpr int P = (C6Geo<RB>::M * 8 - C6Dma<RB>::LZ) / 1024;
+      if (go) C6Dma<RB>::template part<P>(rnx, xb + C6Dma<RB>::LZ, (uint32_t)C6Dma<RB>::LZ, w, lane16);
+    }
+  }
+};
+
+template <int RB, bool INV, int KN, bool REAL = false>
+__global__ __launch_bounds__(C6Geo<RB>::T) __attribute__((amdgpu_waves_per_eu(4))) void chirpz6k_x2_kernel(
+    const void *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
+    const cd *__restrict__ tw, const cd *__restrict__ chirp, const cd *__restrict__ bhat,
+    double scale) {
+  using G = C6Geo<RB>;
+  using D = C6Dma<RB>;
+  static_assert(KN >= 1 && KN <= 8, "n <= M/2");
+  static_assert(!REAL || G::M * 4 <= D::LZ, "float64 rows land whole");
+  static_assert(REAL || G::NA * 4 * 16 == D::LZ, "complex rows split at r = 4");
+  __shared__ double lds[G::M];
+  extern __shared__ double dyn[];  // D::DYN bytes: twiddle bases, landing zone
+  cd *const ltw = reinterpret_cast<cd *>(dyn);
+  char *const lz = reinterpret_cast<char *>(dyn) + D::NTW * 16;
+  const int t = threadIdx.x;
+  const bool pa = G::NA == G::T || t < G::NA;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int64_t rowb = n * 16;
+  const int64_t inb = REAL ? n * 8 : rowb;
+  const int64_t ga = 2 * xcd_remap(blockIdx.x, gridDim.x);
+  if (ga >= batch) return;
+  const bool hasb = ga + 1 < batch;
+  const rsrc_t rnx = make_rsrc(static_cast<const char *>(in) + (hasb ? ga + 1 : ga) * inb, inb);
+  for (int i = t; i < D::NTW; i += G::T) ltw[i] = tw[i];  // (first read after 2 barriers)
+  // row A: registers, as the one-shot kernel
+  {
+    const uint32_t off = (uint32_t)t * 16u;
+    cd v[16];
+    if (pa) {
+      const rsrc_t rin = make_rsrc(static_cast<const char *>(in) + ga * inb, inb);
+      const rsrc_t rch = make_rsrc(chirp, rowb);
+      cd xv[KN], cv[KN];
+#pragma unroll
+      for (int r = 0; r < KN; ++r) {
+        if constexpr (REAL)
+          xv[r] = {buf_ld1(rin, (uint32_t)t * 8u + (uint32_t)(r * G::NA * 8)), 0.0};
+        else
+          xv[r] = buf_ld(rin, off + (uint32_t)(r * G::NA * 16));
+        cv[r] = buf_ld(rch, off + (uint32_t)(r * G::NA * 16));
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (r < KN) {
+          cd x = xv[r];
+          if constexpr (INV) x.y = -x.y;
+          v[r] = cmul(x, cv[r]);
+        } else {
+          v[r] = {0.0, 0.0};
+        }
+      }
+    }
+    const uint32_t lane16 = (uint32_t)(t & 63) * 16u;
+    C6Bhat<RB> be{make_rsrc(bhat, (int64_t)G::M * 16), off, {}};
+    C6DmaHook1<RB> h1{{ltw}, rnx, lz, w, lane16, hasb};
+    c6_fft<RB, KN, C6Bhat<RB>, 64, C6DmaHook1<RB>>(v, t, tw, lds, true, be, h1);
+    const int t2 = opaque_int(t);
+    C6Out<RB, KN, INV> oe{make_rsrc(opaque_ptr(chirp), rowb), make_rsrc(out + ga * n, rowb),
+                          (uint32_t)t2 * 16u, scale, {}};
+    C6DmaHook2<RB, REAL> h2{{ltw}, rnx, (char *)lds, w, (uint32_t)(t2 & 63) * 16u, hasb};
+    c6_fft<RB, 0, C6Out<RB, KN, INV>, 64, C6DmaHook2<RB, REAL>>(v, t2, tw, lds, false, oe, h2);
+  }
+  if (!hasb) return;
+  // row B: from the landing zone and the exchange buffer
+  const int tb = opaque_int(t);
+  const uint32_t offb = (uint32_t)tb * 16u;
+  cd v[16];
+  cd cv[KN];
+  if (pa) {
+    const rsrc_t rch = make_rsrc(opaque_ptr(chirp), rowb);
+#pragma unroll
+    for (int r = 0; r < KN; ++r) cv[r] = buf_ld(rch, offb + (uint32_t)(r * G::NA * 16));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // row B's DMA has landed
+  __syncthreads();
+  if (pa) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (r < KN) {
+        const int e = tb + r * G::NA;
+        cd x;
+        if constexpr (REAL) x = {reinterpret_cast<const double *>(lz)[e], 0.0};
+        else if (r < 4) x = reinterpret_cast<const cd *>(lz)[e];
+        else x = reinterpret_cast<const cd *>(lds)[e];
+        if constexpr (INV) x.y = -x.y;
+        v[r] = cmul(x, cv[r]);
+      } else {
+        v[r] = {0.0, 0.0};
+      }
+    }
+  }
+  C6LdsTw hb{ltw};
+  C6Bhat<RB> be{make_rsrc(opaque_ptr(bhat), (int64_t)G::M * 16), offb, {}};
+  c6_fft<RB, KN, C6Bhat<RB>, 0, C6LdsTw>(v, tb, tw, lds, false, be, hb);
+  const int t2 = opaque_int(tb);
+  C6Out<RB, KN, INV> oe{make_rsrc(opaque_ptr(chirp), rowb),
+                        make_rsrc(opaque_ptr(out) + (ga + 1) * n, rowb), (uint32_t)t2 * 16u,
+                        scale, {}};
+  c6_fft<RB, 0, C6Out<RB, KN, INV>, 0, C6LdsTw>(v, t2, tw, lds, false, oe, hb);
+}
+
 // The convolution length for n (0: neither size applies)
 int chirpz6k_m(int64_t n) {
   if (n >= 2049 && 2 * n - 1 <= 6144) return 6144;
@@ -445,7 +643,7 @@ static hipError_t launch_c6(bool inv, int load, const void *in, cd *out, int64_t
     hipLaunchKernelGGL((chirpz6k_kernel<24, false, 8, false, A>), grid, block, 0, s, in, out, n, \
                        batch, tw, chirp, bhat, scale);                                           \
     return hipGetLastError();
-        GDSP_C6A(1) GDSP_C6A(2) GDSP_C6A(4) GDSP_C6A(7) GDSP_C6A(8) GDSP_C6A(15) GDSP_C6A(16) GDSP_C6A(32)
+        GDSP_C6A(1) GDSP_C6A(2) GDSP_C6A(4) GDSP_C6A(7) GDSP_C6A(8) GDSP_C6A(15) GDSP_C6A(16) GDSP_C6A(32) GDSP_C6A(64)
 #undef GDSP_C6A
         default: break;
       }
@@ -475,6 +673,19 @@ static hipError_t launch_c6(bool inv, int load, const void *in, cd *out, int64_t
     else
       hipLaunchKernelGGL((chirpz6k_kernel<RB, false, 8, false, 0, 0, true>), grid, block, 0, s, in,
                          out, n, batch, tw, chirp, bhat, scale);
+    return hipGetLastError();
+  }
+  if (const char *e = dev_switch("GDSP_C6_X2"); RB == 24 && e && e[0] == '1') {
+    const dim3 g2((unsigned)((batch + 1) / 2));
+    if (load == LOAD_REAL)
+      hipLaunchKernelGGL((chirpz6k_x2_kernel<RB, false, 8, true>), g2, block, C6Dma<RB>::DYN, s, in,
+                         out, n, batch, tw, chirp, bhat, scale);
+    else if (inv)
+      hipLaunchKernelGGL((chirpz6k_x2_kernel<RB, true, 8>), g2, block, C6Dma<RB>::DYN, s, in, out, n,
+                         batch, tw, chirp, bhat, scale);
+    else
+      hipLaunchKernelGGL((chirpz6k_x2_kernel<RB, false, 8>), g2, block, C6Dma<RB>::DYN, s, in, out,
+                         n, batch, tw, chirp, bhat, scale);
     return hipGetLastError();
   }
   if (const char *e = dev_switch("GDSP_C6_PERSIST"); e && e[0] == '1') {
