@@ -181,9 +181,11 @@ struct C6Out {
 // (M = 3072: none) pass B; all take part in the barriers.
 // ABL (development ablations, results wrong): bit 3 drops the exchanges'
 // barriers (a race, timing only)
-// bit 6 (64, not an ablation): a bare s_barrier after the wave's own LDS
-// operations, so an LDS-DMA in flight is not drained (__syncthreads' fence
-// waits vmcnt(0) for it; cdna_hip_programming.md "Pipelining across barriers")
+// bit 6 (64, not an ablation): a barrier fencing LDS only. With an LDS-DMA in
+// flight the compiler still waits vmcnt(0) at it (the DMA is a pending LDS
+// write); the bare form (s_waitcnt lgkmcnt(0) + s_barrier between compiler
+// memory barriers) keeps the DMA in flight but spilled 26 VGPRs in
+// chirpz6k_x2_kernel and ran 5 % slower (profiles/r04/chirpz6k_ablation.txt)
 template <int ABL>
 __device__ __forceinline__ void c6_sync() {
   if constexpr (ABL & 64) {
@@ -201,7 +203,7 @@ __device__ __forceinline__ void c6_sync() {
 // this thread takes part in pass C); tw_b / tw_c give the pass twiddle bases
 // (from registers where a load's wait would drain an LDS-DMA in flight).
 struct C6NoHook {
-  __device__ __forceinline__ void after_first() {}
+  __device__ __forceinline__ void after_first(cd (&)[16]) {}
   __device__ __forceinline__ cd tw_b(const cd *tw, int t) const { return tw[t & 15]; }
   __device__ __forceinline__ cd tw_c(const cd *tw, int t) const { return tw[16 + t]; }
   __device__ __forceinline__ void before_c(const cd *, int, bool) {}
@@ -225,7 +227,7 @@ __device__ __forceinline__ void c6_fft(cd (&v)[16], int t, const cd *__restrict_
   const int ra = t ^ ((t >> 4) & 15);
   cd u[RB];
   if (!first) c6_sync<ABL>();
-  hk.after_first();
+  hk.after_first(v);
   if (pa) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) lds[wa + (r ^ ma)] = v[r].x;
@@ -488,7 +490,7 @@ struct C6Dma {
 };
 struct C6LdsTw {  // twiddle bases from the LDS copy
   const cd *ltw;
-  __device__ __forceinline__ void after_first() {}
+  __device__ __forceinline__ void after_first(cd (&)[16]) {}
   __device__ __forceinline__ cd tw_b(const cd *, int t) const { return ltw[t & 15]; }
   __device__ __forceinline__ cd tw_c(const cd *, int t) const { return ltw[16 + t]; }
   __device__ __forceinline__ void before_c(const cd *, int, bool) {}
@@ -500,8 +502,12 @@ struct C6DmaHook1 : C6LdsTw {  // FFT 1: row B's bytes [0, LZ) into the landing 
   int w;
   uint32_t lane16;
   bool go;
-  __device__ __forceinline__ void after_first() {
-    __builtin_amdgcn_sched_barrier(0);  // pass A (every use of row A's loads) stays before
+  __device__ __forceinline__ void after_first(cd (&v)[16]) {
+    // pass A's results (so every use of row A's loads) complete before the
+    // DMA issues: otherwise the arithmetic sinks below it and the first use
+    // of a row-A load waits vmcnt(0), draining the DMA at once
+#pragma unroll
+    for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(v[r].x), "+v"(v[r].y)::"memory");
     if (go) C6Dma<RB>::template part<C6Dma<RB>::LZ / 1024>(rnx, lz, 0u, w, lane16);
   }
 };
