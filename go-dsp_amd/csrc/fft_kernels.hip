@@ -1105,9 +1105,6 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
       if (const char *e = dev_switch("GDSP_PW_ROWX"); e && e[0] >= '1' && e[0] <= '9')
         return launch_pwelch_rowx4096(e[0] - '0', x, seg_begin, seg_end, ppw, nworkers, win, tw,
                                       partial, s);
-      if (const char *e = dev_switch("GDSP_PW_E8"); e && (e[0] == '1' || e[0] == '2'))
-        return launch_pwelch_row4096_e8(e[0] - '0', x, seg_begin, seg_end, ppw, nworkers, win, tw,
-                                        partial, s);
       if (const char *e = dev_switch("GDSP_PW_HALF"); e && e[0] == '1')
         return launch_pwh_t<12, 2, 1, 4, true, true>(x, seg_begin, seg_end, ppw, nworkers, win, tw,
                                                      partial, s);

@@ -142,11 +142,6 @@ hipError_t launch_pwelch_rowx4096(int variant, const double *x, int64_t seg_begi
                                   int64_t seg_end, int64_t ppw, int64_t nworkers,
                                   const double *win, const cd *tw, double *partial,
                                   hipStream_t s);
-// the row kernel at E = 8 (4 radix-8 passes, 512 threads; pwelch_row.hip)
-hipError_t launch_pwelch_row4096_e8(int variant, const double *x, int64_t seg_begin,
-                                    int64_t seg_end, int64_t ppw, int64_t nworkers,
-                                    const double *win, const cd *tw, double *partial,
-                                    hipStream_t s);
 #endif
 // the row kernel (pwelch_row.hip) behind launch_pwelch_half(12, ...)
 hipError_t launch_pwelch_row4096(const double *x, int64_t seg_begin, int64_t seg_end, int64_t ppw,

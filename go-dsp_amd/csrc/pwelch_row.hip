@@ -39,7 +39,8 @@ namespace gdsp {
 // workgroups per CU: 3.10-3.17 against 2.83 ms.)
 // Also measured and not kept: E = 8 (4 passes of radix 8, 512 threads,
 // 116 VGPRs, four waves per SIMD; XOR exchange slots, table twiddles):
-// 3.18-3.29 against 2.76 ms. And the window folded into pass 0's first radix-2
+// 3.18-3.29 against 2.76 ms; re-measured in round 4 on this kernel, 3.17-3.18
+// against 2.61 ms (profiles/r04/pwelch_rowx_ab.txt). And the window folded into pass 0's first radix-2
 // stage as FMAs (w_j z_j +- w_(j+8) z_(j+8): 16 fewer FP64 instructions per
 // thread and pair), 2.92 against 2.74 ms — the weights stay live in 32 more
 // registers through the first DFT.
@@ -50,8 +51,7 @@ namespace gdsp {
 // lines one pair ahead instead), 10.4 with them; without them at two waves,
 // 3.02 against 2.73-2.77 ms.
 template <int LOG2F, int LOG2E = 4, bool REGTW = true, int LAYOUT = 2>
-__global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG))
-__attribute__((amdgpu_waves_per_eu(LOG2E == 3 ? 4 : 1))) void pwelch_row_kernel(
+__global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_row_kernel(
     const double *__restrict__ x, int64_t seg_begin, int64_t seg_end, int64_t pairs_per_worker,
     const double *__restrict__ win, const cd *__restrict__ tw, double *__restrict__ partial) {
   using G = Geo<LOG2F, LOG2E>;
@@ -148,23 +148,5 @@ hipError_t launch_pwelch_row4096(const double *x, int64_t seg_begin, int64_t seg
                      x, seg_begin, seg_end, ppw, win, tw, partial);
   return hipGetLastError();
 }
-
-#ifdef GDSP_DEV_BUILD
-// E = 8 re-measured on the round-3/4 kernel (register twiddles by recurrence,
-// scalar pair bookkeeping): four waves per SIMD instead of two, 4 passes and
-// 3 exchanges instead of 3 and 2. variant 1: register twiddles; 2: table
-hipError_t launch_pwelch_row4096_e8(int variant, const double *x, int64_t seg_begin,
-                                    int64_t seg_end, int64_t ppw, int64_t nworkers,
-                                    const double *win, const cd *tw, double *partial,
-                                    hipStream_t s) {
-  if (variant == 1)
-    hipLaunchKernelGGL((pwelch_row_kernel<12, 3, true>), dim3((unsigned)nworkers),
-                       dim3(Geo<12, 3>::WG), 0, s, x, seg_begin, seg_end, ppw, win, tw, partial);
-  else
-    hipLaunchKernelGGL((pwelch_row_kernel<12, 3, false>), dim3((unsigned)nworkers),
-                       dim3(Geo<12, 3>::WG), 0, s, x, seg_begin, seg_end, ppw, win, tw, partial);
-  return hipGetLastError();
-}
-#endif
 
 }  // namespace gdsp
