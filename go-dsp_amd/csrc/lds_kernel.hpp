@@ -27,7 +27,11 @@ struct Stage {
   __device__ __forceinline__ static int pad(int i) { return i + i / G::E; }
 };
 
-template <int LOG2N, bool INV, int LOAD, bool SPLIT, int LOG2E = 4>
+// DMA (development build, one complex row per workgroup): the row comes in by
+// LDS-DMA (buffer_load ... lds, nt) instead of register loads — 1: the whole
+// row into a row-sized buffer (the exchange buffer inside it), 2: in two
+// halves through the exchange buffer
+template <int LOG2N, bool INV, int LOAD, bool SPLIT, int LOG2E = 4, int DMA = 0>
 __global__ __launch_bounds__((Geo<LOG2N, LOG2E>::WG),
                              (LOG2N >= 13 && SPLIT ? (LOG2E == 4 ? 4 : 2) : 1)) void
 fft_lds_kernel(const void *__restrict__ in, cd *__restrict__ out, int64_t batch,
@@ -35,7 +39,8 @@ fft_lds_kernel(const void *__restrict__ in, cd *__restrict__ out, int64_t batch,
   using G = Geo<LOG2N, LOG2E>;
   using S = Stage<LOG2N>;
   constexpr int XD = (SPLIT ? 1 : 2) * G::LDS_DOUBLES;
-  __shared__ double lds[XD > S::DOUBLES ? XD : S::DOUBLES];
+  constexpr int XD1 = DMA == 1 && 2 * G::N > XD ? 2 * G::N : XD;
+  __shared__ double lds[XD1 > S::DOUBLES ? XD1 : S::DOUBLES];
   const int lt = threadIdx.x;
   const int slot = lt / G::T;
   const int t = lt & (G::T - 1);
@@ -84,6 +89,33 @@ fft_lds_kernel(const void *__restrict__ in, cd *__restrict__ out, int64_t batch,
       }
     }
     __syncthreads();  // the exchanges below reuse the buffer
+  } else if constexpr (LOAD == LOAD_COMPLEX && DMA > 0) {
+    static_assert(G::TPW == 1 && G::T % 64 == 0, "one row per workgroup");
+    constexpr int HALVES = DMA == 1 ? 1 : 2;
+    constexpr int HB = G::N * 16 / HALVES;  // bytes per DMA round
+    static_assert(HB <= (int)sizeof(lds), "the round fits the buffer");
+    constexpr int NW = G::T / 64, PIECES = HB / 1024;
+    const rsrc_t r = make_rsrc(reinterpret_cast<const cd *>(in) + gl * G::N, G::N * 16);
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const uint32_t lane16 = (uint32_t)(t & 63) * 16u;
+#pragma unroll
+    for (int h = 0; h < HALVES; ++h) {
+      if (h) __syncthreads();  // the previous round's reads are done
+#pragma unroll
+      for (int i = 0; i < PIECES / NW; ++i) {
+        const int p = w + i * NW;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            r, (__attribute__((address_space(3))) void *)((char *)lds + p * 1024), 16, lane16,
+            __builtin_amdgcn_readfirstlane(h * HB + p * 1024), 0, 2);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < G::E / HALVES; ++k) {
+        v[h * (G::E / HALVES) + k] = reinterpret_cast<const cd *>(lds)[t + k * G::T];
+        if constexpr (INV) v[h * (G::E / HALVES) + k].y = -v[h * (G::E / HALVES) + k].y;
+      }
+    }
   } else if constexpr (LOAD == LOAD_COMPLEX) {
     const cd *src = reinterpret_cast<const cd *>(in) + gl * G::N;
 #pragma unroll
@@ -96,7 +128,8 @@ fft_lds_kernel(const void *__restrict__ in, cd *__restrict__ out, int64_t batch,
 #pragma unroll
     for (int k = 0; k < G::E; ++k) v[k] = {ld_nt(&src[t + k * G::T]), 0.0};
   }
-  fft_regs<LOG2N, SPLIT, 0, LOG2E>(v, t, tw, lre, lim);
+  // (after a DMA the first exchange must wait for every read of the row)
+  fft_regs<LOG2N, SPLIT, 0, LOG2E>(v, t, tw, lre, lim, DMA == 0);
   if constexpr (S::ON) {
     const int64_t base = blk * G::TPW * G::N, total = batch * G::N;
     double tmp[2][G::E];
