@@ -735,6 +735,12 @@ def main():
         sys.exit(2)
     if what == "spawn":
         sys.exit(launch([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], info))
+    # stdout carries the one JSON line and nothing else: whatever the
+    # libraries below write to file descriptor 1 (gloo's "[Gloo] Rank 1 is
+    # connected to ..." banner from every rank, runtime notices) goes to stderr
+    sys.stdout.flush()
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     c = Ctx(args)
     w = "radix4096" if args.workload == "default" else args.workload
     head = run(w, c)
@@ -766,7 +772,7 @@ def main():
             if args.config_cpu_seconds > 0:
                 r["cpu_baseline"] = cpu_baseline(cw, args.config_cpu_seconds)
     if c.rank == 0:
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=result_out, flush=True)
     if c.world > 1:
         c.dist.destroy_process_group()
 
