@@ -708,6 +708,69 @@ __global__ __launch_bounds__(WGT) void colfft_tile_kernel(
   }
 }
 
+// Row pass of the two-pass four-step (2^15 <= N <= 2^20, N = R*C, C = 256,
+// 512 or 1024): DFT_C along TPW consecutive rows k1 of the R x C matrix Y (rows of
+// the column pass's output), with the transpose X[k1 + R*k2] = Y[k1][k2]
+// fused into the store. The workgroup stages its TPW rows through LDS so that
+// every store wave-instruction writes, for 64 / TPW output indices k2, TPW
+// consecutive k1: 16 * TPW-byte segments (256 B at C = 256 ... 64 B at 1024),
+// where the row-per-workgroup form of this fusion wrote 16-B pieces R * 16 B
+// apart (DESIGN.md §3 "Four-step": slower than a separate transpose).
+// CONJ_SCALE_OUT: the inverse's conj and 1/N on the way out.
+template <int LOG2C, bool CONJ_SCALE_OUT>
+__global__ __launch_bounds__(256) void rowfft_t_kernel(const cd *__restrict__ in,
+                                                       cd *__restrict__ out, int log2r,
+                                                       const cd *__restrict__ tw, double scale) {
+  using G = Geo<LOG2C>;
+  static_assert(G::WG == 256 && G::TPW >= 4 && G::NPASS > 1, "rows of 256 to 1024");
+  constexpr int TPW = G::TPW, T = G::T, E = G::E, C = G::N;
+  constexpr int SD = C * (TPW + 1);  // staging: element a of row slot at a (TPW + 1) + slot
+  __shared__ double lds[G::LDS_DOUBLES > SD ? G::LDS_DOUBLES : SD];
+  const int lt = threadIdx.x, slot = lt / T, t = lt & (T - 1);
+  const int64_t g0 = xcd_remap(blockIdx.x, gridDim.x) * TPW;
+  const cd *src = in + (g0 + slot) * C;
+  cd v[E];
+#pragma unroll
+  for (int k = 0; k < E; ++k) v[k] = ld_nt(&src[t + k * T]);
+  double *lre = lds + slot * G::STRIDE;
+  fft_regs<LOG2C, true, 0, 4>(v, t, tw, lre, lre);
+  // store lane lt: row g0 + s (s fastest), outputs a = a0 + q T
+  const int s = lt % TPW, a0 = lt / TPW;
+  const int64_t g = g0 + s, R = (int64_t)1 << log2r;
+  cd *dst = out + (g >> log2r) * (R * C) + (g & (R - 1));
+  double re[E];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    __syncthreads();  // the last exchange's (or the real parts') reads are done
+#pragma unroll
+    for (int k = 0; k < E; ++k) lds[(t + k * T) * (TPW + 1) + slot] = h ? v[k].y : v[k].x;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < E; ++q) {
+      const double d = lds[(a0 + q * T) * (TPW + 1) + s];
+      if (h == 0) {
+        re[q] = d;
+      } else {
+        cd o = {re[q], d};
+        if constexpr (CONJ_SCALE_OUT) o = {o.x * scale, -o.y * scale};
+        st_nt(&dst[(int64_t)(a0 + q * T) * R], o);
+      }
+    }
+  }
+}
+
+hipError_t launch_rowfft_t(int log2c, bool conj_scale_out, const cd *in, cd *out, int64_t rows,
+                           int log2r, const cd *tw, double scale, hipStream_t s) {
+  if (rows <= 0 || log2r < 0 || log2r > 30 || (rows & (((int64_t)1 << log2r) - 1)))
+    return hipErrorInvalidValue;
+#define GDSP_RT(L)                                                                                if (log2c == L) {                                                                                 constexpr int TPW = Geo<L>::TPW;                                                                if (log2r < 3 || ((int64_t)1 << log2r) % TPW || rows / TPW > 0x7fffffff)                          return hipErrorInvalidValue;                                                                  const dim3 grid((unsigned)(rows / TPW));                                                        if (conj_scale_out)                                                                               hipLaunchKernelGGL((rowfft_t_kernel<L, true>), grid, dim3(256), 0, s, in, out, log2r, tw,                          scale);                                                                    else                                                                                              hipLaunchKernelGGL((rowfft_t_kernel<L, false>), grid, dim3(256), 0, s, in, out, log2r, tw,                          scale);                                                                    return hipGetLastError();                                                                     }
+  GDSP_RT(8)
+  GDSP_RT(9)
+  GDSP_RT(10)
+#undef GDSP_RT
+  return hipErrorInvalidValue;
+}
+
 // out[c*rows + r] = in[r*cols + c] through a 32x33 LDS tile (complex128),
 // for `batch` consecutive matrices. Tiles of all matrices form one index
 // space that a bounded grid strides over, so small matrices (the 210 x 210
@@ -1248,6 +1311,7 @@ hipError_t launch_colfft(int log2l, bool conj_in, int twiddle, bool conj_scale_o
                               in_stride, out_step, out_stride, twl, twr, log2r, scale, batch, \
                               mat_stride, twn, s);
     GDSP_CFC(4) GDSP_CFC(5) GDSP_CFC(6) GDSP_CFC(7) GDSP_CFC(8) GDSP_CFC(9)
+    GDSP_CFC(10)  // (beyond kColMaxLog2: the two-pass four-step's 2^20 columns only)
 #undef GDSP_CFC
     default: return hipErrorInvalidValue;
   }

@@ -937,9 +937,51 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
 
 void fourstep_split(int ln, int *lr, int *lc);
 
+// 2^15 <= N <= 2^20: two HBM round trips instead of three. N = R*C with
+// rows of C = 256 (512 at 2^18, 1024 from 2^19): the column pass as below,
+// then the rows DFT_C with the transpose fused into their store
+// (rowfft_t_kernel: a workgroup's TPW = 256 / (C / 16) rows leave as 64-256-B
+// segments of X). Per 2^27 samples (profiles/r04/fourstep2_ab.txt): 2^15
+// 2.10 -> 1.46 ms, 2^16 2.17 -> 1.55, 2^17 2.16 -> 1.57, 2^18 2.11 -> 1.60,
+// 2^19 2.16 -> 1.88, 2^20 2.21 -> 1.90; BenchmarkFFT's one 2^20 transform
+// 0.039 -> 0.031 ms. (GDSP_FS3=1 / GDSP_FS2_MAX in the development build.)
+int exec_fourstep2(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
+                   hipStream_t s, int depth) {
+  const int ln = p->log2n;
+  const int lc = ln >= 19 ? 10 : (ln >= 18 ? 9 : 8), lr = ln - lc;
+  gdsp_plan *pr = nullptr, *pcol = nullptr;
+  STCHK(get_plan((int64_t)1 << lr, &pr));
+  STCHK(get_plan((int64_t)1 << lc, &pcol));
+  const int64_t N = p->n, R = (int64_t)1 << lr, C = (int64_t)1 << lc;
+  DevBuf work;
+  // (its own slot per recursion depth: as the rows of a longer four-step it
+  // runs while the caller's work buffer, SLOT_FS0 + depth - 1, holds them)
+  STCHK(work.alloc((size_t)batch * (size_t)N * sizeof(cd), s, (Slot)(SLOT_FS0 + depth)));
+  cd *w = (cd *)work.p;
+  const cd *src = (const cd *)in;
+  if (load == gdsp::LOAD_REAL) {
+    HIPCHK(gdsp::launch_real_to_complex((const double *)in, w, batch * N, s));
+    src = w;
+  }
+  for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+    const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+    HIPCHK(gdsp::launch_colfft(lr, inv, 2, false, src + b0 * N, w + b0 * N, C, 1, 0, 1, 0, 1,
+                               pr->tw, p->tw, ln, 1.0, nb, N, s));
+  }
+  HIPCHK(gdsp::launch_rowfft_t(lc, inv, w, out, batch * R, lr, pcol->tw, 1.0 / (double)N, s));
+  return GDSP_OK;
+}
+
 int exec_fourstep(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
                   hipStream_t s, int depth) {
   const int ln = p->log2n;
+  if (depth >= 4) return fail(GDSP_ERR_UNSUPPORTED, "transform too long");
+  static const int fs2_max = [] {  // development build: GDSP_FS2_MAX, largest log2 N
+    const char *e = gdsp::dev_switch("GDSP_FS2_MAX");
+    return e ? atoi(e) : 20;
+  }();
+  if (ln >= 15 && ln <= fs2_max && ln <= 20 && !gdsp::dev_switch("GDSP_FS3"))
+    return exec_fourstep2(p, in, out, batch, inv, load, s, depth);
   int lr, lc;
   fourstep_split(ln, &lr, &lc);
   // Few transforms: rows of 8192 leave the row pass at <= 256 workgroups, and

@@ -138,6 +138,28 @@ def test_fourstep_split_by_batch(gdsp, oracle, log2n, batch):
     assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
 
 
+@pytest.mark.parametrize("log2n,batch", [(15, 1), (15, 6), (16, 1), (16, 3), (17, 2), (18, 1),
+                                          (18, 2)])
+def test_fourstep_two_pass(gdsp, oracle, log2n, batch):
+    # 2^15..2^18: column pass + rows with the transpose fused into their store
+    # (rowfft_t_kernel), forward / inverse / real input, and in place on the
+    # device
+    import torch
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    n = 1 << log2n
+    rng = np.random.default_rng(log2n * 10 + batch)
+    x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
+    ref = oracle.fft_rows(x)
+    assert row_nrel(gdsp.fft.FFTBatch(x), ref) < TOL
+    assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL
+    xr = x.real.copy()
+    assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
+    xt = torch.from_numpy(x).cuda()
+    D.fft_batch(xt, xt)
+    torch.cuda.synchronize()
+    assert row_nrel(xt.cpu().numpy(), ref) < TOL
+
+
 @pytest.mark.parametrize("n", [2, 4, 8, 16, 32, 64, 128, 256])
 def test_short_rows_many_blocks(gdsp, oracle, n):
     # short transforms stage whole workgroup chunks through LDS: several
