@@ -716,11 +716,16 @@ __global__ __launch_bounds__(WGT) void colfft_tile_kernel(
 // consecutive k1: 16 * TPW-byte segments (256 B at C = 256 ... 64 B at 1024),
 // where the row-per-workgroup form of this fusion wrote 16-B pieces R * 16 B
 // apart (DESIGN.md §3 "Four-step": slower than a separate transpose).
-// CONJ_SCALE_OUT: the inverse's conj and 1/N on the way out.
-template <int LOG2C, bool CONJ_SCALE_OUT>
+// MODE 0: X as is; 1: the inverse's conj and 1/N on the way out; 2 and 3
+// (the composed chirp-z's two FFT_M, as transpose_blu_kernel's modes 1 and
+// 2): 2 stores conj(X[k] tab[k]) (tab = b-hat), 3 stores the k < n outputs
+// conj(X[k]) tab[k] (tab = chirp; inv: conj and scale) into rows of n.
+template <int LOG2C, int MODE>
 __global__ __launch_bounds__(256) void rowfft_t_kernel(const cd *__restrict__ in,
                                                        cd *__restrict__ out, int log2r,
-                                                       const cd *__restrict__ tw, double scale) {
+                                                       const cd *__restrict__ tw, double scale,
+                                                       const cd *__restrict__ tab, int64_t n,
+                                                       int inv) {
   using G = Geo<LOG2C>;
   static_assert(G::WG == 256 && G::TPW >= 4 && G::NPASS > 1, "rows of 256 to 1024");
   constexpr int TPW = G::TPW, T = G::T, E = G::E, C = G::N;
@@ -736,8 +741,8 @@ __global__ __launch_bounds__(256) void rowfft_t_kernel(const cd *__restrict__ in
   fft_regs<LOG2C, true, 0, 4>(v, t, tw, lre, lre);
   // store lane lt: row g0 + s (s fastest), outputs a = a0 + q T
   const int s = lt % TPW, a0 = lt / TPW;
-  const int64_t g = g0 + s, R = (int64_t)1 << log2r;
-  cd *dst = out + (g >> log2r) * (R * C) + (g & (R - 1));
+  const int64_t g = g0 + s, R = (int64_t)1 << log2r, k1 = g & (R - 1);
+  cd *dst = out + (g >> log2r) * (MODE == 3 ? n : R * C) + k1;
   double re[E];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -752,22 +757,48 @@ __global__ __launch_bounds__(256) void rowfft_t_kernel(const cd *__restrict__ in
         re[q] = d;
       } else {
         cd o = {re[q], d};
-        if constexpr (CONJ_SCALE_OUT) o = {o.x * scale, -o.y * scale};
-        st_nt(&dst[(int64_t)(a0 + q * T) * R], o);
+        const int64_t kk = (int64_t)(a0 + q * T) * R;  // k - k1
+        if constexpr (MODE == 1) o = {o.x * scale, -o.y * scale};
+        if constexpr (MODE == 2) o = conjg(cmul(o, tab[kk + k1]));
+        if constexpr (MODE == 3) {
+          if (kk + k1 >= n) continue;
+          o = cmul(conjg(o), tab[kk + k1]);
+          if (inv) o = {o.x * scale, -o.y * scale};
+        }
+        st_nt(&dst[kk], o);
       }
     }
   }
 }
 
-hipError_t launch_rowfft_t(int log2c, bool conj_scale_out, const cd *in, cd *out, int64_t rows,
-                           int log2r, const cd *tw, double scale, hipStream_t s) {
-  if (rows <= 0 || log2r < 0 || log2r > 30 || (rows & (((int64_t)1 << log2r) - 1)))
+hipError_t launch_rowfft_t(int log2c, int mode, const cd *in, cd *out, int64_t rows, int log2r,
+                           const cd *tw, double scale, hipStream_t s, const cd *tab, int64_t n,
+                           bool inv) {
+  if (rows <= 0 || log2r < 0 || log2r > 30 || (rows & (((int64_t)1 << log2r) - 1)) || mode < 0 ||
+      mode > 3 || (mode >= 2 && !tab))
     return hipErrorInvalidValue;
-#define GDSP_RT(L)                                                                                if (log2c == L) {                                                                                 constexpr int TPW = Geo<L>::TPW;                                                                if (log2r < 3 || ((int64_t)1 << log2r) % TPW || rows / TPW > 0x7fffffff)                          return hipErrorInvalidValue;                                                                  const dim3 grid((unsigned)(rows / TPW));                                                        if (conj_scale_out)                                                                               hipLaunchKernelGGL((rowfft_t_kernel<L, true>), grid, dim3(256), 0, s, in, out, log2r, tw,                          scale);                                                                    else                                                                                              hipLaunchKernelGGL((rowfft_t_kernel<L, false>), grid, dim3(256), 0, s, in, out, log2r, tw,                          scale);                                                                    return hipGetLastError();                                                                     }
+#define GDSP_RTM(L, MO)                                                                          \
+  hipLaunchKernelGGL((rowfft_t_kernel<L, MO>), grid, dim3(256), 0, s, in, out, log2r, tw, scale, \
+                     tab, n, (int)inv)
+#define GDSP_RT(L)                                                                 \
+  if (log2c == L) {                                                                \
+    constexpr int TPW = Geo<L>::TPW;                                               \
+    if (log2r < 3 || ((int64_t)1 << log2r) % TPW || rows / TPW > 0x7fffffff)       \
+      return hipErrorInvalidValue;                                                 \
+    const dim3 grid((unsigned)(rows / TPW));                                       \
+    switch (mode) {                                                                \
+      case 0: GDSP_RTM(L, 0); break;                                               \
+      case 1: GDSP_RTM(L, 1); break;                                               \
+      case 2: GDSP_RTM(L, 2); break;                                               \
+      default: GDSP_RTM(L, 3); break;                                              \
+    }                                                                              \
+    return hipGetLastError();                                                      \
+  }
   GDSP_RT(8)
   GDSP_RT(9)
   GDSP_RT(10)
 #undef GDSP_RT
+#undef GDSP_RTM
   return hipErrorInvalidValue;
 }
 

@@ -945,10 +945,19 @@ void fourstep_split(int ln, int *lr, int *lc);
 // 2.10 -> 1.46 ms, 2^16 2.17 -> 1.55, 2^17 2.16 -> 1.57, 2^18 2.11 -> 1.60,
 // 2^19 2.16 -> 1.88, 2^20 2.21 -> 1.90; BenchmarkFFT's one 2^20 transform
 // 0.039 -> 0.031 ms. (GDSP_FS3=1 / GDSP_FS2_MAX in the development build.)
+bool fourstep2_applies(int ln) {
+  static const int fs2_max = [] {  // development build: GDSP_FS2_MAX, largest log2 N
+    const char *e = gdsp::dev_switch("GDSP_FS2_MAX");
+    return e ? atoi(e) : 20;
+  }();
+  return ln >= 15 && ln <= fs2_max && ln <= 20 && !gdsp::dev_switch("GDSP_FS3");
+}
+int fourstep2_lc(int ln) { return ln >= 19 ? 10 : (ln >= 18 ? 9 : 8); }
+
 int exec_fourstep2(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
                    hipStream_t s, int depth) {
   const int ln = p->log2n;
-  const int lc = ln >= 19 ? 10 : (ln >= 18 ? 9 : 8), lr = ln - lc;
+  const int lc = fourstep2_lc(ln), lr = ln - lc;
   gdsp_plan *pr = nullptr, *pcol = nullptr;
   STCHK(get_plan((int64_t)1 << lr, &pr));
   STCHK(get_plan((int64_t)1 << lc, &pcol));
@@ -968,7 +977,8 @@ int exec_fourstep2(const gdsp_plan *p, const void *in, cd *out, int64_t batch, b
     HIPCHK(gdsp::launch_colfft(lr, inv, 2, false, src + b0 * N, w + b0 * N, C, 1, 0, 1, 0, 1,
                                pr->tw, p->tw, ln, 1.0, nb, N, s));
   }
-  HIPCHK(gdsp::launch_rowfft_t(lc, inv, w, out, batch * R, lr, pcol->tw, 1.0 / (double)N, s));
+  HIPCHK(gdsp::launch_rowfft_t(lc, inv ? 1 : 0, w, out, batch * R, lr, pcol->tw, 1.0 / (double)N,
+                               s));
   return GDSP_OK;
 }
 
@@ -976,12 +986,7 @@ int exec_fourstep(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bo
                   hipStream_t s, int depth) {
   const int ln = p->log2n;
   if (depth >= 4) return fail(GDSP_ERR_UNSUPPORTED, "transform too long");
-  static const int fs2_max = [] {  // development build: GDSP_FS2_MAX, largest log2 N
-    const char *e = gdsp::dev_switch("GDSP_FS2_MAX");
-    return e ? atoi(e) : 20;
-  }();
-  if (ln >= 15 && ln <= fs2_max && ln <= 20 && !gdsp::dev_switch("GDSP_FS3"))
-    return exec_fourstep2(p, in, out, batch, inv, load, s, depth);
+  if (fourstep2_applies(ln)) return exec_fourstep2(p, in, out, batch, inv, load, s, depth);
   int lr, lc;
   fourstep_split(ln, &lr, &lc);
   // Few transforms: rows of 8192 leave the row pass at <= 256 workgroups, and
@@ -1145,6 +1150,33 @@ int exec_bluestein_composed(const gdsp_plan *p, const cd *in, cd *out, int64_t b
           HIPCHK(gdsp::launch_transpose_blu(w + b0 * M, out + b0 * p->n, mp->n1, mp->n2, nb, 2,
                                             p->n, p->chirp, inv, 1.0 / (double)p->n, s));
       }
+    }
+    return GDSP_OK;
+  }
+  if (!p->unfused && p->mplan->kind == KIND_GLOBAL && fourstep2_applies(p->log2m)) {
+    // 2^15 <= M <= 2^20: both FFT_M as the two-pass four-step, the b-hat and
+    // output steps in the rows' transposed store (rowfft_t_kernel modes 2
+    // and 3): premultiply + 2 + 2 passes over M instead of 1 + 3 + 3
+    const int lc2 = fourstep2_lc(p->log2m), lr2 = p->log2m - lc2;
+    const int64_t M = p->m, R = (int64_t)1 << lr2, C = (int64_t)1 << lc2;
+    gdsp_plan *pr = nullptr, *pcol = nullptr;
+    STCHK(get_plan(R, &pr));
+    STCHK(get_plan(C, &pcol));
+    DevBuf work;
+    STCHK(work.alloc((size_t)batch * (size_t)M * sizeof(cd), s, SLOT_FS0));
+    cd *w = (cd *)work.p;
+    for (int pass = 1; pass <= 2; ++pass) {
+      for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+        const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+        HIPCHK(gdsp::launch_colfft(lr2, false, 2, false, da + b0 * M, w + b0 * M, C, 1, 0, 1, 0, 1,
+                                   pr->tw, p->mplan->tw, p->log2m, 1.0, nb, M, s));
+      }
+      if (pass == 1)
+        HIPCHK(gdsp::launch_rowfft_t(lc2, 2, w, da, batch * R, lr2, pcol->tw, 1.0, s, p->bhat,
+                                     p->n, false));
+      else
+        HIPCHK(gdsp::launch_rowfft_t(lc2, 3, w, out, batch * R, lr2, pcol->tw,
+                                     1.0 / (double)p->n, s, p->chirp, p->n, inv));
     }
     return GDSP_OK;
   }

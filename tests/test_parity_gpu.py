@@ -964,6 +964,42 @@ print("ok", flags)
         assert r.returncode == 0 and "ok" in r.stdout, (extra, r.stdout + r.stderr[-3000:])
 
 
+@pytest.mark.gpu
+def test_chirpz_composed_two_pass_fft_m():
+    """The composed chirp-z on a power-of-2 M in 2^15..2^20 runs both FFT_M as
+    the two-pass four-step with the b-hat and output steps in the rows'
+    transposed store (rowfft_t_kernel modes 2 and 3): primes whose
+    NextPowerOf2(2n-1) is each of those M (GDSP_ALGO_CHIRPZ_POW2, so the
+    reference's M), batch 2, forward / inverse / real, against the oracle."""
+    code = r'''
+import importlib, os, sys
+sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
+import numpy as np, oracle
+g = importlib.import_module("go-dsp_amd")
+D = importlib.import_module("go-dsp_amd.device")
+g.fft.SetAlgorithm(g.fft.ALGO_CHIRPZ_POW2 | g.fft.ALGO_NO_CHIRPZ_PARTS)
+rng = np.random.default_rng(15)
+for n, lm in ((16381, 15), (16411, 16), (40009, 17), (65537, 18), (200003, 19), (262147, 20)):
+    p = D.plan(n)
+    assert p.kind == 4 and p.m == 1 << lm, (n, p.kind, p.m)
+    x = rng.standard_normal((2, n)) + 1j * rng.standard_normal((2, n))
+    for inv in (False, True):
+        y = g.fft.FFTBatch(x, inverse=inv)
+        ref = oracle.ifft_rows(x) if inv else oracle.fft_rows(x)
+        err = max(np.linalg.norm(a - b) / np.linalg.norm(b) for a, b in zip(y, ref))
+        assert err < 1e-9, (n, inv, err)
+    xr = x.real.copy()
+    yr = g.fft.FFTRealBatch(xr)
+    ref = oracle.fft_rows(xr.astype(np.complex128))
+    err = max(np.linalg.norm(a - b) / np.linalg.norm(b) for a, b in zip(yr, ref))
+    assert err < 1e-9, (n, "real", err)
+print("ok")
+'''
+    env = dict(os.environ, REPO=REPO)
+    r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr[-3000:]
+
+
 # primes whose NextPowerOf2(2n-1) is 32768: 2 parts (8209, 10007, 10909), 3
 # (11003, 12281), 4 (12289), 6 (13999), 8 (14563, the largest length with P <= 8)
 PARTS = [(8209, 2), (10007, 2), (10909, 2), (11003, 3), (12281, 3), (12289, 4), (13999, 6),
