@@ -655,6 +655,8 @@ int build_shfl_tables(gdsp_plan *p) {
 }
 #endif  // GDSP_DEV_BUILD
 
+bool fourstep2_applies(int ln);  // (exec_fourstep2 below)
+
 int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   p->device = dev;
   p->n = n;
@@ -766,10 +768,15 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
     // single-radix columns, one-kernel rows) instead of bluestein.go:70's
     // power of 2; the convolution, hence the DFT, is the same. Only where it
     // measured faster: M <= 0.55 of a power of 2 <= 2^16 (8209: 19.5 vs 22.1
-    // ms, 16411: 19.4 vs 21.3; 10007, 65537, 100003 were slower). The forced
-    // chirp-z plan keeps the reference's M for the composed chirp-z (the
-    // fused one at 1025..1536 / 2049..3072 takes M = 3072 / 6144 below).
-    for (int64_t m = 2 * n - 1; p->m <= 65536 && m <= (p->m * 11) / 20; ++m) {
+    // ms, 16411: 19.4 vs 21.3; 10007, 65537, 100003 were slower), and only
+    // where the power of 2 has no two-pass FFT (exec_fourstep2, 2^15..2^20):
+    // against it the smooth M lost (16411 15.6 vs 13.4 ms per 2^27 samples,
+    // 17011 16.0 vs 12.9, 17987 15.9 vs 12.3; profiles/r04/fourstep2_ab.txt).
+    // The forced chirp-z plan keeps the reference's M for the composed
+    // chirp-z (the fused one at 1025..1536 / 2049..3072 takes M = 3072 / 6144
+    // below).
+    for (int64_t m = 2 * n - 1;
+         p->m <= 65536 && !fourstep2_applies(ilog2(p->m)) && m <= (p->m * 11) / 20; ++m) {
       int64_t r = 0, c = 0;
       if (pow2col_split(m, r, c) || radixcol_split(m, r, c)) {
         gdsp_plan *mp = nullptr;
