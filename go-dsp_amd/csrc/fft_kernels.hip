@@ -708,6 +708,76 @@ __global__ __launch_bounds__(WGT) void colfft_tile_kernel(
   }
 }
 
+// The composed chirp-z's first column pass with the premultiply folded in
+// (as colfft_tile_kernel, TWIDDLE 2, on a = x * chirp zero-padded to M =
+// R * C): element (j, col) of the R x C view is a[j C + col] = x[e] chirp[e]
+// for e = j C + col < n (x conjugated for an inverse), 0 past n (not loaded).
+// x rows of n per transform (blockIdx.z), out rows of M.
+template <int LOG2L, bool CONJ_IN, int WGT>
+__global__ __launch_bounds__(WGT) void colfft_chirp_kernel(
+    const cd *__restrict__ x, cd *__restrict__ out, int64_t C, int64_t n,
+    const cd *__restrict__ chirp, const cd *__restrict__ twl, const cd *__restrict__ twr) {
+  using G = Geo<LOG2L>;
+  constexpr int CW = WGT / G::T;
+  __shared__ double lds[G::NPASS > 1 ? CW * G::N : 1];
+  const int lt = threadIdx.x;
+  const int c = lt & (CW - 1);
+  const int t = lt / CW;
+  const int64_t col = (int64_t)blockIdx.x * CW + c;  // C is a multiple of CW
+  const int64_t M = (int64_t)G::N * C;
+  x += (int64_t)blockIdx.z * n;
+  out += (int64_t)blockIdx.z * M;
+  cd v[G::E];
+#pragma unroll
+  for (int k = 0; k < G::E; ++k) {
+    const int64_t e = (int64_t)(t + k * G::T) * C + col;
+    cd a = {0.0, 0.0};
+    if (e < n) {
+      cd xe = ld_nt(&x[e]);
+      if constexpr (CONJ_IN) xe.y = -xe.y;
+      a = cmul(xe, chirp[e]);
+    }
+    v[k] = a;
+  }
+  fft_regs<LOG2L, true, false, 4, CW>(v, t, twl, lds + c, lds + c);
+  // times W_M^(col j), j = t + k T: base and step from the table, then the
+  // recurrence (as colfft_tile_kernel's TWIDDLE 2)
+  cd w = twr[(col * t) & (M - 1)];
+  const cd wstep = twr[(col * G::T) & (M - 1)];
+  cd *dst = out + col;
+#pragma unroll
+  for (int k = 0; k < G::E; ++k) {
+    st_nt(&dst[(int64_t)(t + k * G::T) * C], cmul(v[k], w));
+    if (k + 1 < G::E) w = cmul(w, wstep);
+  }
+}
+
+hipError_t launch_colfft_chirp(int log2l, bool conj_in, const cd *x, cd *out, int64_t C,
+                               int64_t n, const cd *chirp, const cd *twl, const cd *twr,
+                               int64_t batch, hipStream_t s) {
+  if (batch < 1 || batch > 65535 || C <= 0 || (C & (C - 1)) || n < 1 || n > (C << log2l))
+    return hipErrorInvalidValue;
+#define GDSP_CCH(L, WGT)                                                                       \
+  if (log2l == L) {                                                                            \
+    constexpr int CW = WGT / Geo<L>::T;                                                        \
+    if (C % CW) return hipErrorInvalidValue;                                                   \
+    const dim3 grid((unsigned)(C / CW), 1, (unsigned)batch);                                   \
+    if (conj_in)                                                                               \
+      hipLaunchKernelGGL((colfft_chirp_kernel<L, true, WGT>), grid, dim3(WGT), 0, s, x, out, C, \
+                         n, chirp, twl, twr);                                                  \
+    else                                                                                       \
+      hipLaunchKernelGGL((colfft_chirp_kernel<L, false, WGT>), grid, dim3(WGT), 0, s, x, out,  \
+                         C, n, chirp, twl, twr);                                               \
+    return hipGetLastError();                                                                  \
+  }
+  GDSP_CCH(7, 256)
+  GDSP_CCH(8, 256)
+  GDSP_CCH(9, 512)
+  GDSP_CCH(10, 512)
+#undef GDSP_CCH
+  return hipErrorInvalidValue;
+}
+
 // Row pass of the two-pass four-step (2^15 <= N <= 2^20, N = R*C, C = 256,
 // 512 or 1024): DFT_C along TPW consecutive rows k1 of the R x C matrix Y (rows of
 // the column pass's output), with the transpose X[k1 + R*k2] = Y[k1][k2]

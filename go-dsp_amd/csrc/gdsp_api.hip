@@ -1138,7 +1138,10 @@ int exec_bluestein_composed(const gdsp_plan *p, const cd *in, cd *out, int64_t b
   DevBuf a;
   STCHK(a.alloc((size_t)batch * (size_t)p->m * sizeof(cd), s, SLOT_BLU));
   cd *da = (cd *)a.p;
-  HIPCHK(gdsp::launch_chirp_premul(in, da, p->n, p->m, batch, p->chirp, inv, s));
+  const bool two_pass =
+      !p->unfused && p->mplan->kind == KIND_GLOBAL && fourstep2_applies(p->log2m);
+  // (the two-pass form folds the premultiply into its first column pass)
+  if (!two_pass) HIPCHK(gdsp::launch_chirp_premul(in, da, p->n, p->m, batch, p->chirp, inv, s));
   const gdsp_plan *mp = p->mplan;
   if (!p->unfused && mp->kind == KIND_MIXED4 && (mp->pow2col || mp->radixcol || mp->mixcol)) {
     // smooth M (a three-pass mixed four-step): the same two fused transposes
@@ -1160,10 +1163,12 @@ int exec_bluestein_composed(const gdsp_plan *p, const cd *in, cd *out, int64_t b
     }
     return GDSP_OK;
   }
-  if (!p->unfused && p->mplan->kind == KIND_GLOBAL && fourstep2_applies(p->log2m)) {
-    // 2^15 <= M <= 2^20: both FFT_M as the two-pass four-step, the b-hat and
-    // output steps in the rows' transposed store (rowfft_t_kernel modes 2
-    // and 3): premultiply + 2 + 2 passes over M instead of 1 + 3 + 3
+  if (two_pass) {
+    // 2^15 <= M <= 2^20: both FFT_M as the two-pass four-step, the
+    // premultiply in the first column pass's loads (colfft_chirp_kernel: x
+    // read once, the zero padding never), the b-hat and output steps in the
+    // rows' transposed store (rowfft_t_kernel modes 2 and 3): 2 + 2 passes
+    // over M instead of 1 + 3 + 3
     const int lc2 = fourstep2_lc(p->log2m), lr2 = p->log2m - lc2;
     const int64_t M = p->m, R = (int64_t)1 << lr2, C = (int64_t)1 << lc2;
     gdsp_plan *pr = nullptr, *pcol = nullptr;
@@ -1175,8 +1180,12 @@ int exec_bluestein_composed(const gdsp_plan *p, const cd *in, cd *out, int64_t b
     for (int pass = 1; pass <= 2; ++pass) {
       for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
         const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
-        HIPCHK(gdsp::launch_colfft(lr2, false, 2, false, da + b0 * M, w + b0 * M, C, 1, 0, 1, 0, 1,
-                                   pr->tw, p->mplan->tw, p->log2m, 1.0, nb, M, s));
+        if (pass == 1)
+          HIPCHK(gdsp::launch_colfft_chirp(lr2, inv, in + b0 * p->n, w + b0 * M, C, p->n, p->chirp,
+                                           pr->tw, p->mplan->tw, nb, s));
+        else
+          HIPCHK(gdsp::launch_colfft(lr2, false, 2, false, da + b0 * M, w + b0 * M, C, 1, 0, 1, 0,
+                                     1, pr->tw, p->mplan->tw, p->log2m, 1.0, nb, M, s));
       }
       if (pass == 1)
         HIPCHK(gdsp::launch_rowfft_t(lc2, 2, w, da, batch * R, lr2, pcol->tw, 1.0, s, p->bhat,

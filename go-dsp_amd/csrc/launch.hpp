@@ -167,6 +167,12 @@ hipError_t launch_colradix(int L, bool conj_in, const cd *in, cd *out, int64_t C
 constexpr int kColMinLog2 = 4, kColMaxLog2 = 9;
 // twiddle: 0 none, 1 W_R^(group*j), 2 W_R^(col*j); table index mod 2^log2r, or mod
 // twn when twn > 0 (a non-power-of-2 N)
+// the composed chirp-z's first column pass (DFT_R, R = 2^log2l, 7 ... 10, of
+// the R x C view, times W_M^(col j)) on a = x * chirp zero-padded to M = R C,
+// the premultiply folded into its loads: x rows of n, out rows of M
+hipError_t launch_colfft_chirp(int log2l, bool conj_in, const cd *x, cd *out, int64_t C,
+                               int64_t n, const cd *chirp, const cd *twl, const cd *twr,
+                               int64_t batch, hipStream_t s);
 // row DFT_C (C = 2^log2c, 8 ... 10) of `rows` rows (a multiple of R = 2^log2r
 // per transform) with the four-step transpose fused into the store:
 // out[b N + k2 R + k1] = DFT_C(in row b R + k1)[k2] (fft_kernels.hip). mode 0
