@@ -770,8 +770,8 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
     // measured faster: M <= 0.55 of a power of 2 <= 2^16 (8209: 19.5 vs 22.1
     // ms, 16411: 19.4 vs 21.3; 10007, 65537, 100003 were slower), and only
     // where the power of 2 has no two-pass FFT (exec_fourstep2, 2^15..2^20):
-    // against it the smooth M lost (16411 15.6 vs 13.4 ms per 2^27 samples,
-    // 17011 16.0 vs 12.9, 17987 15.9 vs 12.3; profiles/r04/fourstep2_ab.txt).
+    // against it the smooth M lost (16411 15.6 vs 9.9 ms per 2^27 samples
+    // with the premultiply folded in; profiles/r04/fourstep2_ab.txt).
     // The forced chirp-z plan keeps the reference's M for the composed
     // chirp-z (the fused one at 1025..1536 / 2049..3072 takes M = 3072 / 6144
     // below).
