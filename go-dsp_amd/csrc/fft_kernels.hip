@@ -778,32 +778,37 @@ hipError_t launch_colfft_chirp(int log2l, bool conj_in, const cd *x, cd *out, in
   return hipErrorInvalidValue;
 }
 
-// Row pass of the two-pass four-step (2^15 <= N <= 2^20, N = R*C, C = 256,
-// 512 or 1024): DFT_C along TPW consecutive rows k1 of the R x C matrix Y (rows of
-// the column pass's output), with the transpose X[k1 + R*k2] = Y[k1][k2]
-// fused into the store. The workgroup stages its TPW rows through LDS so that
+// Row pass of the two-pass four-steps (N = R*C, C = 2^LOG2C, 16 ... 1024): DFT_C
+// along TPW = 4096 / C consecutive rows k1 of the R x C matrix Y (rows of the
+// column pass's output), with the transpose X[k1 + R*k2] = Y[k1][k2] fused
+// into the store. The workgroup stages its TPW rows through LDS so that
 // every store wave-instruction writes, for 64 / TPW output indices k2, TPW
-// consecutive k1: 16 * TPW-byte segments (256 B at C = 256 ... 64 B at 1024),
+// consecutive k1: 16 * TPW-byte segments (4 KiB at C = 16 ... 64 B at 1024),
 // where the row-per-workgroup form of this fusion wrote 16-B pieces R * 16 B
-// apart (DESIGN.md §3 "Four-step": slower than a separate transpose).
+// apart (DESIGN.md §3 "Four-step": slower than a separate transpose). R is
+// any length (log2r >= 0: a power of 2, shifts instead of divisions); `rows`
+// = batch * R, the last workgroup's rows past it load a valid row and store
+// nothing.
 // MODE 0: X as is; 1: the inverse's conj and 1/N on the way out; 2 and 3
 // (the composed chirp-z's two FFT_M, as transpose_blu_kernel's modes 1 and
 // 2): 2 stores conj(X[k] tab[k]) (tab = b-hat), 3 stores the k < n outputs
 // conj(X[k]) tab[k] (tab = chirp; inv: conj and scale) into rows of n.
-template <int LOG2C, int MODE>
+template <int LOG2C, int MODE, bool P2R>
 __global__ __launch_bounds__(256) void rowfft_t_kernel(const cd *__restrict__ in,
-                                                       cd *__restrict__ out, int log2r,
+                                                       cd *__restrict__ out, int64_t R,
+                                                       int log2r, int64_t rows,
                                                        const cd *__restrict__ tw, double scale,
                                                        const cd *__restrict__ tab, int64_t n,
                                                        int inv) {
   using G = Geo<LOG2C>;
-  static_assert(G::WG == 256 && G::TPW >= 4 && G::NPASS > 1, "rows of 256 to 1024");
+  static_assert(G::WG == 256 && G::TPW >= 4, "rows of 16 to 1024");
   constexpr int TPW = G::TPW, T = G::T, E = G::E, C = G::N;
   constexpr int SD = C * (TPW + 1);  // staging: element a of row slot at a (TPW + 1) + slot
   __shared__ double lds[G::LDS_DOUBLES > SD ? G::LDS_DOUBLES : SD];
   const int lt = threadIdx.x, slot = lt / T, t = lt & (T - 1);
   const int64_t g0 = xcd_remap(blockIdx.x, gridDim.x) * TPW;
-  const cd *src = in + (g0 + slot) * C;
+  const int64_t gl = g0 + slot < rows ? g0 + slot : rows - 1;
+  const cd *src = in + gl * C;
   cd v[E];
 #pragma unroll
   for (int k = 0; k < E; ++k) v[k] = ld_nt(&src[t + k * T]);
@@ -811,8 +816,11 @@ __global__ __launch_bounds__(256) void rowfft_t_kernel(const cd *__restrict__ in
   fft_regs<LOG2C, true, 0, 4>(v, t, tw, lre, lre);
   // store lane lt: row g0 + s (s fastest), outputs a = a0 + q T
   const int s = lt % TPW, a0 = lt / TPW;
-  const int64_t g = g0 + s, R = (int64_t)1 << log2r, k1 = g & (R - 1);
-  cd *dst = out + (g >> log2r) * (MODE == 3 ? n : R * C) + k1;
+  const int64_t g = g0 + s;
+  const int64_t b = P2R ? g >> log2r : g / R;
+  const int64_t k1 = g - b * R;
+  cd *dst = out + b * (MODE == 3 ? n : R * C) + k1;
+  const bool valid = g < rows;
   double re[E];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -825,7 +833,7 @@ __global__ __launch_bounds__(256) void rowfft_t_kernel(const cd *__restrict__ in
       const double d = lds[(a0 + q * T) * (TPW + 1) + s];
       if (h == 0) {
         re[q] = d;
-      } else {
+      } else if (valid) {
         cd o = {re[q], d};
         const int64_t kk = (int64_t)(a0 + q * T) * R;  // k - k1
         if constexpr (MODE == 1) o = {o.x * scale, -o.y * scale};
@@ -841,29 +849,43 @@ __global__ __launch_bounds__(256) void rowfft_t_kernel(const cd *__restrict__ in
   }
 }
 
-hipError_t launch_rowfft_t(int log2c, int mode, const cd *in, cd *out, int64_t rows, int log2r,
+hipError_t launch_rowfft_t(int log2c, int mode, const cd *in, cd *out, int64_t rows, int64_t R,
                            const cd *tw, double scale, hipStream_t s, const cd *tab, int64_t n,
                            bool inv) {
-  if (rows <= 0 || log2r < 0 || log2r > 30 || (rows & (((int64_t)1 << log2r) - 1)) || mode < 0 ||
-      mode > 3 || (mode >= 2 && !tab))
+  if (rows <= 0 || R <= 0 || rows % R || mode < 0 || mode > 3 || (mode >= 2 && !tab))
     return hipErrorInvalidValue;
-#define GDSP_RTM(L, MO)                                                                          \
-  hipLaunchKernelGGL((rowfft_t_kernel<L, MO>), grid, dim3(256), 0, s, in, out, log2r, tw, scale, \
-                     tab, n, (int)inv)
-#define GDSP_RT(L)                                                                 \
-  if (log2c == L) {                                                                \
-    constexpr int TPW = Geo<L>::TPW;                                               \
-    if (log2r < 3 || ((int64_t)1 << log2r) % TPW || rows / TPW > 0x7fffffff)       \
-      return hipErrorInvalidValue;                                                 \
-    const dim3 grid((unsigned)(rows / TPW));                                       \
-    switch (mode) {                                                                \
-      case 0: GDSP_RTM(L, 0); break;                                               \
-      case 1: GDSP_RTM(L, 1); break;                                               \
-      case 2: GDSP_RTM(L, 2); break;                                               \
-      default: GDSP_RTM(L, 3); break;                                              \
-    }                                                                              \
-    return hipGetLastError();                                                      \
+  int log2r = -1;
+  if ((R & (R - 1)) == 0) {
+    log2r = 0;
+    while (((int64_t)1 << log2r) < R) ++log2r;
   }
+#define GDSP_RTM(L, MO)                                                                          \
+  do {                                                                                           \
+    if (log2r >= 0)                                                                              \
+      hipLaunchKernelGGL((rowfft_t_kernel<L, MO, true>), grid, dim3(256), 0, s, in, out, R,      \
+                         log2r, rows, tw, scale, tab, n, (int)inv);                              \
+    else                                                                                         \
+      hipLaunchKernelGGL((rowfft_t_kernel<L, MO, false>), grid, dim3(256), 0, s, in, out, R,     \
+                         log2r, rows, tw, scale, tab, n, (int)inv);                              \
+  } while (0)
+#define GDSP_RT(L)                                                  \
+  if (log2c == L) {                                                 \
+    constexpr int TPW = Geo<L>::TPW;                                \
+    const int64_t nb = (rows + TPW - 1) / TPW;                      \
+    if (nb > 0x7fffffff) return hipErrorInvalidValue;               \
+    const dim3 grid((unsigned)nb);                                  \
+    switch (mode) {                                                 \
+      case 0: GDSP_RTM(L, 0); break;                                \
+      case 1: GDSP_RTM(L, 1); break;                                \
+      case 2: GDSP_RTM(L, 2); break;                                \
+      default: GDSP_RTM(L, 3); break;                               \
+    }                                                               \
+    return hipGetLastError();                                       \
+  }
+  GDSP_RT(4)
+  GDSP_RT(5)
+  GDSP_RT(6)
+  GDSP_RT(7)
   GDSP_RT(8)
   GDSP_RT(9)
   GDSP_RT(10)

@@ -322,6 +322,9 @@ struct gdsp_plan {
   // (either way 3 HBM passes instead of 5)
   int64_t n1 = 0, n2 = 0;
   bool pow2col = false, radixcol = false;
+  // rowst: n2 a power of 2 in [16, 1024] and n1 a radixcol / mixcol column:
+  // two passes, the rows' store carrying the transpose (rowfft_t_kernel)
+  bool rowst = false;
   // mixcol: n1 in [26, 1016] smooth, its column pass runtime-compiled
   gdsp::JitCol *mixcol = nullptr;
   gdsp_plan *p1 = nullptr, *p2 = nullptr;
@@ -568,21 +571,54 @@ bool radixcol_split(int64_t n, int64_t &l, int64_t &c) {
 // column pass, colfixed_kernel compiled for L's radix list) and C a
 // one-kernel length; the smallest such L (widest column tiles) whose column
 // kernel builds wins.
+// the runtime-compiled column pass for the column length L of n = L * (n / L)
+bool mixcol_try(int dev, int64_t n, int64_t L, gdsp_plan *p) {
+  if (!gdsp::jit_enabled() || n % L || L < 26 || L > 1016 || is_pow2(L) || !one_kernel_len(L))
+    return false;
+  gdsp_plan *p1 = nullptr;
+  if (get_plan_locked(dev, L, &p1) != GDSP_OK || p1->kind != KIND_MIXED) return false;
+  int rad[16], np = p1->md.npass;
+  if (np < 2 || np > 16) return false;
+  for (int q = 0; q < np; ++q) rad[q] = (int)((p1->md.codes >> (5 * q)) & 31);
+  gdsp::JitCol *col = gdsp::jit_col_build(dev, rad, np);
+  if (!col) return false;
+  p->mixcol = col;
+  p->n1 = L;
+  p->n2 = n / L;
+  p->p1 = p1;
+  return true;
+}
+
 bool mixcol_build(int dev, int64_t n, gdsp_plan *p) {
   if (!gdsp::jit_enabled()) return false;
   for (int64_t L = 26; L <= 1016; ++L) {
     if (n % L || is_pow2(L) || !one_kernel_len(n / L) || !one_kernel_len(L)) continue;
-    gdsp_plan *p1 = nullptr;
-    if (get_plan_locked(dev, L, &p1) != GDSP_OK || p1->kind != KIND_MIXED) continue;
-    int rad[16], np = p1->md.npass;
-    if (np < 2 || np > 16) continue;
-    for (int q = 0; q < np; ++q) rad[q] = (int)((p1->md.codes >> (5 * q)) & 31);
-    gdsp::JitCol *col = gdsp::jit_col_build(dev, rad, np);
-    if (!col) continue;
-    p->mixcol = col;
-    p->n1 = L;
-    p->n2 = n / L;
-    p->p1 = p1;
+    if (mixcol_try(dev, n, L, p)) return true;
+  }
+  return false;
+}
+
+// n = L * 2^k, 2^k in [16, 1024], with a column pass for L (one radix <= 25:
+// colradix_kernel; 26 <= L <= 1016 smooth: the runtime-compiled
+// colfixed_kernel): two HBM passes, the columns and then the rows of 2^k
+// with the transpose in their store (rowfft_t_kernel), instead of three.
+// Rows of 256 first (256-B output segments), then shorter ones (longer
+// segments, longer columns), then 512 and 1024.
+bool pow2rows_build(int dev, int64_t n, gdsp_plan *p) {
+  if (gdsp::dev_switch("GDSP_MX3")) return false;  // development build: three passes
+  for (int k : {8, 7, 6, 5, 4, 9, 10}) {
+    const int64_t C = (int64_t)1 << k;
+    if (n % C) continue;
+    const int64_t L = n / C;
+    if (L < 2 || is_pow2(L)) continue;
+    if (L <= 25 && gdsp::colradix_supported((int)L)) {
+      p->radixcol = true;
+      p->n1 = L;
+      p->n2 = C;
+    } else if (!mixcol_try(dev, n, L, p)) {
+      continue;
+    }
+    p->rowst = true;
     return true;
   }
   return false;
@@ -705,6 +741,12 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
     }
   }
   if (!chirpz && mixed_radices(n, rad)) return build_mixed(dev, n, rad, p);
+  if (!chirpz && next_pow2_ref(2 * n - 1) > ((int64_t)1 << gdsp::kMaxLdsLog2) &&
+      pow2rows_build(dev, n, p)) {
+    p->kind = KIND_MIXED4;
+    STCHK(get_plan_locked(dev, p->n2, &p->p2));
+    return upload_twiddles(dev, n, &p->tw);
+  }
   if (!chirpz && next_pow2_ref(2 * n - 1) > ((int64_t)1 << gdsp::kMaxLdsLog2) &&
       pow2col_split(n, p->n1, p->n2)) {
     // n = 2^a * C with 2^a in [16, 512] and C a one-kernel length: the
@@ -984,7 +1026,7 @@ int exec_fourstep2(const gdsp_plan *p, const void *in, cd *out, int64_t batch, b
     HIPCHK(gdsp::launch_colfft(lr, inv, 2, false, src + b0 * N, w + b0 * N, C, 1, 0, 1, 0, 1,
                                pr->tw, p->tw, ln, 1.0, nb, N, s));
   }
-  HIPCHK(gdsp::launch_rowfft_t(lc, inv ? 1 : 0, w, out, batch * R, lr, pcol->tw, 1.0 / (double)N,
+  HIPCHK(gdsp::launch_rowfft_t(lc, inv ? 1 : 0, w, out, batch * R, R, pcol->tw, 1.0 / (double)N,
                                s));
   return GDSP_OK;
 }
@@ -1071,6 +1113,30 @@ int mixed4_col_rows(const gdsp_plan *p, const cd *src, cd *w, int64_t batch, boo
 int exec_mixed4(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
                 hipStream_t s) {
   const int64_t N = p->n, N1 = p->n1, N2 = p->n2;
+  if (p->rowst) {
+    // columns DFT_N1 times W_N^(col*k1) (conj in for an inverse), then rows
+    // DFT_N2 (a power of 2) whose store carries the transpose (and conj +
+    // 1/N for an inverse)
+    DevBuf work;
+    STCHK(work.alloc((size_t)batch * (size_t)N * sizeof(cd), s, SLOT_MX0));
+    cd *w = (cd *)work.p;
+    const cd *src = (const cd *)in;
+    if (load == gdsp::LOAD_REAL) {
+      HIPCHK(gdsp::launch_real_to_complex((const double *)in, w, batch * N, s));
+      src = w;
+    }
+    for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+      const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+      if (p->mixcol)
+        HIPCHK(gdsp::jit_launch_col(p->mixcol, inv, src + b0 * N, w + b0 * N, N2, N, nb, p->p1->tw,
+                                    p->tw, s));
+      else
+        HIPCHK(gdsp::launch_colradix((int)N1, inv, src + b0 * N, w + b0 * N, N2, N, nb, p->tw, s));
+    }
+    HIPCHK(gdsp::launch_rowfft_t(ilog2(N2), inv ? 1 : 0, w, out, batch * N1, N1, p->p2->tw,
+                                 1.0 / (double)N, s));
+    return GDSP_OK;
+  }
   if (p->pow2col || p->radixcol || p->mixcol) {
     // as exec_fourstep with R = N1 (power of 2) and C = N2 (any one-kernel
     // length): column DFT_R on row-segment tiles times W_N^(col*k1) (table
@@ -1188,10 +1254,10 @@ int exec_bluestein_composed(const gdsp_plan *p, const cd *in, cd *out, int64_t b
                                      1, pr->tw, p->mplan->tw, p->log2m, 1.0, nb, M, s));
       }
       if (pass == 1)
-        HIPCHK(gdsp::launch_rowfft_t(lc2, 2, w, da, batch * R, lr2, pcol->tw, 1.0, s, p->bhat,
+        HIPCHK(gdsp::launch_rowfft_t(lc2, 2, w, da, batch * R, R, pcol->tw, 1.0, s, p->bhat,
                                      p->n, false));
       else
-        HIPCHK(gdsp::launch_rowfft_t(lc2, 3, w, out, batch * R, lr2, pcol->tw,
+        HIPCHK(gdsp::launch_rowfft_t(lc2, 3, w, out, batch * R, R, pcol->tw,
                                      1.0 / (double)p->n, s, p->chirp, p->n, inv));
     }
     return GDSP_OK;

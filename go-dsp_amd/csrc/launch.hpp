@@ -173,13 +173,12 @@ constexpr int kColMinLog2 = 4, kColMaxLog2 = 9;
 hipError_t launch_colfft_chirp(int log2l, bool conj_in, const cd *x, cd *out, int64_t C,
                                int64_t n, const cd *chirp, const cd *twl, const cd *twr,
                                int64_t batch, hipStream_t s);
-// row DFT_C (C = 2^log2c, 8 ... 10) of `rows` rows (a multiple of R = 2^log2r
-// per transform) with the four-step transpose fused into the store:
-// out[b N + k2 R + k1] = DFT_C(in row b R + k1)[k2] (fft_kernels.hip). mode 0
-// as is, 1 conj and scale (inverse), 2 conj(X tab) (the composed chirp-z's
-// b-hat step), 3 conj(X) tab for k < n into rows of n (its output step; inv:
-// conj and scale)
-hipError_t launch_rowfft_t(int log2c, int mode, const cd *in, cd *out, int64_t rows, int log2r,
+// row DFT_C (C = 2^log2c, 4 ... 10) of `rows` rows (batch * R, any R) with
+// the four-step transpose fused into the store: out[b N + k2 R + k1] =
+// DFT_C(in row b R + k1)[k2] (fft_kernels.hip). mode 0 as is, 1 conj and
+// scale (inverse), 2 conj(X tab) (the composed chirp-z's b-hat step), 3
+// conj(X) tab for k < n into rows of n (its output step; inv: conj and scale)
+hipError_t launch_rowfft_t(int log2c, int mode, const cd *in, cd *out, int64_t rows, int64_t R,
                            const cd *tw, double scale, hipStream_t s, const cd *tab = nullptr,
                            int64_t n = 0, bool inv = false);
 hipError_t launch_colfft(int log2l, bool conj_in, int twiddle, bool conj_scale_out, const cd *in,
