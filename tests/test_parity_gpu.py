@@ -160,6 +160,27 @@ def test_fourstep_two_pass(gdsp, oracle, log2n, batch):
     assert row_nrel(xt.cpu().numpy(), ref) < TOL
 
 
+@pytest.mark.parametrize("n,batch", [(10000, 3), (12000, 2), (48000, 3), (196608, 1), (160000, 2)])
+def test_mixed_fourstep_two_pass(gdsp, oracle, n, batch):
+    # n = L * 2^k: the column pass, then rows of 2^k whose store carries the
+    # transpose (rowfft_t_kernel with R = L, not a power of 2; the last
+    # workgroup's rows run past batch * L), forward / inverse / real / in place
+    import torch
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    assert D.plan(n).kind == 6
+    rng = np.random.default_rng(n + batch)
+    x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
+    ref = oracle.fft_rows(x)
+    assert row_nrel(gdsp.fft.FFTBatch(x), ref) < TOL
+    assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL
+    xr = x.real.copy()
+    assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
+    xt = torch.from_numpy(x).cuda()
+    D.fft_batch(xt, xt)
+    torch.cuda.synchronize()
+    assert row_nrel(xt.cpu().numpy(), ref) < TOL
+
+
 @pytest.mark.parametrize("n", [2, 4, 8, 16, 32, 64, 128, 256])
 def test_short_rows_many_blocks(gdsp, oracle, n):
     # short transforms stage whole workgroup chunks through LDS: several
