@@ -325,6 +325,7 @@ struct gdsp_plan {
   // rowst: n2 a power of 2 in [16, 1024] and n1 a radixcol / mixcol column:
   // two passes, the rows' store carrying the transpose (rowfft_t_kernel)
   bool rowst = false;
+  gdsp::JitRowT *rowt = nullptr;  // rowst with n2 smooth, not a power of 2: the rows' kernel
   // mixcol: n1 in [26, 1016] smooth, its column pass runtime-compiled
   gdsp::JitCol *mixcol = nullptr;
   gdsp_plan *p1 = nullptr, *p2 = nullptr;
@@ -624,6 +625,60 @@ bool pow2rows_build(int dev, int64_t n, gdsp_plan *p) {
   return false;
 }
 
+// n = L * C with C <= 1024 a smooth one-kernel length (not a power of 2; its
+// rows by the runtime-compiled rowt_fixed_kernel, the transpose in their
+// store) and a column pass for L (a power of 2 in [16, 512], one radix <= 25
+// or a runtime-compiled column length in [26, 1016]): two HBM passes where
+// pow2rows_build finds no power-of-2 row length (10^6 = 1000 x 1000, 44100).
+// The longest C first (longest row segments per HBM pass, shortest columns).
+bool mixrows_build(int dev, int64_t n, gdsp_plan *p) {
+  // (below 50000 the three-pass plans held their own: 44100 2.35 against
+  // 2.42 ms per 2^27 samples, 30000 2.50 against 2.31; profiles/r04/
+  // mixed4_rows_ab.txt)
+  if (gdsp::dev_switch("GDSP_MX3") || !gdsp::jit_enabled() || n < 50000) return false;
+  for (int64_t C = 1024; C >= 16; --C) {
+    if (n % C || is_pow2(C) || !one_kernel_len(C)) continue;
+    const int64_t L = n / C;
+    // columns of at least 64 (rows of 1000 over columns of 30 / 45, 30000 /
+    // 44100, measured 10-25 % slower than the three-pass plans)
+    if (L < 64) continue;
+    const bool p2col = is_pow2(L) && L >= 16 && L <= 512;
+    const bool rcol = !is_pow2(L) && L <= 25 && gdsp::colradix_supported((int)L);
+    const bool mcol = !is_pow2(L) && L >= 26 && L <= 1016 && one_kernel_len(L);
+    if (!p2col && !rcol && !mcol) continue;
+    gdsp_plan *pc = nullptr;
+    if (get_plan_locked(dev, C, &pc) != GDSP_OK || pc->kind != KIND_MIXED) continue;
+    int rad[16], np = pc->md.npass;
+    if (np < 1 || np > 16) continue;
+    for (int q = 0; q < np; ++q) rad[q] = (int)((pc->md.codes >> (5 * q)) & 31);
+    gdsp_plan save = *p;
+    if (p2col) {
+      p->pow2col = true;
+      p->n1 = L;
+      p->n2 = C;
+      if (get_plan_locked(dev, L, &p->p1) != GDSP_OK) {
+        *p = save;
+        continue;
+      }
+    } else if (rcol) {
+      p->radixcol = true;
+      p->n1 = L;
+      p->n2 = C;
+    } else if (!mixcol_try(dev, n, L, p)) {
+      continue;
+    }
+    gdsp::JitRowT *rt = gdsp::jit_rowt_build(dev, rad, np);
+    if (!rt) {
+      *p = save;  // (a built column kernel stays cached in the JIT module list)
+      continue;
+    }
+    p->rowt = rt;
+    p->rowst = true;
+    return true;
+  }
+  return false;
+}
+
 #ifdef GDSP_DEV_BUILD
 // ---- measured and rejected chirp-z kernels (development build) ----
 // The wave-resident chirp-z kernel (fft_wave.hip) for 512 < n <= 4096, when
@@ -742,7 +797,7 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   }
   if (!chirpz && mixed_radices(n, rad)) return build_mixed(dev, n, rad, p);
   if (!chirpz && next_pow2_ref(2 * n - 1) > ((int64_t)1 << gdsp::kMaxLdsLog2) &&
-      pow2rows_build(dev, n, p)) {
+      (pow2rows_build(dev, n, p) || mixrows_build(dev, n, p))) {
     p->kind = KIND_MIXED4;
     STCHK(get_plan_locked(dev, p->n2, &p->p2));
     return upload_twiddles(dev, n, &p->tw);
@@ -1130,11 +1185,18 @@ int exec_mixed4(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool
       if (p->mixcol)
         HIPCHK(gdsp::jit_launch_col(p->mixcol, inv, src + b0 * N, w + b0 * N, N2, N, nb, p->p1->tw,
                                     p->tw, s));
-      else
+      else if (p->radixcol)
         HIPCHK(gdsp::launch_colradix((int)N1, inv, src + b0 * N, w + b0 * N, N2, N, nb, p->tw, s));
+      else
+        HIPCHK(gdsp::launch_colfft(ilog2(N1), inv, 2, false, src + b0 * N, w + b0 * N, N2, 1, 0, 1,
+                                   0, 1, p->p1->tw, p->tw, 0, 1.0, nb, N, s, N));
     }
-    HIPCHK(gdsp::launch_rowfft_t(ilog2(N2), inv ? 1 : 0, w, out, batch * N1, N1, p->p2->tw,
-                                 1.0 / (double)N, s));
+    if (p->rowt)
+      HIPCHK(gdsp::jit_launch_rowt(p->rowt, inv, w, out, batch * N1, N1, p->p2->tw,
+                                   1.0 / (double)N, s));
+    else
+      HIPCHK(gdsp::launch_rowfft_t(ilog2(N2), inv ? 1 : 0, w, out, batch * N1, N1, p->p2->tw,
+                                   1.0 / (double)N, s));
     return GDSP_OK;
   }
   if (p->pow2col || p->radixcol || p->mixcol) {

@@ -76,6 +76,12 @@ JitSpec *jit_spec_build(int dev, const int *rad, int np, int n);  // nullptr: no
 // colfixed_kernel (mixed_fixed.hpp) for the column length prod(rad)
 struct JitCol;
 JitCol *jit_col_build(int dev, const int *rad, int np);  // nullptr: not built
+// rowt_fixed_kernel (mixed_fixed.hpp) for the row length prod(rad): rows of
+// a two-pass mixed four-step with the transpose in their store
+struct JitRowT;
+JitRowT *jit_rowt_build(int dev, const int *rad, int np);  // nullptr: not built
+hipError_t jit_launch_rowt(const JitRowT *j, bool conj_scale_out, const cd *in, cd *out,
+                           int64_t rows, int64_t L, const cd *tw, double scale, hipStream_t s);
 hipError_t jit_launch_col(const JitCol *j, bool conj_in, const cd *in, cd *out, int64_t C,
                           int64_t n, int64_t batch, const cd *tw, const cd *twn, hipStream_t s);
 hipError_t jit_launch_fft(const JitSpec *j, bool inv, int load, const void *in, cd *out,

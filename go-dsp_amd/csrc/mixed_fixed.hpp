@@ -23,6 +23,7 @@ namespace gdsp {
 // four barriers).
 template <int R, int N, int NS, int T1>
 struct FPass {
+  static constexpr int RV = R, NSV = NS;  // (the pass's radix and stride, for sinks)
   static constexpr int NB = N / R;
   static constexpr int J = (NB + T1 - 1) / T1;
   static constexpr bool FULL = NB % T1 == 0;
@@ -289,6 +290,84 @@ __device__ __forceinline__ void fixed_chain_to(const Prev &prev, int tl, bool va
     fixed_chain_to<SPLIT, SWZ, N, T1, NS * R, TWOFF + NS, FPass<R, N, NS, T1>, F, REST...>(
         cur, tl, valid, lds, tw, sink);
   }
+}
+
+// Rows of a two-pass mixed four-step (n = L * N, N = prod RS a smooth
+// non-power-of-2 length <= 1024; gdsp_api.hip exec_mixed4): W consecutive
+// rows k1 of the L x N matrix per workgroup, DFT_N along each (the inlined
+// chain, exchanges as real / imaginary halves), then the transpose
+// X[k1 + L k2] = Y[k1][k2] through LDS into the store, so each store
+// wave-instruction writes W consecutive k1 (W * 16-B segments; the power-of-2
+// rows' rowfft_t_kernel does the same). CSO: conj and scale on the way out
+// (an inverse). `rows` = batch * L; rows past it load a valid row and store
+// nothing.
+template <int W, bool CSO, int N, int T1>
+struct RowtSink {  // the last pass's outputs, staged transposed and stored
+  double *lds;
+  cd *out;
+  int64_t L, rows, g0;
+  int sub, tl;
+  double scale;
+  template <class P>
+  __device__ __forceinline__ void operator()(const P &cur) const {
+    constexpr int NQ = (N + T1 - 1) / T1;
+    const int lt = (int)threadIdx.x, s = lt % W, a0 = lt / W;
+    const int64_t g = g0 + s, b = g / L, k1 = g - b * L;
+    cd *dst = out + b * L * N + k1;
+    double re[NQ];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      __syncthreads();  // every read of the last exchange (or the real parts) is done
+#pragma unroll
+      for (int jj = 0; jj < P::J; ++jj) {
+        const int j = tl + jj * T1;
+        if (P::act(j, true)) {
+          const int k = j % P::NSV, o = (j - k) * P::RV + k;
+#pragma unroll
+          for (int r = 0; r < P::RV; ++r)
+            lds[(o + r * P::NSV) * (W + 1) + sub] = h ? cur.v[jj][r].y : cur.v[jj][r].x;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int a = a0 + q * T1;
+        if (a < N) {
+          const double d = lds[a * (W + 1) + s];
+          if (h == 0) {
+            re[q] = d;
+          } else if (g < rows) {
+            cd o = {re[q], d};
+            if constexpr (CSO) o = {o.x * scale, -o.y * scale};
+            st_nt(&dst[(int64_t)a * L], o);
+          }
+        }
+      }
+    }
+  }
+};
+
+template <int W, bool CSO, bool SWZ, int R0, int... RS>
+__global__ __launch_bounds__((W * FixedGeo<R0, RS...>::T1)) void rowt_fixed_kernel(
+    const cd *__restrict__ in, cd *__restrict__ out, int64_t L, int64_t rows,
+    const cd *__restrict__ tw, double scale) {
+  using G = FixedGeo<R0, RS...>;
+  constexpr int N = G::N, T1 = G::T1, SL = G::SLOTS;
+  constexpr int XD = W * SL, SD = N * (W + 1);
+  __shared__ double lds[XD > SD ? XD : SD];
+  const int sub = (int)threadIdx.x / T1;
+  const int tl = (int)threadIdx.x - sub * T1;
+  const int64_t g0 = (int64_t)blockIdx.x * W;
+  const int64_t gl = g0 + sub < rows ? g0 + sub : rows - 1;
+  RowtSink<W, CSO, N, T1> sink{lds, out, L, rows, g0, sub, tl, scale};
+  FPass<R0, N, 1, T1> p0;
+  p0.template load_hbm<false, LOAD_COMPLEX>(tl, true, in + gl * N);
+  p0.compute(tl, true, tw);
+  if constexpr (sizeof...(RS) == 0)
+    sink(p0);
+  else
+    fixed_chain_to<true, SWZ, N, T1, R0, 0, FPass<R0, N, 1, T1>, RowtSink<W, CSO, N, T1>, RS...>(
+        p0, tl, true, lds + sub * SL, tw, sink);
 }
 
 template <int R0, int... RS>

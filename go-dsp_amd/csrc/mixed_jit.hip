@@ -54,6 +54,11 @@ struct JitCol {  // colfixed_kernel for one column length
   hipFunction_t fwd = nullptr, inv = nullptr;
   int l = 0, w = 0, wg = 0;
 };
+struct JitRowT {  // rowt_fixed_kernel for one row length (forward, conj + scale out)
+  hipModule_t mod = nullptr;
+  hipFunction_t fwd = nullptr, cso = nullptr;
+  int n = 0, w = 0, wg = 0;
+};
 
 namespace {
 
@@ -440,6 +445,51 @@ JitCol *jit_col_build(int dev, const int *rad, int np) {
   j->w = w;
   j->wg = w * t1;
   return j;
+}
+
+JitRowT *jit_rowt_build(int dev, const int *rad, int np) {
+  if (!jit_enabled() || np < 1) return nullptr;
+  int n = 1;
+  for (int q = 0; q < np; ++q) n *= rad[q];
+  int t1 = 0, tpw = 0;
+  fixed_geo(rad, np, &t1, &tpw);
+  // rows per workgroup: the widest of 16, 8, 4 within 1024 threads and 80 KiB
+  // of LDS (two workgroups per CU): the exchange (W rows of n-double halves)
+  // or the transposed staging (n x (W + 1) doubles), whichever is larger
+  const int sl = (n + 7) & ~7;
+  int w = 16;
+  while (w >= 4 && (w * t1 > 1024 || 8 * std::max(w * sl, n * (w + 1)) > 81920)) w >>= 1;
+  if (w < 4) return nullptr;
+  const std::string list = radix_list(rad, np), sw = rad[0] % 2 == 0 ? "true" : "false";
+  const std::string ws = std::to_string(w);
+  const std::vector<std::string> names = {
+      "&gdsp::rowt_fixed_kernel<" + ws + ", false, " + sw + list + ">",
+      "&gdsp::rowt_fixed_kernel<" + ws + ", true, " + sw + list + ">"};
+  hipModule_t mod = nullptr;
+  std::vector<hipFunction_t> fs;
+  if (!compile_module(dev, names, "transposed rows for C = " + std::to_string(n) + " (" +
+                                      list.substr(2) + "), " + ws + " rows",
+                      &mod, fs))
+    return nullptr;
+  JitRowT *j = new JitRowT;
+  j->mod = mod;
+  j->fwd = fs[0];
+  j->cso = fs[1];
+  j->n = n;
+  j->w = w;
+  j->wg = w * t1;
+  return j;
+}
+
+hipError_t jit_launch_rowt(const JitRowT *j, bool conj_scale_out, const cd *in, cd *out,
+                           int64_t rows, int64_t L, const cd *tw, double scale, hipStream_t s) {
+  if (rows < 1 || L < 1 || rows % L) return hipErrorInvalidValue;
+  const int64_t gx = (rows + j->w - 1) / j->w;
+  if (gx > 0x7fffffff) return hipErrorInvalidValue;
+  void *args[] = {(void *)&in, (void *)&out, (void *)&L, (void *)&rows, (void *)&tw,
+                  (void *)&scale};
+  return hipModuleLaunchKernel(conj_scale_out ? j->cso : j->fwd, (unsigned)gx, 1, 1,
+                               (unsigned)j->wg, 1, 1, 0, s, args, nullptr);
 }
 
 hipError_t jit_launch_col(const JitCol *j, bool conj_in, const cd *in, cd *out, int64_t C,

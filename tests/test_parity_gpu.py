@@ -181,6 +181,27 @@ def test_mixed_fourstep_two_pass(gdsp, oracle, n, batch):
     assert row_nrel(xt.cpu().numpy(), ref) < TOL
 
 
+@pytest.mark.parametrize("n,batch", [(50000, 3), (88200, 1), (100000, 2), (600000, 1), (1000000, 1)])
+def test_mixed_rows_two_pass(gdsp, oracle, n, batch):
+    # n = L * C with C <= 1024 smooth (not a power of 2): the column pass, then
+    # rows of C by the runtime-compiled rowt_fixed_kernel with the transpose in
+    # their store; forward / inverse / real / in place
+    import torch
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    assert D.plan(n).kind == 6
+    rng = np.random.default_rng(n + 7 * batch)
+    x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
+    ref = oracle.fft_rows(x)
+    assert row_nrel(gdsp.fft.FFTBatch(x), ref) < TOL
+    assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL
+    xr = x.real.copy()
+    assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
+    xt = torch.from_numpy(x).cuda()
+    D.fft_batch(xt, xt)
+    torch.cuda.synchronize()
+    assert row_nrel(xt.cpu().numpy(), ref) < TOL
+
+
 @pytest.mark.parametrize("n", [2, 4, 8, 16, 32, 64, 128, 256])
 def test_short_rows_many_blocks(gdsp, oracle, n):
     # short transforms stage whole workgroup chunks through LDS: several
