@@ -630,18 +630,29 @@ bool pow2rows_build(int dev, int64_t n, gdsp_plan *p) {
 // store) and a column pass for L (a power of 2 in [16, 512], one radix <= 25
 // or a runtime-compiled column length in [26, 1016]): two HBM passes where
 // pow2rows_build finds no power-of-2 row length (10^6 = 1000 x 1000, 44100).
-// The longest C first (longest row segments per HBM pass, shortest columns).
+// Rows of 1000 (10 x 10 x 10) first where the columns are >= 64 points long,
+// then the split closest to C = sqrt(n): per 2^27 samples (profiles/r04/
+// mixed4_rows_ab.txt) 10^6, 600000, 200000, 100000, 50000 took 1.6-2.0 ms
+// on rows of 1000 but up to 3.1 on the balanced split, while 44100 took
+// 1.93-2.03 ms at C = 225 / 210 and 2.42 at 630 (2.34 in three passes), and
+// 30000 1.78 at C = 150 and 2.50 at 1000.
 bool mixrows_build(int dev, int64_t n, gdsp_plan *p) {
-  // (below 50000 the three-pass plans held their own: 44100 2.35 against
-  // 2.42 ms per 2^27 samples, 30000 2.50 against 2.31; profiles/r04/
-  // mixed4_rows_ab.txt)
-  if (gdsp::dev_switch("GDSP_MX3") || !gdsp::jit_enabled() || n < 50000) return false;
-  for (int64_t C = 1024; C >= 16; --C) {
-    if (n % C || is_pow2(C) || !one_kernel_len(C)) continue;
+  if (gdsp::dev_switch("GDSP_MX3") || !gdsp::jit_enabled()) return false;
+  static const int64_t force_c = [] {  // development build: GDSP_MXROW_C, the row length
+    const char *e = gdsp::dev_switch("GDSP_MXROW_C");
+    return e ? (int64_t)atoll(e) : (int64_t)0;
+  }();
+  std::vector<int64_t> cands;
+  for (int64_t C = 16; C <= 1024; ++C)
+    if (n % C == 0 && !is_pow2(C) && n / C >= 64 && (!force_c || C == force_c)) cands.push_back(C);
+  const long double r = sqrtl((long double)n);
+  std::stable_sort(cands.begin(), cands.end(), [r](int64_t a, int64_t b) {
+    if ((a == 1000) != (b == 1000)) return a == 1000;
+    return fabsl((long double)a - r) < fabsl((long double)b - r);
+  });
+  for (const int64_t C : cands) {
+    if (!one_kernel_len(C)) continue;
     const int64_t L = n / C;
-    // columns of at least 64 (rows of 1000 over columns of 30 / 45, 30000 /
-    // 44100, measured 10-25 % slower than the three-pass plans)
-    if (L < 64) continue;
     const bool p2col = is_pow2(L) && L >= 16 && L <= 512;
     const bool rcol = !is_pow2(L) && L <= 25 && gdsp::colradix_supported((int)L);
     const bool mcol = !is_pow2(L) && L >= 26 && L <= 1016 && one_kernel_len(L);

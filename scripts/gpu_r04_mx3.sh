@@ -8,7 +8,7 @@ timeout -k 10 900 python -u -m pytest tests/test_parity_gpu.py -m gpu -q -x --ti
 echo "pytest rc=$rc $(tail -1 gpurun_out/mx3_pytest.log)"; [ $rc -eq 0 ] || { grep -E "^FAILED|Error|assert|hipRTC" gpurun_out/mx3_pytest.log | head -20; exit $rc; }
 unset GDSP_JIT_VERBOSE
 DEV=$GRAFT_REPO_ROOT/go-dsp_amd/lib_dev/libgdspfft.so
-SZ="30000 44100 88200 100000 1000000 600000 50000 200000"
+SZ="9000 27000 30000 44100 50000 60000 72000 88200 100000 200000 600000 1000000 4961250"
 for r in 1 2; do
   timeout -k 10 300 python scripts/bench_sizes_default.py $SZ > gpurun_out/mx3_new_$r.jsonl 2>> gpurun_out/mx3.err || exit $?
   GDSP_LIB=$DEV GDSP_MX3=1 timeout -k 10 300 python scripts/bench_sizes_default.py $SZ > gpurun_out/mx3_old_$r.jsonl 2>> gpurun_out/mx3.err || exit $?
