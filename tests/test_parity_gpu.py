@@ -181,7 +181,8 @@ def test_mixed_fourstep_two_pass(gdsp, oracle, n, batch):
     assert row_nrel(xt.cpu().numpy(), ref) < TOL
 
 
-@pytest.mark.parametrize("n,batch", [(50000, 3), (88200, 1), (100000, 2), (600000, 1), (1000000, 1)])
+@pytest.mark.parametrize("n,batch", [(9000, 5), (44100, 2), (50000, 3), (88200, 1), (100000, 2),
+                                     (600000, 1), (1000000, 1)])
 def test_mixed_rows_two_pass(gdsp, oracle, n, batch):
     # n = L * C with C <= 1024 smooth (not a power of 2): the column pass, then
     # rows of C by the runtime-compiled rowt_fixed_kernel with the transpose in
