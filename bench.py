@@ -111,12 +111,12 @@ class Ctx:
         self.backend = os.environ.get("GDSP_DIST_BACKEND", "nccl")
         if self.world > 1:
             ndev = torch.cuda.device_count()
-            if self.backend == "nccl" and ndev < self.world:
-                raise SystemExit(f"bench.py: {self.world} ranks over nccl (RCCL) need "
-                                 f"{self.world} GPUs, this node has {ndev}")
+            err = rank_device_check(ndev, local, self.backend, dict(os.environ), self.world)
+            if err:
+                raise SystemExit(f"bench.py: {err}")
             torch.cuda.set_device(local % ndev)
             if self.backend == "nccl":
-                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local % ndev))
             else:
                 dist.init_process_group(self.backend)
         else:
@@ -721,10 +721,87 @@ def launch(cmd: list, ranks: list, poll_s: float = 0.2) -> int:
     return rc if rc >= 0 else 128 - rc  # a signalled child: 128 + signal number
 
 
+def rank_device_check(ndev: int, local: int, backend: str, env: dict, world: int):
+    """A rank's own check before it binds a GPU (None: fine, else the reason).
+    RCCL needs one GPU per rank of this node, so the ranks on this node
+    (LOCAL_WORLD_SIZE, set by torch.distributed.run and by launch(); WORLD_SIZE
+    only when neither set it) are compared with the GPUs this rank sees. A
+    launcher that hands each rank its own GPU through a visibility variable
+    leaves every rank one device, which is fine. Multi-node jobs pass, since
+    only the node's own ranks count."""
+    if backend != "nccl":
+        return None  # the gloo rehearsal may share one GPU
+    local_world = int(env.get("LOCAL_WORLD_SIZE", str(world)))
+    if ndev >= local_world and local < ndev:
+        return None
+    if ndev == 1 and _visible_limit(env) == 1:
+        return None
+    return (f"{local_world} ranks on this node over nccl (RCCL) need {local_world} GPUs, "
+            f"rank {local} sees {ndev}")
+
+
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def _visible_limit(env: dict):
+    """How many devices the visibility variables leave (None: no limit). The
+    HIP runtime honours ROCR_VISIBLE_DEVICES, then HIP_VISIBLE_DEVICES /
+    CUDA_VISIBLE_DEVICES on top of it; each is a comma list of indices or
+    UUIDs, so the count is its number of entries (an empty value hides all)."""
+    lim = None
+    for k in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(k)
+        if v is None:
+            continue
+        n = len([p for p in v.split(",") if p.strip()])
+        lim = n if lim is None else min(lim, n)
+    return lim
+
+
+def kfd_gpu_count(root: str = None, env: dict = None):
+    """GPUs in the KFD topology (sysfs): nodes with a nonzero gpu_id and SIMDs.
+    Reading sysfs loads no HIP/HSA runtime, so the launcher parent stays free
+    of any GPU state before it starts the ranks. None when the topology is not
+    readable (no amdgpu driver, or a sandbox without /sys)."""
+    env = os.environ if env is None else env
+    root = KFD_NODES if root is None else root
+    try:
+        nodes = os.listdir(root)
+    except OSError:
+        return None
+    n = 0
+    for d in nodes:
+        try:
+            with open(os.path.join(root, d, "gpu_id")) as f:
+                gid = int(f.read().strip() or "0")
+            simd = 0
+            with open(os.path.join(root, d, "properties")) as f:
+                for line in f:
+                    k, _, v = line.partition(" ")
+                    if k == "simd_count":
+                        simd = int(v)
+        except (OSError, ValueError):
+            continue
+        if gid != 0 and simd > 0:
+            n += 1
+    lim = _visible_limit(env)
+    return n if lim is None else min(n, lim)
+
+
 def _device_count() -> int:
-    # counting devices does not initialise the GPU (no HIP context is made)
-    import torch
-    return torch.cuda.device_count()
+    """GPUs visible to the ranks, counted without initialising HIP in this
+    (launcher) process: the KFD topology in sysfs, or else a short-lived
+    child process that asks torch (its runtime dies with it)."""
+    n = kfd_gpu_count()
+    if n is not None:
+        return n
+    import subprocess
+    p = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True, timeout=600)
+    try:
+        return int(p.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return 0
 
 
 def main():

@@ -644,10 +644,14 @@ bool mixrows_build(int dev, int64_t n, gdsp_plan *p) {
   }();
   std::vector<int64_t> cands;
   for (int64_t C = 16; C <= 1024; ++C)
-    if (n % C == 0 && !is_pow2(C) && n / C >= 64 && (!force_c || C == force_c)) cands.push_back(C);
+    if (n % C == 0 && !is_pow2(C) && (!force_c || C == force_c)) cands.push_back(C);
   const long double r = sqrtl((long double)n);
-  std::stable_sort(cands.begin(), cands.end(), [r](int64_t a, int64_t b) {
-    if ((a == 1000) != (b == 1000)) return a == 1000;
+  // the rows-of-1000 preference holds only where its columns are >= 64
+  // points; every other candidate (short columns included: the single-radix
+  // colradix_kernel takes L <= 25) is ordered by its distance from sqrt(n)
+  auto pref = [n](int64_t c) { return c == 1000 && n / c >= 64; };
+  std::stable_sort(cands.begin(), cands.end(), [r, pref](int64_t a, int64_t b) {
+    if (pref(a) != pref(b)) return pref(a);
     return fabsl((long double)a - r) < fabsl((long double)b - r);
   });
   for (const int64_t C : cands) {

@@ -301,6 +301,15 @@ int nccl_fail(const Rccl &r, ncclResult_t e, const char *what) {
 // a collective on it fails (drop_comms).
 std::mutex g_comms_mu;
 std::map<std::vector<int>, std::vector<ncclComm_t>> g_comms;
+// device lists whose clique ncclCommInitAll refused, with its message: later
+// calls on the same set go straight to the host sum instead of paying the
+// failed setup again
+std::map<std::vector<int>, std::string> g_comms_refused;
+
+bool clique_refused(const std::vector<int> &devs) {
+  std::lock_guard<std::mutex> lk(g_comms_mu);
+  return g_comms_refused.count(devs) != 0;
+}
 
 int comms_for(const std::vector<int> &devs, std::vector<ncclComm_t> **out) {
   auto &mu = g_comms_mu;
@@ -308,11 +317,17 @@ int comms_for(const std::vector<int> &devs, std::vector<ncclComm_t> **out) {
   const Rccl &r = rccl();
   if (!r.why.empty()) return set_error(GDSP_ERR_UNSUPPORTED, r.why);
   std::lock_guard<std::mutex> lk(mu);
+  auto bad = g_comms_refused.find(devs);
+  if (bad != g_comms_refused.end()) return set_error(GDSP_ERR_UNSUPPORTED, bad->second);
   auto it = cache.find(devs);
   if (it == cache.end()) {
     std::vector<ncclComm_t> c(devs.size());
     const ncclResult_t e = r.init_all(c.data(), (int)devs.size(), devs.data());
-    if (e != ncclSuccess) return nccl_fail(r, e, "ncclCommInitAll");
+    if (e != ncclSuccess) {
+      const int st = nccl_fail(r, e, "ncclCommInitAll");
+      g_comms_refused.emplace(devs, std::string(gdsp_last_error()));
+      return st;
+    }
     it = cache.emplace(devs, std::move(c)).first;
   }
   *out = &it->second;
@@ -458,7 +473,7 @@ int pwelch_multi(const double *x, int64_t n, double fs, int64_t nfft, int64_t pa
     std::vector<int> sorted(devs);
     std::sort(sorted.begin(), sorted.end());
     const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-    const bool use_rccl = distinct && rccl().why.empty();
+    const bool use_rccl = distinct && rccl().why.empty() && !clique_refused(devs);
     bool reduced_by_rccl = false;
     std::vector<std::vector<double>> part((size_t)D);
     std::vector<CallBuf> dacc((size_t)D);
@@ -503,16 +518,19 @@ int pwelch_multi(const double *x, int64_t n, double fs, int64_t nfft, int64_t pa
     auto reduce = [&]() -> int {
       const Rccl &r = rccl();
       std::vector<ncclComm_t> *comms = nullptr;
+      const std::string prev_error(gdsp_last_error());
       if (comms_for(devs, &comms) != GDSP_OK) {
-        // no clique for this set (e.g. ncclCommInitAll refused it): the
-        // accumulators come back to the host and are summed there
+        // no clique for this set (ncclCommInitAll refused it; cached, so the
+        // next call on this set skips RCCL): the accumulators come back to
+        // the host and are summed there, and the call succeeds without
+        // leaving the refusal as its last error
         for (int i = 0; i < D; ++i) {
           MHIPCHK(hipSetDevice(devs[i]));
           part[(size_t)i].resize((size_t)flen);
           MSTCHK(d2h(part[(size_t)i].data(), dacc[(size_t)i].p, (size_t)flen * sizeof(double),
                      streams[(size_t)i]));
         }
-        return GDSP_OK;
+        return set_error(GDSP_OK, prev_error);
       }
       ncclResult_t e = r.group_start();
       if (e != ncclSuccess) return nccl_fail(r, e, "ncclGroupStart");

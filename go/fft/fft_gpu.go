@@ -33,12 +33,27 @@ import (
 )
 
 // GPUMinN is the small-n policy: a one-vector FFT/IFFT/FFTReal/IFFTReal/
-// Convolve shorter than this stays on the reference's own pure-Go code
-// (radix2FFT / bluesteinFFT), which is faster than a launch + synchronisation
-// there (crossover n = 4096, bench.py configs.fftreal1024.small_n; INTEGRATION.md
-// "Small-n policy"). 0 sends every call to the GPU. FFT2, FFTN and FFTBatch
-// always run on the GPU.
+// Convolve whose largest transform is shorter than this stays on the
+// reference's own pure-Go code (radix2FFT / bluesteinFFT), which is faster
+// than a launch + synchronisation there (crossover n = 4096, bench.py
+// configs.fftreal1024.small_n; INTEGRATION.md "Small-n policy"). 0 sends
+// every call to the GPU. FFT2, FFTN and FFTBatch always run on the GPU.
 var GPUMinN = 4096
+
+// onHost applies GPUMinN to the largest transform the pure-Go code would run
+// for n: n itself for a power of 2, bluesteinFFT's convolution length
+// NextPowerOf2(2n-1) otherwise (bluestein.go:70). So a host call never
+// reaches the GPU from inside: bluesteinFFT's Convolve (bluestein.go:87),
+// which is this package's Convolve, gets that power-of-2 length and stays on
+// the host too; a non-power-of-2 n whose convolution would be >= GPUMinN goes
+// to the GPU as one transform instead of a host Bluestein around a GPU
+// convolution.
+func onHost(n int) bool {
+	if dsputils.IsPowerOf2(n) {
+		return n < GPUMinN
+	}
+	return dsputils.NextPowerOf2(2*n-1) < GPUMinN
+}
 
 // read by radix2.go:92 (declared in fft.go:89-91 in the pure-Go build)
 var worker_pool_size = 0
@@ -78,7 +93,7 @@ func real64(x []float64) *C.double {
 // 2, bluesteinFFT (bluestein.go:68-94) otherwise. x is not modified; the
 // result is a fresh slice.
 func FFT(x []complex128) []complex128 {
-	if len(x) < GPUMinN {
+	if onHost(len(x)) {
 		return fftPureGo(x)
 	}
 	r := make([]complex128, len(x))
@@ -102,7 +117,7 @@ func fftPureGo(x []complex128) []complex128 {
 func IFFT(x []complex128) []complex128 {
 	_ = x[0]
 	n := len(x)
-	if n < GPUMinN {
+	if onHost(n) {
 		// fft.go:35-52 on the pure-Go FFT: reversed input, forward FFT, /n
 		rev := make([]complex128, n)
 		rev[0] = x[0]
@@ -124,7 +139,7 @@ func IFFT(x []complex128) []complex128 {
 // FFTReal replaces fft/fft.go:25-27: the float64 samples go over as they are
 // (the kernel reads real rows; no ToComplex copy).
 func FFTReal(x []float64) []complex128 {
-	if len(x) < GPUMinN {
+	if onHost(len(x)) {
 		return fftPureGo(dsputils.ToComplex(x))
 	}
 	r := make([]complex128, len(x))
@@ -135,7 +150,7 @@ func FFTReal(x []float64) []complex128 {
 // IFFTReal replaces fft/fft.go:30-32 (panics on an empty x like IFFT).
 func IFFTReal(x []float64) []complex128 {
 	_ = x[0]
-	if len(x) < GPUMinN {
+	if onHost(len(x)) {
 		return IFFT(dsputils.ToComplex(x))
 	}
 	r := make([]complex128, len(x))
@@ -148,7 +163,7 @@ func Convolve(x, y []complex128) []complex128 {
 	if len(x) != len(y) {
 		panic("arrays not of equal size")
 	}
-	if len(x) < GPUMinN {
+	if onHost(len(x)) {
 		fx, fy := fftPureGo(x), fftPureGo(y)
 		for i := range fx {
 			fx[i] *= fy[i]

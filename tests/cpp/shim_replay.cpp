@@ -47,6 +47,22 @@ namespace goshim {
 
 int GPUMinN = 4096;
 
+// dsputils.IsPowerOf2 / NextPowerOf2 (dsputils.go:34-45)
+static bool IsPowerOf2(int64_t x) { return (x & (x - 1)) == 0; }
+static int64_t NextPowerOf2(int64_t x) {
+  if (IsPowerOf2(x)) return x;
+  int64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+// the small-n policy on the largest transform the pure-Go code would run
+// (fft_gpu.go onHost): n for a power of 2, bluesteinFFT's M otherwise
+bool onHost(int64_t n) {
+  if (IsPowerOf2(n)) return n < GPUMinN;
+  return NextPowerOf2(2 * n - 1) < GPUMinN;
+}
+
 static void check(int st) {
   switch (st) {
     case GDSP_OK:
@@ -85,7 +101,7 @@ static std::vector<complex128> ToComplex(const std::vector<double> &x) {
 }
 
 std::vector<complex128> FFT(const std::vector<complex128> &x) {
-  if ((int)x.size() < GPUMinN) return fftPureGo(x);
+  if (onHost((int64_t)x.size())) return fftPureGo(x);
   std::vector<complex128> r(x.size());
   check(gdsp_fft(cplx(x), cplx(r), (int64_t)x.size()));
   return r;
@@ -94,7 +110,7 @@ std::vector<complex128> FFT(const std::vector<complex128> &x) {
 std::vector<complex128> IFFT(const std::vector<complex128> &x) {
   index0(x);
   const size_t n = x.size();
-  if ((int)n < GPUMinN) {
+  if (onHost((int64_t)n)) {
     std::vector<complex128> rev(n);
     rev[0] = x[0];
     for (size_t i = 1; i < n; ++i) rev[i] = x[n - i];
@@ -108,7 +124,7 @@ std::vector<complex128> IFFT(const std::vector<complex128> &x) {
 }
 
 std::vector<complex128> FFTReal(const std::vector<double> &x) {
-  if ((int)x.size() < GPUMinN) return fftPureGo(ToComplex(x));
+  if (onHost((int64_t)x.size())) return fftPureGo(ToComplex(x));
   std::vector<complex128> r(x.size());
   check(gdsp_fft_real(real64(x), cplx(r), (int64_t)x.size()));
   return r;
@@ -116,7 +132,7 @@ std::vector<complex128> FFTReal(const std::vector<double> &x) {
 
 std::vector<complex128> IFFTReal(const std::vector<double> &x) {
   index0(x);
-  if ((int)x.size() < GPUMinN) return IFFT(ToComplex(x));
+  if (onHost((int64_t)x.size())) return IFFT(ToComplex(x));
   std::vector<complex128> r(x.size());
   check(gdsp_ifft_real(real64(x), cplx(r), (int64_t)x.size()));
   return r;
@@ -124,7 +140,7 @@ std::vector<complex128> IFFTReal(const std::vector<double> &x) {
 
 std::vector<complex128> Convolve(const std::vector<complex128> &x, const std::vector<complex128> &y) {
   if (x.size() != y.size()) throw GoPanic("arrays not of equal size");
-  if ((int)x.size() < GPUMinN) {
+  if (onHost((int64_t)x.size())) {
     auto fx = fftPureGo(x), fy = fftPureGo(y);
     for (size_t i = 0; i < fx.size(); ++i) fx[i] *= fy[i];
     return IFFT(fx);
@@ -492,7 +508,16 @@ int main(int argc, char **argv) {
 
   // FFT / IFFT / FFTReal / IFFTReal / Convolve: below, at and above GPUMinN,
   // powers of 2 and not, against the restatement of the reference
-  for (size_t n : {1ul, 2ul, 5ul, 1024ul, 3000ul, 4095ul, 4096ul, 5000ul, 65536ul}) {
+  // the small-n policy on bluesteinFFT's convolution length (fft_gpu.go
+  // onHost): non-powers of 2 in (1024, 4096) convolve on M = 4096
+  // or 8192 >= GPUMinN, so they go to the GPU as one transform rather than a
+  // host Bluestein around a GPU Convolve; up to 1024 they stay on the host
+  EXPECT(goshim::onHost(1000) && goshim::onHost(1024) && goshim::onHost(2048) &&
+             !goshim::onHost(1025) && !goshim::onHost(1500) && !goshim::onHost(3000) &&
+             !goshim::onHost(4096) && goshim::onHost(0) && goshim::onHost(1),
+         "onHost policy");
+  for (size_t n : {1ul, 2ul, 5ul, 1000ul, 1024ul, 1025ul, 1500ul, 2048ul, 3000ul, 4095ul, 4096ul,
+                   5000ul, 65536ul}) {
     auto x = randc(n, 100 + n);
     EXPECT(nrel(goshim::FFT(x), oracle1(x, false)) < 1e-9, "FFT n=" << n);
     EXPECT(nrel(goshim::IFFT(x), oracle1(x, true)) < 1e-9, "IFFT n=" << n);

@@ -135,3 +135,57 @@ def test_bench_nccl_without_enough_gpus_exits_nonzero():
                        env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 2 and "needs 2 GPUs" in p.stderr, (p.returncode, p.stderr)
     assert p.stdout.strip() == ""
+
+
+def _fake_kfd(root, nodes):
+    # nodes: list of (gpu_id, simd_count); node 0 of a real topology is the CPU
+    for i, (gid, simd) in enumerate(nodes):
+        d = root / str(i)
+        d.mkdir(parents=True)
+        (d / "gpu_id").write_text(f"{gid}\n")
+        (d / "properties").write_text(f"cpu_cores_count 0\nsimd_count {simd}\nmax_waves_per_simd 8\n")
+    return str(root)
+
+
+def test_kfd_gpu_count_reads_sysfs(tmp_path):
+    b = _bench()
+    root = _fake_kfd(tmp_path / "nodes", [(0, 0)] + [(1000 + i, 1024) for i in range(8)])
+    assert b.kfd_gpu_count(root, env={}) == 8
+    assert b.kfd_gpu_count(root, env={"HIP_VISIBLE_DEVICES": "0,1"}) == 2
+    assert b.kfd_gpu_count(root, env={"ROCR_VISIBLE_DEVICES": "3", "HIP_VISIBLE_DEVICES": "0,1"}) == 1
+    assert b.kfd_gpu_count(root, env={"CUDA_VISIBLE_DEVICES": ""}) == 0
+    assert b.kfd_gpu_count(str(tmp_path / "missing"), env={}) is None
+
+
+def test_launcher_count_loads_no_gpu_runtime(tmp_path):
+    # the launcher parent counts devices from sysfs: no torch / HIP module is
+    # imported by the count itself when the topology is readable
+    root = _fake_kfd(tmp_path / "nodes", [(0, 0), (7, 256)])
+    code = ("import importlib.util, sys\n"
+            f"spec = importlib.util.spec_from_file_location('b', {os.path.join(REPO, 'bench.py')!r})\n"
+            "b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)\n"
+            f"b.KFD_NODES = {root!r}\n"
+            "n = b._device_count()\n"
+            "assert n == 1, n\n"
+            "assert 'torch' not in sys.modules, 'torch imported by the launcher count'\n")
+    env = {k: v for k, v in os.environ.items() if not k.endswith("VISIBLE_DEVICES")}
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                       env=env)
+    assert p.returncode == 0, p.stderr
+
+
+def test_rank_device_check():
+    b = _bench()
+    # one GPU per local rank
+    assert b.rank_device_check(8, 3, "nccl", {"LOCAL_WORLD_SIZE": "8"}, 8) is None
+    # a two-node job of 16 ranks, 8 per node: only the node's ranks count
+    assert b.rank_device_check(8, 7, "nccl", {"LOCAL_WORLD_SIZE": "8"}, 16) is None
+    # a launcher that gives each rank one GPU through HIP_VISIBLE_DEVICES
+    assert b.rank_device_check(1, 5, "nccl", {"LOCAL_WORLD_SIZE": "8",
+                                              "HIP_VISIBLE_DEVICES": "5"}, 8) is None
+    # too few GPUs for the node's ranks
+    msg = b.rank_device_check(1, 1, "nccl", {"LOCAL_WORLD_SIZE": "2"}, 2)
+    assert msg and "need 2 GPUs" in msg
+    assert b.rank_device_check(4, 0, "nccl", {}, 8) is not None
+    # the gloo rehearsal shares one GPU
+    assert b.rank_device_check(1, 1, "gloo", {"LOCAL_WORLD_SIZE": "2"}, 2) is None

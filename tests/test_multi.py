@@ -332,3 +332,123 @@ def test_torch_nccl_world1(gdsp, oracle):
         assert nrel(y.cpu().numpy(), oracle.fft2(m)) < 1e-12
     finally:
         dist.destroy_process_group()
+
+
+# ---- GPU, distinct devices (an 8-GPU node pins RCCL parity) -----------------
+# On a one-GPU box these skip with their reason; on a node with N >= 2 GPUs
+# they run the real cross-device paths against the oracle: the in-library
+# RCCL clique (ncclCommInitAll + one grouped ncclReduce, multi.hip) and the
+# torch.distributed "nccl" (RCCL) world of N ranks.
+
+def _ndev_or_skip(gdsp, need=2):
+    n = gdsp.device_count()
+    if n < need:
+        pytest.skip(f"needs >= {need} GPUs (this box has {n}): the cross-device RCCL path")
+    return n
+
+
+@pytest.mark.gpu
+def test_fft_batch_multi_distinct_devices_vs_oracle(gdsp, oracle):
+    """gdsp_fft_batch_multi over every visible GPU (row shards, no
+    collective; fft/radix2.go:89-151's parallelism across devices)."""
+    n_dev = _ndev_or_skip(gdsp)
+    devs = list(range(n_dev))
+    rng = np.random.default_rng(31)
+    x = rng.standard_normal((4 * n_dev + 3, 4096)) + 1j * rng.standard_normal((4 * n_dev + 3, 4096))
+    s0 = gdsp.fft.MultiStats()
+    y = gdsp.fft.FFTBatchMulti(x, devices=devs)
+    assert gdsp.fft.MultiStats()["batch_calls"] == s0["batch_calls"] + 1
+    ref = oracle.fft_rows(x)
+    assert max(nrel(a, b) for a, b in zip(y, ref)) < 1e-9
+    xs = rng.standard_normal((2 * n_dev + 1, 3000)) + 1j * rng.standard_normal((2 * n_dev + 1, 3000))
+    z = gdsp.fft.FFTBatchMulti(xs, inverse=True, devices=devs)
+    assert max(nrel(a, b) for a, b in zip(z, oracle.ifft_rows(xs))) < 1e-9
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c", [
+    dict(n=1 << 24, nfft=4096, noverlap=2048, pad=0, fs=1.0),   # configs[4]'s shape
+    dict(n=300001, nfft=1000, noverlap=250, pad=2048, fs=3.0),
+    dict(n=5000, nfft=4096, noverlap=2048, pad=0, fs=2.0),      # fewer segments than GPUs
+], ids=lambda c: f"{c['n']}-{c['nfft']}")
+def test_pwelch_multi_distinct_devices_rccl_vs_oracle(gdsp, oracle, c):
+    """gdsp_pwelch_multi over every visible GPU (up to 8, configs[4]'s split):
+    segment shards with their halo, one grouped RCCL ncclReduce of the per-bin
+    sums over a real clique of distinct devices (rccl_reduces counts it),
+    against the reference restatement (spectral/pwelch.go:107-122)."""
+    n_dev = _ndev_or_skip(gdsp)
+    devs = list(range(min(n_dev, 8)))
+    x = oracle.fill_uniform(c["n"], 0x5EED) if c["n"] == 1 << 24 else \
+        np.sin(2 * np.pi * 0.1234 * np.arange(c["n"])) + \
+        0.5 * np.random.default_rng(4).standard_normal(c["n"])
+    o = gdsp.spectral.PwelchOptions(NFFT=c["nfft"], Noverlap=c["noverlap"], Pad=c["pad"])
+    s0 = gdsp.fft.MultiStats()
+    p, f = gdsp.spectral.PwelchMulti(x, c["fs"], o, devices=devs)
+    s1 = gdsp.fft.MultiStats()
+    assert s1["pwelch_calls"] == s0["pwelch_calls"] + 1
+    assert s1["rccl_reduces"] == s0["rccl_reduces"] + 1, (s0, s1)
+    pr, fr = oracle.pwelch(x, c["fs"], c["nfft"], c["pad"], c["noverlap"])
+    assert nrel(p, pr) < 1e-9 and nrel(f, fr) < 1e-15
+    # the same call on one device: the sharded sum equals the one-device sum
+    p1, _ = gdsp.spectral.PwelchMulti(x, c["fs"], o, devices=[0])
+    assert nrel(p, p1) < 1e-13
+
+
+_WORLD = r"""
+import importlib, os, sys
+sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
+import numpy as np, torch, torch.distributed as dist
+local = int(os.environ["LOCAL_RANK"]); W = int(os.environ["WORLD_SIZE"]); r = int(os.environ["RANK"])
+torch.cuda.set_device(local)
+dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+import oracle
+g = importlib.import_module("go-dsp_amd")
+Dd = importlib.import_module("go-dsp_amd.distributed")
+def nrel(a, b):
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+# configs[4]'s Pwelch at 2^24 samples: segment shards, one RCCL all-reduce
+n = 1 << 24
+x = oracle.fill_uniform(n, 0x5EED)
+sh = Dd.plan_pwelch(n, W, r, 4096, 0, 2048)
+xl = torch.tensor(x[sh.sample_lo:sh.sample_hi], device=f"cuda:{local}")
+o = g.spectral.PwelchOptions(NFFT=4096, Noverlap=2048)
+p, f = Dd.pwelch(xl, 1.0, o, sh)
+# FFT2 row shards with two RCCL all-to-alls (uneven: 1000 rows, 768 columns)
+rows, cols = 1000, 768
+rng = np.random.default_rng(9)
+m = rng.standard_normal((rows, cols)) + 1j * rng.standard_normal((rows, cols))
+lo, hi = Dd.shard_range(rows, W, r)
+y = Dd.fft2_sharded(torch.tensor(m[lo:hi], device=f"cuda:{local}"), rows)
+torch.cuda.synchronize()
+yl = y.cpu().numpy()
+if r == 0:
+    pr, _ = oracle.pwelch(x, 1.0, 4096, 0, 2048)
+    e1 = nrel(p, pr)
+    ref = oracle.fft2(m)
+    e2 = nrel(yl, ref[lo:hi])
+    assert e1 < 1e-9 and e2 < 1e-12, (e1, e2)
+    print(f"ok world={W} pwelch={e1:.2e} fft2={e2:.2e}", flush=True)
+dist.barrier()
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.gpu
+def test_torch_nccl_world_n_vs_oracle(gdsp, tmp_path):
+    """torch.distributed over RCCL with one rank per visible GPU
+    (torch.distributed.run, 127.0.0.1): the sharded Pwelch of configs[4]'s
+    shape at 2^24 samples (one all-reduce) and a sharded FFT2 (two
+    all-to-alls), against the oracle."""
+    import subprocess
+    import sys
+    n_dev = _ndev_or_skip(gdsp)
+    world = min(n_dev, 8)
+    script = tmp_path / "world.py"
+    script.write_text(_WORLD)
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, REPO=repo)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), str(script)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0 and f"ok world={world}" in r.stdout, r.stdout + r.stderr[-4000:]

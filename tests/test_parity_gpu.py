@@ -203,6 +203,31 @@ def test_mixed_rows_two_pass(gdsp, oracle, n, batch):
     assert row_nrel(xt.cpu().numpy(), ref) < TOL
 
 
+@pytest.mark.parametrize("n,batch", [(10571, 3), (9889, 2)])
+def test_mixed_rows_short_columns(gdsp, oracle, n, batch):
+    # lengths whose only two-pass split has columns of <= 25 points: 10571 =
+    # 11 x 961 and 9889 = 11 x 899 (the balanced divisors are primes 29 / 31,
+    # which are chirp-z lengths, not mixed rows): the single-radix column pass
+    # (colradix_kernel) + runtime-compiled rows of C with the transpose in
+    # their store (mixrows_build's short-column branch)
+    import torch
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    p = D.plan(n)
+    assert p.kind == 6 and p.n1 * p.n2 == n, (p.kind, p.n1, p.n2)
+    assert p.n1 <= 25, (p.n1, p.n2)
+    rng = np.random.default_rng(n + 3 * batch)
+    x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
+    ref = oracle.fft_rows(x)
+    assert row_nrel(gdsp.fft.FFTBatch(x), ref) < TOL
+    assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL
+    xr = x.real.copy()
+    assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
+    xt = torch.from_numpy(x).cuda()
+    D.fft_batch(xt, xt)
+    torch.cuda.synchronize()
+    assert row_nrel(xt.cpu().numpy(), ref) < TOL
+
+
 @pytest.mark.parametrize("n", [2, 4, 8, 16, 32, 64, 128, 256])
 def test_short_rows_many_blocks(gdsp, oracle, n):
     # short transforms stage whole workgroup chunks through LDS: several
