@@ -14,7 +14,8 @@ independent). value = 2^28 samples / max-over-ranks wall time; at N > 1 a
 weak-scaling figure (65536 rows per rank) is added as "weak_scaling".
 
 The default run also times the other BASELINE configs and nests them under
-"configs": bluestein3000 and chirpz3000 (configs[2]), fft2_8192 (configs[3];
+"configs": bluestein3000, chirpz3000 and prime3001 (configs[2]; the prime n = 3001
+through the production dispatch, Rader), fft2_8192 (configs[3];
 rows sharded with two RCCL all-to-alls at N > 1) and pwelch (configs[4]; one
 RCCL all-reduce of the PSD accumulators). --workload X runs one alone.
 bluestein3000 is fft.FFT of N = 3000 through the production dispatch (the
@@ -49,6 +50,7 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (tools/fp64peak.hip measures 
 # kernels whose FP64 work is taken from the committed SQ counter passes
 # (profiles/r02/sq_counters.json: 64 x (2 FMA + ADD + MUL) F64 instructions)
 SQ_KERNELS = {"radix4096": ["fft_lds_kernel<12"], "bluestein3000": ["fft_mixed_fixed_kernel"],
+              "prime3001": ["rader_fixed_kernel"],
               "chirpz3000": ["chirpz6k_kernel"], "pwelch": ["pwelch_row_kernel<12"],
               "fft2_8192": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"],
               "fft2_dist": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"]}
@@ -63,7 +65,8 @@ WARM_S = 0.06  # untimed GPU work before the timed steps (steady clocks; measure
 # committed PMC (profiles/pmc_*.json) and SQ (profiles/r02/sq_counters.json)
 # summaries were measured on
 PROFILED_ALG_BYTES = {"radix4096": 32 * 4096 * 65536, "bluestein3000": 32 * 3000 * 65536,
-                      "chirpz3000": 32 * 3000 * 65536, "fft2_8192": 4 * 16 * 8192 * 8192,
+                      "chirpz3000": 32 * 3000 * 65536, "prime3001": 32 * 3001 * 65536,
+                      "fft2_8192": 4 * 16 * 8192 * 8192,
                       "fft2_dist": 4 * 16 * 8192 * 8192, "pwelch": 8 * (1 << 30),
                       "fftn_512": 3 * 2 * 16 * 512 ** 3, "wav_decode": 10 * (1 << 30),
                       "fft_2p20": 32 * (1 << 20)}
@@ -88,11 +91,12 @@ def parse():
     return ap.parse_args()
 
 
-WORKLOADS = ["radix4096", "bluestein3000", "chirpz3000", "fft2_8192", "fft2_dist", "pwelch",
+WORKLOADS = ["radix4096", "bluestein3000", "chirpz3000", "prime3001", "fft2_8192", "fft2_dist",
+             "pwelch",
              "fftn_512", "wav_decode", "fft_2p20", "fftreal1024"]
 # the BASELINE configs nested in the default line: configs[2] (production
 # dispatch and the reference's chirp-z algorithm), configs[3], configs[4]
-NESTED = ["bluestein3000", "chirpz3000", "fft2_8192", "pwelch", "fftreal1024"]
+NESTED = ["bluestein3000", "chirpz3000", "prime3001", "fft2_8192", "pwelch", "fftreal1024"]
 HEADLINE_METRIC = "Gsamples/s + % HBM roofline, batched N=4096 complex128 FFT at 1/2/4/8 GPUs"
 
 
@@ -138,8 +142,8 @@ def setup(w: str, c: Ctx, weak: bool = False) -> dict:
     reference's own benchmark is fixed-work, fft/fft_test.go:262-280);
     weak=True gives every rank the full 65536 rows instead."""
     torch, D, Dd, dev, stream, rank, world = c.torch, c.D, c.Dd, c.dev, c.stream, c.rank, c.world
-    if w in ("radix4096", "bluestein3000", "chirpz3000"):
-        n = 4096 if w == "radix4096" else 3000
+    if w in ("radix4096", "bluestein3000", "chirpz3000", "prime3001"):
+        n = {"radix4096": 4096, "prime3001": 3001}.get(w, 3000)
         chirpz = w == "chirpz3000"
         total = c.args.batch or 65536
         if weak:
@@ -156,9 +160,12 @@ def setup(w: str, c: Ctx, weak: bool = False) -> dict:
             D.fft_batch(x, y, stream=stream, chirpz=chirpz)
 
         algo = {1: "Stockham radix-16 (one kernel)", 3: "Bluestein chirp-z (fused, M=8192)",
-                5: "mixed-radix Stockham 25*15*8 (one compiled kernel)"}.get(kind, str(kind))
+                5: "mixed-radix Stockham 25*15*8 (one compiled kernel)",
+                7: f"Rader (cyclic convolution of length {n - 1} = 25*15*8, two FFTs in one "
+                   "runtime-compiled kernel; the reference: Bluestein, M=8192)"}.get(kind, str(kind))
         kernel = {1: "fft_lds_kernel<12>", 3: "bluestein_kernel<13>",
-                  5: "fft_mixed_fixed_kernel<25,15,8>"}.get(kind, str(kind))
+                  5: "fft_mixed_fixed_kernel<25,15,8>",
+                  7: "rader_fixed_kernel"}.get(kind, str(kind))
         if kind == 3 and p.m == 6144:
             # 2049 <= n <= 3072: the convolution on M = 6144 (chirpz6k.hip);
             # bluestein.go:70 pads to 8192 (GDSP_ALGO_CHIRPZ_POW2 keeps it)
@@ -342,7 +349,7 @@ def parity(w: str, wl: dict, c: Ctx):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
     import oracle
-    if w in ("radix4096", "bluestein3000", "chirpz3000"):
+    if w in ("radix4096", "bluestein3000", "chirpz3000", "prime3001"):
         x, y = wl["x"], wl["y"]
         rows = np.linspace(0, y.shape[0] - 1, c.args.check_rows).astype(int)
         xs, ys = x[rows].cpu().numpy(), y[rows].cpu().numpy()
@@ -603,6 +610,25 @@ def run(w: str, c: Ctx, weak: bool = False) -> dict:
             "avg_launch_ms": round(m8["avg_launch_s"] * 1e3, 4),
             "frac": round(w8["alg_bytes"] / m8["avg_launch_s"] / 1e9 / HBM_PEAK_GBS, 4)}
         del w8
+        c.torch.cuda.empty_cache()
+        return out
+    if w == "prime3001" and not weak and wl["kernel"] == "rader_fixed_kernel":
+        # the same prime on the chirp-z kernel it took before Rader
+        # (GDSP_ALGO_NO_RADER: the fused chirp-z on M = 6144), timed the same way
+        F = c.gdsp.fft
+        del wl
+        F.SetAlgorithm(F.ALGO_NO_RADER)
+        try:
+            wc = setup(w, c)
+            mc = measure(wc, c)
+        finally:
+            F.SetAlgorithm(F.ALGO_DEFAULT)
+        out["chirpz"] = {
+            "kernel": wc["kernel"], "algorithm": wc["cfg"]["algorithm"],
+            "ms_per_step": round(mc["elapsed"] / args.steps * 1e3, 4),
+            "avg_launch_ms": round(mc["avg_launch_s"] * 1e3, 4),
+            "frac": round(wc["alg_bytes"] / mc["avg_launch_s"] / 1e9 / HBM_PEAK_GBS, 4)}
+        del wc
         c.torch.cuda.empty_cache()
         return out
     if c.rank == 0 and w == "fft_2p20":
@@ -1052,7 +1078,8 @@ def _cpu_baseline(workload: str, seconds: float, cores: int, pool: str, np, orac
                           f"786432 line FFTs of one 512^3 FFTN, {pool}"}
     if workload == "fft2_dist":
         workload = "fft2_8192"
-    n = {"radix4096": 4096, "bluestein3000": 3000, "chirpz3000": 3000, "fft2_8192": 8192}[workload]
+    n = {"radix4096": 4096, "bluestein3000": 3000, "chirpz3000": 3000, "prime3001": 3001,
+         "fft2_8192": 8192}[workload]
     rows = 64 if n != 8192 else 16
     x = oracle.fill_uniform(2 * n * rows, SEED).view(np.complex128).reshape(rows, n)
     done = 0

@@ -100,7 +100,8 @@ bool lds_split_default() {
 
 std::atomic<unsigned> g_algo{GDSP_ALGO_DEFAULT};
 constexpr unsigned kAlgoAll = GDSP_ALGO_GENERIC_MIXED | GDSP_ALGO_NO_CHIRPZ_PARTS |
-                              GDSP_ALGO_CHIRPZ_POW2 | GDSP_ALGO_CHIRPZ_UNFUSED;
+                              GDSP_ALGO_CHIRPZ_POW2 | GDSP_ALGO_CHIRPZ_UNFUSED |
+                              GDSP_ALGO_NO_RADER;
 
 // Scratch device memory: a grow-only buffer per (device, stream, use-site
 // slot), allocated with hipMalloc. Reuse is ordered by the stream itself: a
@@ -303,7 +304,7 @@ int zero_copy_get(ZeroCopy **out) {
 }  // namespace
 
 enum PlanKind { KIND_TRIVIAL = 0, KIND_LDS = 1, KIND_GLOBAL = 2, KIND_BLUESTEIN = 3,
-                KIND_BLUESTEIN_COMPOSED = 4, KIND_MIXED = 5, KIND_MIXED4 = 6 };
+                KIND_BLUESTEIN_COMPOSED = 4, KIND_MIXED = 5, KIND_MIXED4 = 6, KIND_RADER = 7 };
 
 struct gdsp_plan {
   int device = 0;
@@ -357,6 +358,11 @@ struct gdsp_plan {
   // composed chirp-z without its fused transposes (GDSP_ALGO_CHIRPZ_UNFUSED)
   bool unfused = false;
   int64_t kpart = 0;
+  // Rader (KIND_RADER, a prime n whose n - 1 has a radix list): the kernel,
+  // m = n - 1 (the cyclic convolution's length), tw its per-pass twiddle
+  // bases, bhat = FFT_m(b)/m, gpow[q] = g^q mod n, ginv[r] = g^-r mod n
+  gdsp::JitRader *rader = nullptr;
+  int *gpow = nullptr, *ginv = nullptr;
 };
 
 namespace {
@@ -763,6 +769,129 @@ int build_shfl_tables(gdsp_plan *p) {
 
 bool fourstep2_applies(int ln);  // (exec_fourstep2 below)
 
+bool is_prime64(int64_t n) {
+  if (n < 2) return false;
+  for (int64_t d = 2; d * d <= n; ++d)
+    if (n % d == 0) return false;
+  return true;
+}
+
+int64_t pow_mod(int64_t b, int64_t e, int64_t m) {
+  int64_t r = 1 % m;
+  b %= m;
+  for (; e > 0; e >>= 1) {
+    if (e & 1) r = r * b % m;
+    b = b * b % m;
+  }
+  return r;
+}
+
+// smallest primitive root of the prime p
+int64_t primitive_root(int64_t p) {
+  std::vector<int64_t> f;
+  int64_t m = p - 1;
+  for (int64_t d = 2; d * d <= m; ++d)
+    if (m % d == 0) {
+      f.push_back(d);
+      while (m % d == 0) m /= d;
+    }
+  if (m > 1) f.push_back(m);
+  for (int64_t g = 2; g < p; ++g) {
+    bool ok = true;
+    for (int64_t q : f) ok = ok && pow_mod(g, (p - 1) / q, p) != 1;
+    if (ok) return g;
+  }
+  return 0;
+}
+
+// Radix list of Rader's convolution length N = P - 1: the compiled
+// specialisation's list where there is one, else the runtime-compiled
+// choice (jit_radices); a power of 2 as radix-16 passes with the remainder
+// last (FPass runs any radix dft_any has).
+bool rader_radices(int64_t N, std::vector<int> &rad) {
+  rad.clear();
+  if (N < 2 || N > gdsp::kMixedSpecMax) return false;
+  if (is_pow2(N)) {
+    int a = ilog2(N);
+    while (a >= 4) {
+      rad.push_back(16);
+      a -= 4;
+    }
+    if (a) rad.push_back(1 << a);
+    return true;
+  }
+  int fr[16], fnp = 0;
+  if (gdsp::mixed_fixed_radices((int)N, fr, &fnp) || gdsp::jit_radices((int)N, fr, &fnp)) {
+    rad.assign(fr, fr + fnp);
+    return true;
+  }
+  return false;
+}
+
+// Rader's algorithm (rader_fixed_kernel, mixed_fixed.hpp) for a prime n >= 17
+// whose n - 1 has a radix list: the DFT as a cyclic convolution of length
+// n - 1 (two FFTs of n - 1 points in one kernel) instead of bluestein.go:68-94's
+// chirp-z (FFTs of NextPowerOf2(2n - 1), or the M = 6144 / 3072 kernel).
+// *built = false (and p untouched) where it does not apply or the kernel
+// does not compile: the plan then takes the chirp-z below.
+int rader_try(int dev, int64_t n, gdsp_plan *p, bool *built) {
+  *built = false;
+  if ((plan_flags() & GDSP_ALGO_NO_RADER) || !gdsp::jit_enabled() || n < 17 ||
+      n > gdsp::kMixedSpecMax + 1 || !is_prime64(n))
+    return GDSP_OK;
+  const int64_t N = n - 1;
+  std::vector<int> rad;
+  if (!rader_radices(N, rad)) return GDSP_OK;
+  gdsp::JitRader *j = gdsp::jit_rader_build(dev, rad.data(), (int)rad.size());
+  if (!j) return GDSP_OK;
+  gdsp_plan *pn = nullptr;  // FFT_N for bhat
+  STCHK(get_plan_locked(dev, N, &pn));
+  gdsp::MixedDesc d{};
+  cd *tw = nullptr;
+  STCHK(make_mixed_desc(dev, N, rad, d, &tw));
+  const int64_t g = primitive_root(n);
+  if (!g) return fail(GDSP_ERR_INVALID, "no primitive root");
+  std::vector<int> gp((size_t)N), gi((size_t)N);
+  int64_t x = 1;
+  for (int64_t q = 0; q < N; ++q) {
+    gp[(size_t)q] = (int)x;
+    x = x * g % n;
+  }
+  for (int64_t r = 0; r < N; ++r) gi[(size_t)r] = gp[(size_t)((N - r) % N)];
+  // b[q] = W_n^ginv[q], the exponent reduced exactly, in long double
+  std::vector<cd> b((size_t)N);
+  for (int64_t q = 0; q < N; ++q) {
+    const long double a =
+        -2.0L * 3.141592653589793238462643383279502884L * (long double)gi[(size_t)q] / (long double)n;
+    b[(size_t)q] = {(double)cosl(a), (double)sinl(a)};
+  }
+  hipStream_t s = thread_stream(dev);
+  HIPCHK(hipMalloc((void **)&p->gpow, (size_t)N * sizeof(int)));
+  HIPCHK(hipMalloc((void **)&p->ginv, (size_t)N * sizeof(int)));
+  HIPCHK(hipMalloc((void **)&p->bhat, (size_t)N * sizeof(cd)));
+  STCHK(copy_h2d(p->gpow, gp.data(), (size_t)N * sizeof(int), s));
+  STCHK(copy_h2d(p->ginv, gi.data(), (size_t)N * sizeof(int), s));
+  cd *db = nullptr;
+  HIPCHK(hipMalloc((void **)&db, (size_t)N * sizeof(cd)));
+  STCHK(copy_h2d(db, b.data(), (size_t)N * sizeof(cd), s));
+  // FFT_N(b) on the device with the engine itself, with the inverse's 1/N
+  int st = exec_plan(pn, db, p->bhat, 1, false, gdsp::LOAD_COMPLEX, s);
+  if (st == GDSP_OK) {
+    hipError_t e = gdsp::launch_scale(p->bhat, N, 1.0 / (double)N, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) st = fail(GDSP_ERR_HIP, hipGetErrorString(e));
+  }
+  (void)hipFree(db);
+  STCHK(st);
+  p->kind = KIND_RADER;
+  p->rader = j;
+  p->tw = tw;
+  p->md = d;
+  p->m = N;
+  *built = true;
+  return GDSP_OK;
+}
+
 int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   p->device = dev;
   p->n = n;
@@ -851,6 +980,11 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
     STCHK(get_plan_locked(dev, p->n1, &p->p1));
     STCHK(get_plan_locked(dev, p->n2, &p->p2));
     return upload_twiddles(dev, n, &p->tw);
+  }
+  if (!chirpz) {
+    bool built = false;
+    STCHK(rader_try(dev, n, p, &built));
+    if (built) return GDSP_OK;
   }
   // Bluestein factors, bluestein.go:32-61: w_k = (cos, sin)(Pi/n * k*k),
   // k = 0 exactly 1 (angle not reduced, as the reference computes it).
@@ -1408,6 +1542,10 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
       return GDSP_OK;
     case KIND_MIXED4:
       return exec_mixed4(p, in, out, batch, inv, load, s);
+    case KIND_RADER:
+      HIPCHK(gdsp::jit_launch_rader(p->rader, inv, load, in, out, batch, p->tw, p->bhat, p->gpow,
+                                    p->ginv, scale, s));
+      return GDSP_OK;
     case KIND_LDS:
       HIPCHK(gdsp::launch_fft_lds(p->log2n, inv, load, lds_split_default(), in, out, batch, p->tw,
                                   scale, s));
@@ -1940,7 +2078,7 @@ int gdsp_plan_info(const gdsp_plan *plan, int64_t *n, int64_t *m, int64_t *n1, i
   if (m) *m = plan->m;
   if (n1) *n1 = plan->n1;
   if (n2) *n2 = plan->n2;
-  if (runtime_compiled) *runtime_compiled = (plan->jit || plan->mixcol) ? 1 : 0;
+  if (runtime_compiled) *runtime_compiled = (plan->jit || plan->mixcol || plan->rader) ? 1 : 0;
   return GDSP_OK;
 }
 

@@ -87,6 +87,13 @@ hipError_t jit_launch_col(const JitCol *j, bool conj_in, const cd *in, cd *out, 
 hipError_t jit_launch_fft(const JitSpec *j, bool inv, int load, const void *in, cd *out,
                           int64_t batch, const cd *tw, double scale, hipStream_t s);
 int jit_pw_tpw(const JitSpec *j);
+// rader_fixed_kernel (mixed_fixed.hpp): a prime P = prod(rad) + 1 by Rader's
+// algorithm on the inlined mixed-radix chain of its N = P - 1
+struct JitRader;
+JitRader *jit_rader_build(int dev, const int *rad, int np);  // nullptr: not built
+hipError_t jit_launch_rader(const JitRader *j, bool inv, int load, const void *in, cd *out,
+                            int64_t batch, const cd *tw, const cd *bhat, const int *gpow,
+                            const int *ginv, double scale, hipStream_t s);
 hipError_t jit_launch_pwelch(const JitSpec *j, const double *x, int64_t nfft, int64_t stride,
                              int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,
                              const double *win, const cd *tw, double *partial, hipStream_t s);

@@ -528,6 +528,247 @@ __global__ __launch_bounds__((W * FixedGeo<R0, RS...>::T1)) void colfixed_kernel
                                                                                tw, sink);
 }
 
+// ---------------------------------------------------------------------------
+// Rader's algorithm for a prime length P = N + 1 whose N = prod(R0, RS...) is
+// smooth (the reference sends every non-power-of-2 length to Bluestein,
+// fft/bluestein.go:68-94: three FFTs of NextPowerOf2(2P - 1), ~4 P points
+// each). With g a primitive root mod P, gpow[q] = g^q and ginv[r] = g^-r:
+//   X[0]       = y[0] + sum_q a[q],            a[q] = y[gpow[q]],
+//   X[ginv[r]] = y[0] + (a (*) b)[r],          b[q] = W_P^ginv[q],
+// a cyclic convolution of length N, done as FFT_N(a) * bhat (bhat = FFT_N(b)
+// / N, built on the device at plan creation) and an inverse FFT_N by the
+// conjugation identity. The same DFT with two N-point FFTs instead of three
+// 2^ceil(log2(2P - 1))-point ones. One workgroup slot per row:
+//  1. the row's P samples (coalesced, nontemporal) into LDS in natural order;
+//  2. the first pass gathers a[q] = LDS[gpow[q]] and FFT_N runs as the
+//     mixed-radix chain (fixed_chain_to);
+//  3. A[k] * bhat[k] in the last pass's registers; the thread holding k = 0
+//     keeps A[0] (X[0] = y[0] + A[0]) and adds y[0] to C[0], which adds y[0]
+//     to every output of the inverse transform; conjugated for it;
+//  4. LDS exchange into natural order, FFT_N again, conjugated back;
+//  5. c[r] scattered to LDS slot ginv[r] (X[0] from the k = 0 thread), then a
+//     coalesced nontemporal store of the row.
+// The row never leaves the chip between its load and its store: 16 B read +
+// 16 B written per sample, as any one-kernel transform. SPLIT (N > 4096):
+// every LDS round trip goes as real then imaginary halves. In place is safe:
+// a slot reads its whole row before the first barrier and stores it after
+// the last. INV: IDFT = conj(DFT(conj(x))) * scale; LOAD_REAL: float64 rows.
+template <int R0, int... RS>
+struct RaderGeo {
+  using G = FixedGeo<R0, RS...>;
+  static constexpr int N = G::N, P = N + 1, T1 = G::T1;
+  static constexpr bool SPLIT = N > 4096;
+  static constexpr int SLOTS = (P + 7) & ~7;  // staging slots (>= the FFT exchange's)
+  static constexpr int DPT = SPLIT ? SLOTS : 2 * SLOTS;  // doubles of LDS per transform
+  static constexpr int NQ = (P + T1 - 1) / T1;           // row elements per thread
+  static constexpr int tpw() {
+    int t = 256 / T1 > 1 ? 256 / T1 : 1;
+    while (t > 1 && t * DPT * 8 > 65536) --t;
+    return t;
+  }
+  static constexpr int TPW = tpw();
+  static constexpr int WG = TPW * T1;
+};
+
+template <bool INV, int LOAD, bool SWZ, int R0, int... RS>
+__global__ __launch_bounds__((RaderGeo<R0, RS...>::WG)) void rader_fixed_kernel(
+    const void *__restrict__ in, cd *__restrict__ out, int64_t batch, const cd *__restrict__ tw,
+    const cd *__restrict__ bhat, const int *__restrict__ gpow, const int *__restrict__ ginv,
+    double scale) {
+  using RG = RaderGeo<R0, RS...>;
+  constexpr int N = RG::N, P = RG::P, T1 = RG::T1, NQ = RG::NQ;
+  constexpr bool SPLIT = RG::SPLIT;
+  using First = FPass<R0, N, 1, T1>;
+  using FL = FixedLast<R0, RS...>;
+  using Last = typename FL::Pass;
+  constexpr int RL = FL::R, NSL = N / RL;
+  __shared__ double lds[RG::TPW * RG::DPT];
+  const int sub = RG::TPW == 1 ? 0 : (int)threadIdx.x / T1;
+  const int tl = (int)threadIdx.x - sub * T1;
+  const int64_t row = xcd_remap(blockIdx.x, gridDim.x) * RG::TPW + sub;
+  const bool valid = row < batch;
+  const int64_t lrow = valid ? row : batch - 1;  // a slot past the batch reads a valid row
+  double *ld = lds + sub * RG::DPT;
+  cd *lc = reinterpret_cast<cd *>(ld);
+  // 1. the row, natural order
+  cd xr[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int i = tl + q * T1;
+    if (q * T1 + T1 <= P || i < P) {
+      if constexpr (LOAD == LOAD_REAL) {
+        xr[q] = {ld_nt(reinterpret_cast<const double *>(in) + lrow * P + i), 0.0};
+      } else {
+        xr[q] = ld_nt(reinterpret_cast<const cd *>(in) + lrow * P + i);
+        if constexpr (INV) xr[q].y = -xr[q].y;
+      }
+    }
+  }
+  const cd y0 = xr[0];  // (meaningful in the thread with tl = 0: element 0)
+  // 2. gather a[q] = y[gpow[q]] into the first pass's registers
+  First p0;
+  int gi[First::J][R0];
+#pragma unroll
+  for (int jj = 0; jj < First::J; ++jj) {
+    const int j = tl + jj * T1;
+#pragma unroll
+    for (int r = 0; r < R0; ++r) gi[jj][r] = First::act(j, true) ? gpow[j + r * First::NB] : 0;
+  }
+  if constexpr (SPLIT) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h) __syncthreads();  // the real parts' gathers are done
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int i = tl + q * T1;
+        if (q * T1 + T1 <= P || i < P) ld[i] = h ? xr[q].y : xr[q].x;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int jj = 0; jj < First::J; ++jj) {
+        const int j = tl + jj * T1;
+        if (First::act(j, true)) {
+#pragma unroll
+          for (int r = 0; r < R0; ++r) {
+            if (h) p0.v[jj][r].y = ld[gi[jj][r]];
+            else p0.v[jj][r].x = ld[gi[jj][r]];
+          }
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int i = tl + q * T1;
+      if (q * T1 + T1 <= P || i < P) lc[i] = xr[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int jj = 0; jj < First::J; ++jj) {
+      const int j = tl + jj * T1;
+      if (First::act(j, true)) {
+#pragma unroll
+        for (int r = 0; r < R0; ++r) p0.v[jj][r] = lc[gi[jj][r]];
+      }
+    }
+  }
+  // FFT_N(a)
+  p0.compute(tl, true, tw);
+  Last keep;
+  if constexpr (sizeof...(RS) == 0) {
+    keep = p0;
+  } else {
+    __syncthreads();  // every gather is done before the first exchange writes
+    auto sink = [&](const Last &c) { keep = c; };
+    fixed_chain_to<SPLIT, SWZ, N, T1, R0, 0, First, decltype(sink), RS...>(p0, tl, true, ld, tw,
+                                                                          sink);
+  }
+  // 3. C = A * bhat (+ y0 at k = 0), conjugated for the inverse transform
+  cd a0 = {0.0, 0.0};
+#pragma unroll
+  for (int jj = 0; jj < Last::J; ++jj) {
+    const int j = tl + jj * T1;
+    if (Last::act(j, true)) {
+      const int k0 = j % NSL, o = (j - k0) * RL + k0;
+#pragma unroll
+      for (int r = 0; r < RL; ++r) {
+        const int k = o + r * NSL;
+        const cd A = keep.v[jj][r];
+        cd c = cmul(A, bhat[k]);
+        if (k == 0) {
+          a0 = A;
+          c = c + y0;
+        }
+        keep.v[jj][r] = conjg(c);
+      }
+    }
+  }
+  // 4. natural order for the second FFT's first pass, FFT_N, conjugated back
+  const int t2 = opaque_int(tl);
+  const cd *tw2 = opaque_ptr(tw);
+  First p1;
+  __syncthreads();  // the last exchange's reads (or the gathers) are done
+  if constexpr (SPLIT) {
+    keep.template store_lds<0, SWZ>(t2, true, ld);
+    __syncthreads();
+    p1.template load_lds<0, SWZ>(t2, true, ld);
+    __syncthreads();
+    keep.template store_lds<1, SWZ>(t2, true, ld);
+    __syncthreads();
+    p1.template load_lds<1, SWZ>(t2, true, ld);
+  } else {
+    keep.template store_lds<2, SWZ>(t2, true, ld);
+    __syncthreads();
+    p1.template load_lds<2, SWZ>(t2, true, ld);
+  }
+  p1.compute(t2, true, tw2);
+  Last fin;
+  if constexpr (sizeof...(RS) == 0) {
+    fin = p1;
+  } else {
+    __syncthreads();
+    auto sink = [&](const Last &c) { fin = c; };
+    fixed_chain_to<SPLIT, SWZ, N, T1, R0, 0, First, decltype(sink), RS...>(p1, t2, true, ld, tw2,
+                                                                          sink);
+  }
+  // 5. X[ginv[r]] = conj(fin[r]); X[0] = y0 + A[0]; then the row's store
+  int oi[Last::J][RL];
+#pragma unroll
+  for (int jj = 0; jj < Last::J; ++jj) {
+    const int j = t2 + jj * T1;
+    const int k0 = j % NSL, o = (j - k0) * RL + k0;
+#pragma unroll
+    for (int r = 0; r < RL; ++r) oi[jj][r] = Last::act(j, true) ? ginv[o + r * NSL] : 0;
+  }
+  const cd x0 = y0 + a0;
+  cd *dst = out + lrow * P;
+  cd res[NQ];
+#pragma unroll
+  for (int h = 0; h < (SPLIT ? 2 : 1); ++h) {
+    __syncthreads();  // the previous LDS reads are done
+#pragma unroll
+    for (int jj = 0; jj < Last::J; ++jj) {
+      const int j = t2 + jj * T1;
+      if (Last::act(j, true)) {
+#pragma unroll
+        for (int r = 0; r < RL; ++r) {
+          const cd c = conjg(fin.v[jj][r]);
+          if constexpr (SPLIT) ld[oi[jj][r]] = h ? c.y : c.x;
+          else lc[oi[jj][r]] = c;
+        }
+      }
+    }
+    if (t2 == 0) {
+      if constexpr (SPLIT) ld[0] = h ? x0.y : x0.x;
+      else lc[0] = x0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int i = t2 + q * T1;
+      if (q * T1 + T1 <= P || i < P) {
+        if constexpr (SPLIT) {
+          if (h) res[q].y = ld[i];
+          else res[q].x = ld[i];
+        } else {
+          res[q] = lc[i];
+        }
+      }
+    }
+  }
+  if (valid) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int i = t2 + q * T1;
+      if (q * T1 + T1 <= P || i < P) {
+        cd y = res[q];
+        if constexpr (INV) y = {y.x * scale, -y.y * scale};
+        st_nt(dst + i, y);
+      }
+    }
+  }
+}
+
 #ifndef __HIPCC_RTC__
 template <int... RS>
 static int spec_pw_tpw(Spec<RS...>, const MixedDesc &d) {

@@ -59,6 +59,11 @@ struct JitRowT {  // rowt_fixed_kernel for one row length (forward, conj + scale
   hipFunction_t fwd = nullptr, cso = nullptr;
   int n = 0, w = 0, wg = 0;
 };
+struct JitRader {  // rader_fixed_kernel for one prime P = N + 1
+  hipModule_t mod = nullptr;
+  hipFunction_t fwd = nullptr, inv = nullptr, real = nullptr;
+  int p = 0, wg = 0, tpw = 0;
+};
 
 namespace {
 
@@ -479,6 +484,54 @@ JitRowT *jit_rowt_build(int dev, const int *rad, int np) {
   j->w = w;
   j->wg = w * t1;
   return j;
+}
+
+JitRader *jit_rader_build(int dev, const int *rad, int np) {
+  if (!jit_enabled() || np < 1) return nullptr;
+  int n = 1;
+  for (int q = 0; q < np; ++q) n *= rad[q];
+  int t1 = 0, tpw = 0;
+  fixed_geo(rad, np, &t1, &tpw);
+  if (t1 > 1024) return nullptr;
+  // RaderGeo (mixed_fixed.hpp) on the host: the staging holds the P = N + 1
+  // samples, as complex slots or (N > 4096) real / imaginary halves
+  const bool split = n > 4096;
+  const int slots = (n + 1 + 7) & ~7, dpt = split ? slots : 2 * slots;
+  tpw = 256 / t1 > 1 ? 256 / t1 : 1;
+  while (tpw > 1 && tpw * dpt * 8 > 65536) --tpw;
+  const std::string list = radix_list(rad, np), sw = rad[0] % 2 == 0 ? "true" : "false";
+  const std::vector<std::string> names = {
+      "&gdsp::rader_fixed_kernel<false, 0, " + sw + list + ">",
+      "&gdsp::rader_fixed_kernel<true, 0, " + sw + list + ">",
+      "&gdsp::rader_fixed_kernel<false, 1, " + sw + list + ">"};
+  hipModule_t mod = nullptr;
+  std::vector<hipFunction_t> fs;
+  if (!compile_module(dev, names, "Rader kernel for P = " + std::to_string(n + 1) + " (N = " +
+                                      list.substr(2) + ")",
+                      &mod, fs))
+    return nullptr;
+  JitRader *j = new JitRader;
+  j->mod = mod;
+  j->fwd = fs[0];
+  j->inv = fs[1];
+  j->real = fs[2];
+  j->p = n + 1;
+  j->tpw = tpw;
+  j->wg = t1 * tpw;
+  return j;
+}
+
+hipError_t jit_launch_rader(const JitRader *j, bool inv, int load, const void *in, cd *out,
+                            int64_t batch, const cd *tw, const cd *bhat, const int *gpow,
+                            const int *ginv, double scale, hipStream_t s) {
+  if (load == LOAD_REAL && inv) return hipErrorInvalidValue;
+  const int64_t nblk = (batch + j->tpw - 1) / j->tpw;
+  if (batch < 1 || nblk > 0x7fffffff) return hipErrorInvalidValue;
+  hipFunction_t f = inv ? j->inv : (load == LOAD_REAL ? j->real : j->fwd);
+  void *args[] = {(void *)&in,   (void *)&out,  (void *)&batch, (void *)&tw,
+                  (void *)&bhat, (void *)&gpow, (void *)&ginv,  (void *)&scale};
+  return hipModuleLaunchKernel(f, (unsigned)nblk, 1, 1, (unsigned)j->wg, 1, 1, 0, s, args,
+                               nullptr);
 }
 
 hipError_t jit_launch_rowt(const JitRowT *j, bool conj_scale_out, const cd *in, cd *out,

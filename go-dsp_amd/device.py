@@ -29,7 +29,9 @@ def _ptr(t) -> ctypes.c_void_p:
 class Plan:
     """Cached device plan for transform length n on the current device
     (gdsp_plan_create). kind: 0 trivial, 1 LDS Stockham, 2 multi-pass
-    Stockham, 3 fused Bluestein, 4 composed Bluestein, 5 mixed radix.
+    Stockham, 3 fused Bluestein, 4 composed Bluestein, 5 mixed radix,
+    6 mixed four-step, 7 Rader (a prime n <= 8193 whose n - 1 has a radix
+    list; m = n - 1, the cyclic convolution's length).
     chirpz=True forces the reference's Bluestein algorithm
     (gdsp_plan_create_chirpz) for a non-trivial length."""
 

@@ -82,7 +82,10 @@ enum {
    * for 2049 <= n <= 3072 (M = 6144 by default) */
   GDSP_ALGO_CHIRPZ_POW2 = 4,
   /* the composed chirp-z without its fused transposes */
-  GDSP_ALGO_CHIRPZ_UNFUSED = 8
+  GDSP_ALGO_CHIRPZ_UNFUSED = 8,
+  /* primes n <= 8193 whose n - 1 has a radix list on the chirp-z kernels
+   * instead of Rader's algorithm (plan kind 7) */
+  GDSP_ALGO_NO_RADER = 16
 };
 /* Unknown bits → GDSP_ERR_INVALID (the selection is left unchanged). */
 int gdsp_set_algorithm(unsigned flags);
@@ -254,12 +257,16 @@ int gdsp_plan_create_chirpz(int64_t n, gdsp_plan **plan);
  * 2 multi-pass global Stockham (large power of 2), 3 fused Bluestein,
  * 4 composed Bluestein (M > 16384), 5 one-kernel mixed radix (non-power-of-2
  * n <= 4096 whose prime factors are all <= 13), 6 mixed four-step (such n
- * above 8192 = n1*n2 with one-kernel factors: transposes + row kernels). */
+ * above 8192 = n1*n2 with one-kernel factors: transposes + row kernels),
+ * 7 Rader (a prime 17 <= n <= 8193 whose n - 1 has a radix list: the DFT as
+ * a cyclic convolution of length n - 1, two FFTs of n - 1 points in one
+ * runtime-compiled kernel; GDSP_ALGO_NO_RADER keeps such primes on kind 3). */
 int gdsp_plan_kind(const gdsp_plan *plan);
 /* Geometry of a plan (any pointer may be NULL): its length n; the chirp-z
  * convolution length m (kinds 3 and 4; the reference's NextPowerOf2(2n-1),
  * bluestein.go:70, or a smooth m >= 2n-1 that the composed chirp-z may
- * choose); the four-step split n = n1*n2 (kinds 2 and 6); and whether a
+ * choose; kind 7: Rader's cyclic convolution length n - 1); the four-step
+ * split n = n1*n2 (kinds 2 and 6); and whether a
  * runtime-compiled specialisation backs it (1) or not (0). 0 where n/a. */
 int gdsp_plan_info(const gdsp_plan *plan, int64_t *n, int64_t *m, int64_t *n1, int64_t *n2,
                    int *runtime_compiled);

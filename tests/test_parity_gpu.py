@@ -432,7 +432,9 @@ def test_plan_kinds(gdsp):
     # four-step rows on the output-split chirp-z (power-of-2 / single-radix columns)
     assert (D.plan(64 * 8209).kind, D.plan(64 * 8209).n2) == (6, 8209)
     assert (D.plan(2 * 10007).kind, D.plan(2 * 10007).n2) == (6, 10007)
-    assert D.plan(8191 * 64).kind == 6  # power-of-2 columns, fused chirp-z rows of 8191
+    assert D.plan(8191 * 64).kind == 6  # power-of-2 columns, Rader rows of 8191
+    assert (D.plan(3001).kind, D.plan(3001).m) == (7, 3000)  # prime: Rader on 25 * 15 * 8
+    assert D.plan(3067).kind == 3  # prime, 3066 = 2 * 3 * 7 * 73: no radix list, chirp-z
     assert D.plan(3000, chirpz=True).kind == 3
     assert D.plan(10000, chirpz=True).kind == 4
     assert D.plan(4096, chirpz=True).kind == 3  # forced chirp-z on a power of 2
@@ -809,7 +811,7 @@ def test_random_large_smooth_lengths(gdsp, oracle):
 
 @pytest.mark.parametrize("n,kind", [(810, 5), (1001, 5), (4095, 5), (4320, 5), (5400, 5),
                                     (6144, 5), (7000, 5), (7680, 5), (8190, 5), (6561, 5),
-                                    (7290, 5), (4802, 5), (7938, 5), (8191, 3),
+                                    (7290, 5), (4802, 5), (7938, 5), (8191, 7),
                                     # radices 17, 19, 23 (runtime-compiled lists only)
                                     (323, 5), (529, 5), (4352, 5), (7600, 5), (6900, 5),
                                     (7429, 5), (899, 5), (7936, 5), (6293, 5)])
@@ -818,7 +820,8 @@ def test_jit_specialisations(gdsp, oracle, n, kind):
     # plan creation (mixed_jit.hip, hipRTC); above 4096 they would otherwise
     # be Bluestein. 8190 = 13 * 10 * 9 * 7, 6561 = 9^4 and 7290 = 10 * 9^3 need
     # 630-910 threads per transform (radix 9/13 passes); 4802 = 2 * 7^4 and
-    # 7938 = 2 * 3^4 * 7^2 have no list shorter than five passes; 8191 is prime.
+    # 7938 = 2 * 3^4 * 7^2 have no list shorter than five passes; 8191 is prime
+    # (Rader on 8190's list, kind 7).
     D = __import__("importlib").import_module("go-dsp_amd.device")
     assert D.plan(n).kind == kind, n
     rng = np.random.default_rng(4000 + n)
@@ -1119,3 +1122,82 @@ def test_chirpz_output_parts_in_place_large_batch(gdsp, oracle):
         rows = [0, batch // 2, batch - 1]
         xs = x[rows].cpu().numpy()
         assert row_nrel(y[rows].cpu().numpy(), oracle.fft_rows(xs)) < TOL
+
+
+# ---- Rader's algorithm (rader_fixed_kernel, plan kind 7) ---------------------
+# primes whose n - 1 has a radix list: small (one pass: 17 -> 16; TPW > 1 with
+# ragged last blocks), power-of-2 n - 1 (257), compiled-specialisation lists
+# (3001 -> 25*15*8, 1201 -> 1200), runtime-compiled ones (2053 -> 2052 = 4 *
+# 27 * 19, 2729 -> 2728 = 8 * 11 * 31), and n - 1 above 4096 (re/im LDS
+# halves: 6007, 7681, 8009, 8191)
+RADER = [17, 19, 23, 29, 31, 37, 41, 61, 97, 101, 257, 641, 1009, 1201, 1531, 2053, 2311, 2729,
+         3001, 6007, 7681, 8009, 8191]
+
+
+@pytest.mark.parametrize("n", RADER)
+def test_rader_vs_oracle(gdsp, oracle, n):
+    """Rader's algorithm against the reference restatement (its Bluestein,
+    fft/bluestein.go:68-94) and numpy's float64 DFT: forward, inverse, real
+    input, batches 1 and 7, in place on the device, and the same rows through
+    the chirp-z plan (GDSP_ALGO_NO_RADER)."""
+    import torch
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    F = __import__("importlib").import_module("go-dsp_amd.fft")
+    p = D.plan(n)
+    assert (p.kind, p.m, p.runtime_compiled) == (7, n - 1, True), (n, p.kind, p.m)
+    rng = np.random.default_rng(7000 + n)
+    for batch in (1, 7):
+        x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
+        ref = oracle.fft_rows(x)
+        y = gdsp.fft.FFTBatch(x)
+        assert row_nrel(y, ref) < TOL
+        assert row_nrel(y, np.fft.fft(x, axis=1)) < 1e-13  # Rader itself is exact to roundoff
+        assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL
+        xr = rng.uniform(-1, 1, (batch, n))
+        assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
+        xt = torch.from_numpy(x).cuda()
+        D.fft_batch(xt, xt)
+        torch.cuda.synchronize()
+        assert row_nrel(xt.cpu().numpy(), ref) < TOL
+    x = rng.uniform(-1, 1, (3, n)) + 1j * rng.uniform(-1, 1, (3, n))
+    assert nrel(gdsp.fft.FFT(x[0]), oracle.fft(x[0])) < TOL
+    F.SetAlgorithm(F.ALGO_NO_RADER)
+    try:
+        assert D.plan(n).kind == 3
+        yc = gdsp.fft.FFTBatch(x)
+    finally:
+        F.SetAlgorithm(0)
+    assert row_nrel(yc, oracle.fft_rows(x)) < TOL
+
+
+@pytest.mark.parametrize("n", [1031, 2039, 3067, 4099])
+def test_primes_without_radix_list_stay_chirpz(gdsp, oracle, n):
+    # n - 1 with a prime factor above 31 (1030 = 2 * 5 * 103, 2038 = 2 * 1019, ...)
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    assert D.plan(n).kind == 3
+    rng = np.random.default_rng(n)
+    x = rng.uniform(-1, 1, (2, n)) + 1j * rng.uniform(-1, 1, (2, n))
+    assert row_nrel(gdsp.fft.FFTBatch(x), oracle.fft_rows(x)) < TOL
+
+
+def test_rader_large_batch_properties(gdsp):
+    """A full-occupancy grid of the prime 3001 (65 536 rows, the bench's
+    prime3001 shape): forward/inverse round trip and linearity on every row,
+    eight rows against numpy's float64 DFT."""
+    import torch
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    n, batch = 3001, 65536
+    assert D.plan(n).kind == 7
+    g = torch.Generator(device="cuda").manual_seed(9)
+    x = torch.complex(torch.rand(batch, n, dtype=torch.float64, device="cuda", generator=g) - 0.5,
+                      torch.rand(batch, n, dtype=torch.float64, device="cuda", generator=g) - 0.5)
+    y = D.fft_batch(x)
+    z = D.fft_batch(y, inverse=True)
+    err = ((z - x).abs().amax(dim=1) / x.abs().amax(dim=1)).max().item()
+    assert err < 1e-12, err
+    y2 = D.fft_batch(2.0 * x[:64] - 1j * x[64:128])
+    lin = ((y2 - (2.0 * y[:64] - 1j * y[64:128])).abs().max() / y[:128].abs().max()).item()
+    assert lin < 1e-13, lin
+    rows = [0, 1, 777, 4096, 30000, 65534, 65535, 12345]
+    xs = x[rows].cpu().numpy()
+    assert row_nrel(y[rows].cpu().numpy(), np.fft.fft(xs, axis=1)) < 1e-13
