@@ -635,9 +635,25 @@ __device__ __forceinline__ int xoff(int i) {
     return lds_off<ILV, E, XOR, LAYOUT == 1>(i);
 }
 
-template <int N, int E, int T, int R, int NS, bool SPLIT, int ILV = 0, int LAYOUT = 0>
+// Exchange synchronisation: the workgroup barrier, or (WS: every transform of
+// the workgroup lies inside one wave, in an LDS region of its own) only an
+// ordering fence for the compiler — a wave's LDS instructions execute in
+// order, so its reads see its own writes without a barrier.
+template <bool WS>
+__device__ __forceinline__ void xsync() {
+  if constexpr (WS) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  } else {
+    __syncthreads();
+  }
+}
+
+template <int N, int E, int T, int R, int NS, bool SPLIT, int ILV = 0, int LAYOUT = 0,
+          bool WS = false>
 __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, double *lim,
                                               bool first) {
+  static_assert(!WS || T <= 64, "wave-synchronised exchanges need a transform inside one wave");
   constexpr int B = E / R;
   // LAYOUT 2 with one butterfly per thread and T = 256 (N = 4096, E = 16),
   // written out so the compiler sees the per-thread base: the first exchange
@@ -699,17 +715,17 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
     if constexpr (L2 || LIN) return rbase + k * rstep;
     else return xoff<ILV, E, (T >= 32), (T >= 32 ? LAYOUT : 0), NS>(t + k * T);
   };
-  if (!first) __syncthreads();
+  if (!first) xsync<WS>();
   if constexpr (SPLIT) {
 #pragma unroll
     for (int k = 0; k < E; ++k) lre[dst[k]] = v[k].x;
-    __syncthreads();
+    xsync<WS>();
 #pragma unroll
     for (int k = 0; k < E; ++k) v[k].x = lre[src(k)];
-    __syncthreads();
+    xsync<WS>();
 #pragma unroll
     for (int k = 0; k < E; ++k) lre[dst[k]] = v[k].y;
-    __syncthreads();
+    xsync<WS>();
 #pragma unroll
     for (int k = 0; k < E; ++k) v[k].y = lre[src(k)];
   } else {
@@ -718,7 +734,7 @@ __device__ __forceinline__ void pass_exchange(cd (&v)[E], int t, double *lre, do
       lre[dst[k]] = v[k].x;
       lim[dst[k]] = v[k].y;
     }
-    __syncthreads();
+    xsync<WS>();
 #pragma unroll
     for (int k = 0; k < E; ++k) {
       const int o = src(k);
@@ -767,9 +783,10 @@ using RegArr = cd[Geo<LOG2N, LOG2E>::E];
 // arithmetic and exchange (wpre carries them down), so their L1/L2 or LDS
 // latency hides behind that work instead of opening the pass; only for
 // passes with at most PREW bases per thread (0: off)
+// WS: wave-synchronised exchanges (xsync), for transforms inside one wave
 template <int LOG2N, bool SPLIT, int OPAQUE = 0, int LOG2E = 4, int ILV = 0, int P = 0,
           class TWP = const cd *, int LINEAR = 0, int HALF_IN = 0, class EPI = NoEpi,
-          int PREW = 0, int CHEBR = 0>
+          int PREW = 0, int CHEBR = 0, bool WS = false>
 __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw, double *lre,
                                          double *lim, bool first_exchange = true,
                                          const EPI &epi = EPI(), const cd *wpre = nullptr) {
@@ -785,8 +802,8 @@ __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw,
       // exchange after the previous pass
       constexpr int RP = G::radix(P - 1);
       constexpr int NSP = G::ns(P - 1);
-      pass_exchange<G::N, G::E, G::T, RP, NSP, SPLIT, ILV, LINEAR>(v, t, lre, lim,
-                                                                    first_exchange && P == 1);
+      pass_exchange<G::N, G::E, G::T, RP, NSP, SPLIT, ILV, LINEAR, WS>(v, t, lre, lim,
+                                                                        first_exchange && P == 1);
     }
     // PREW: the next pass's bases, read now
     constexpr int PN = P + 1 < G::NPASS ? P + 1 : P;
@@ -805,7 +822,7 @@ __device__ __forceinline__ void fft_regs(RegArr<LOG2N, LOG2E> &v, int t, TWP tw,
     else
       pass_compute<G::N, G::E, G::T, R, NS, P == 0 ? HALF_IN : 0, NoEpi, USE_PRE, P, TWP, CH>(
           v, t, tw, NoEpi(), wpre);
-    fft_regs<LOG2N, SPLIT, 0, LOG2E, ILV, P + 1, TWP, LINEAR, false, EPI, PREW, CHEBR>(
+    fft_regs<LOG2N, SPLIT, 0, LOG2E, ILV, P + 1, TWP, LINEAR, false, EPI, PREW, CHEBR, WS>(
         v, t, tw, lre, lim, first_exchange, epi, PRE_NEXT ? wn : nullptr);
   }
 }

@@ -1118,7 +1118,7 @@ static hipError_t launch_blu_t(const cd *in, cd *out, int64_t n, int64_t batch, 
   // M = 8192 / 16384: 32 points per thread (three passes, two exchanges, one
   // twiddle stage fewer; 254 VGPRs, 2 waves per SIMD) beat 16 (four passes,
   // 124 VGPRs, 4 waves per SIMD): chirp-z 3000 3.44 against 3.56 ms, primes
-  // 4099..8191 (M = 16384) 2-5 % (GDSP_BLU_E16=1 to compare); round 3, with
+  // 4099..8191 (M = 16384) 2-5 %; round 3, with
   // the 16-point kernel held to 128 VGPRs (amdgpu_waves_per_eu: at 130 it ran
   // one 512-thread block per CU, 4.37 ms) and n-aware pruning (KN = 6):
   // 3.27-3.34 against 2.80 ms (scripts/gpu_r03_e16.sh). The 32 points
@@ -1126,26 +1126,21 @@ static hipError_t launch_blu_t(const cd *in, cd *out, int64_t n, int64_t batch, 
   // exchange through half-size buffers (34 KiB of LDS) and 168 VGPRs the
   // kernel spills 206 registers, 6.20 against 2.62 ms (scripts/gpu_r03_occ.sh)
   if constexpr (LOG2M == 13 || LOG2M == 14) {
-    static const bool e32 = dev_switch("GDSP_BLU_E16") == nullptr;
-    if (e32) {
-      using G5 = Geo<LOG2M, 5>;
-      const int64_t nb5 = (batch + G5::TPW - 1) / G5::TPW;
-      if constexpr (LOG2M == 13) {
-        // n <= 3072 = 12 T at M = 8192 (the BASELINE n = 3000): 12 of the 32
-        // registers carry input and wanted output
-        static const bool kn_off = dev_switch("GDSP_BLU_NOKN") != nullptr;
-        if (!kn_off && n <= 12 * G5::T) {
-          hipLaunchKernelGGL((bluestein_kernel<LOG2M, INV, true, 5, false, 12>),
-                             dim3((unsigned)nb5), dim3(G5::WG), 0, s, in, out, n, batch, twm,
-                             chirp, bhat, scale, (int64_t)0, 1);
-          return hipGetLastError();
-        }
+    using G5 = Geo<LOG2M, 5>;
+    const int64_t nb5 = (batch + G5::TPW - 1) / G5::TPW;
+    if constexpr (LOG2M == 13) {
+      // n <= 3072 = 12 T at M = 8192 (the BASELINE n = 3000): 12 of the 32
+      // registers carry input and wanted output (2.87 -> 2.77 ms)
+      if (n <= 12 * G5::T) {
+        hipLaunchKernelGGL((bluestein_kernel<LOG2M, INV, true, 5, false, 12>), dim3((unsigned)nb5),
+                           dim3(G5::WG), 0, s, in, out, n, batch, twm, chirp, bhat, scale,
+                           (int64_t)0, 1);
+        return hipGetLastError();
       }
-      hipLaunchKernelGGL((bluestein_kernel<LOG2M, INV, true, 5>), dim3((unsigned)nb5),
-                         dim3(G5::WG), 0, s, in, out, n, batch, twm, chirp, bhat, scale,
-                         (int64_t)0, 1);
-      return hipGetLastError();
     }
+    hipLaunchKernelGGL((bluestein_kernel<LOG2M, INV, true, 5>), dim3((unsigned)nb5), dim3(G5::WG),
+                       0, s, in, out, n, batch, twm, chirp, bhat, scale, (int64_t)0, 1);
+    return hipGetLastError();
   }
   using G = Geo<LOG2M>;
   const int64_t nblk = (batch + G::TPW - 1) / G::TPW;
@@ -1282,19 +1277,6 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
     // F = 4096 (the BASELINE configuration): twiddle bases in LDS and the
     // next pair prefetched (3.16 -> 3.11 ms; 244 VGPRs, still 2 waves/SIMD)
     case 12: {
-#ifdef GDSP_DEV_BUILD
-      // measured alternatives: the wavefront-shuffle variant (pwelch_shfl.hip,
-      // GDSP_PW_SHFL=1) and round 2's pwelch_half_kernel (GDSP_PW_HALF=1)
-      if (const char *e = dev_switch("GDSP_PW_SHFL"); e && e[0] == '1')
-        return launch_pwelch4096_shfl(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
-      // round-4 occupancy variants (pwelch_rowx.hip; the Hann ones ignore win)
-      if (const char *e = dev_switch("GDSP_PW_ROWX"); e && e[0] >= '1' && e[0] <= '9')
-        return launch_pwelch_rowx4096(e[0] - '0', x, seg_begin, seg_end, ppw, nworkers, win, tw,
-                                      partial, s);
-      if (const char *e = dev_switch("GDSP_PW_HALF"); e && e[0] == '1')
-        return launch_pwh_t<12, 2, 1, 4, true, true>(x, seg_begin, seg_end, ppw, nworkers, win, tw,
-                                                     partial, s);
-#endif
       // the row kernel: 2.81-2.84 against 3.13-3.14 ms for pwelch_half_kernel
       return launch_pwelch_row4096(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
     }
@@ -1304,12 +1286,8 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
     // re-read from L1/L2 instead of living in LDS
     case 14: {
       // 32 points per thread (512 threads): 2.25-2.27 against 2.37-2.40 ms at
-      // 2^28 samples for 16 (1024 threads); both spill (GDSP_PWH14_E16=1)
-      static const bool e32 = dev_switch("GDSP_PWH14_E16") == nullptr;
-      if (e32)
-        return launch_pwh_t<14, 1, 1, 5>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial,
-                                         s);
-      return launch_pwh_t<14, 1>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
+      // 2^28 samples for 16 (1024 threads); both spill
+      return launch_pwh_t<14, 1, 1, 5>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
     }
     default: return hipErrorInvalidValue;
   }
@@ -1447,19 +1425,15 @@ hipError_t launch_transpose(const cd *in, cd *out, int64_t rows, int64_t cols, h
   if (tw && (rows - 1) * (cols - 1) >= twn) return hipErrorInvalidValue;  // r*c < twn
   // tile shape (rows x columns): 32 x 64 for large batches, 32 x 32 below
   // 2^22 elements, where twice the tiles spread better over the CUs (one
-  // 2^20 transform: 8.3 against 10.3 us); GDSP_TRANSPOSE=32 (32 x 32) and 64
-  // (64 x 64) to compare
-  static const int forced = dev_switch("GDSP_TRANSPOSE") ? atoi(dev_switch("GDSP_TRANSPOSE")) : 0;
-  const int shape = forced ? forced : (rows * cols * batch < ((int64_t)1 << 22) ? 32 : 0);
-  const int tr = shape == 64 ? 64 : 32, tc = shape == 32 ? 32 : 64;
+  // 2^20 transform: 8.3 against 10.3 us); 64 x 64 measured 1.156 against
+  // 0.873 ms at 10^6
+  const bool small = rows * cols * batch < ((int64_t)1 << 22);
+  const int tr = 32, tc = small ? 32 : 64;
   const int64_t tiles = ((rows + tr - 1) / tr) * ((cols + tc - 1) / tc) * batch;
   const int64_t cap = 256 * 32;  // 32 tile-loop workgroups per CU
   const unsigned nb = (unsigned)(tiles < cap ? tiles : cap);
-  if (shape == 32)
+  if (small)
     hipLaunchKernelGGL((transpose_kernel<32, 32>), dim3(nb), dim3(256), 0, s, in, out, rows, cols,
-                       batch, (int)conj_scale, scale, tw, twn, (int)tw_conj);
-  else if (shape == 64)
-    hipLaunchKernelGGL((transpose_kernel<64, 64>), dim3(nb), dim3(256), 0, s, in, out, rows, cols,
                        batch, (int)conj_scale, scale, tw, twn, (int)tw_conj);
   else
     hipLaunchKernelGGL((transpose_kernel<32, 64>), dim3(nb), dim3(256), 0, s, in, out, rows, cols,

@@ -10,19 +10,8 @@ namespace gdsp {
 
 hipError_t launch_fft_lds12(bool inv, int load, bool split, const void *in, cd *out, int64_t batch,
                             const cd *tw, double scale, hipStream_t s) {
-#ifdef GDSP_DEV_BUILD
-  // the row by LDS-DMA (lds_kernel.hpp DMA), forward complex, split exchange
-  if (const char *e = dev_switch("GDSP_LDS12_DMA");
-      e && (e[0] == '1' || e[0] == '2') && load == LOAD_COMPLEX && !inv && split) {
-    if (e[0] == '1')
-      hipLaunchKernelGGL((fft_lds_kernel<12, false, LOAD_COMPLEX, true, 4, 1>), dim3((unsigned)batch),
-                         dim3(256), 0, s, in, out, batch, tw, scale);
-    else
-      hipLaunchKernelGGL((fft_lds_kernel<12, false, LOAD_COMPLEX, true, 4, 2>), dim3((unsigned)batch),
-                         dim3(256), 0, s, in, out, batch, tw, scale);
-    return hipGetLastError();
-  }
-#endif
+  // (round 4: the row by LDS-DMA instead of register loads measured 1.382 /
+  // 1.471 against 1.379 ms, profiles/r04/lds12_dma_ab.txt: register loads stay)
   if (load == LOAD_COMPLEX)
     return inv ? launch_lds_s<12, true, LOAD_COMPLEX>(in, out, batch, tw, scale, split, s)
                : launch_lds_s<12, false, LOAD_COMPLEX>(in, out, batch, tw, scale, split, s);

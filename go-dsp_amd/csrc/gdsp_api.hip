@@ -89,14 +89,8 @@ hipStream_t thread_stream(int dev) {
 }
 
 // The one-kernel transform exchanges real and imaginary halves in turn
-// (half the LDS; GDSP_LDS_SPLIT=0 in the development build for two buffers).
-bool lds_split_default() {
-  static int v = [] {
-    const char *e = gdsp::dev_switch("GDSP_LDS_SPLIT");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return v != 0;
-}
+// (half the LDS, so more workgroups per CU than with two buffers).
+bool lds_split_default() { return true; }
 
 std::atomic<unsigned> g_algo{GDSP_ALGO_DEFAULT};
 constexpr unsigned kAlgoAll = GDSP_ALGO_GENERIC_MIXED | GDSP_ALGO_NO_CHIRPZ_PARTS |
@@ -612,7 +606,6 @@ bool mixcol_build(int dev, int64_t n, gdsp_plan *p) {
 // Rows of 256 first (256-B output segments), then shorter ones (longer
 // segments, longer columns), then 512 and 1024.
 bool pow2rows_build(int dev, int64_t n, gdsp_plan *p) {
-  if (gdsp::dev_switch("GDSP_MX3")) return false;  // development build: three passes
   for (int k : {8, 7, 6, 5, 4, 9, 10}) {
     const int64_t C = (int64_t)1 << k;
     if (n % C) continue;
@@ -643,14 +636,10 @@ bool pow2rows_build(int dev, int64_t n, gdsp_plan *p) {
 // 1.93-2.03 ms at C = 225 / 210 and 2.42 at 630 (2.34 in three passes), and
 // 30000 1.78 at C = 150 and 2.50 at 1000.
 bool mixrows_build(int dev, int64_t n, gdsp_plan *p) {
-  if (gdsp::dev_switch("GDSP_MX3") || !gdsp::jit_enabled()) return false;
-  static const int64_t force_c = [] {  // development build: GDSP_MXROW_C, the row length
-    const char *e = gdsp::dev_switch("GDSP_MXROW_C");
-    return e ? (int64_t)atoll(e) : (int64_t)0;
-  }();
+  if (!gdsp::jit_enabled()) return false;
   std::vector<int64_t> cands;
   for (int64_t C = 16; C <= 1024; ++C)
-    if (n % C == 0 && !is_pow2(C) && (!force_c || C == force_c)) cands.push_back(C);
+    if (n % C == 0 && !is_pow2(C)) cands.push_back(C);
   const long double r = sqrtl((long double)n);
   // the rows-of-1000 preference holds only where its columns are >= 64
   // points; every other candidate (short columns included: the single-radix
@@ -906,27 +895,6 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   }
   std::vector<int> rad;
   int fr[16], fnp = 0;
-#ifdef GDSP_DEV_BUILD
-  // experiment: GDSP_JIT_RADICES="10x15x20" compiles that radix list (hipRTC)
-  // for the n it multiplies to, compiled specialisation or not
-  if (const char *e = gdsp::dev_switch("GDSP_JIT_RADICES"); e && !chirpz && gdsp::jit_enabled()) {
-    int jr[5], jnp = 0;
-    int64_t prod = 1;
-    for (const char *q = e; *q && jnp < 5;) {
-      char *end = nullptr;
-      const long v = strtol(q, &end, 10);
-      if (end == q) break;
-      jr[jnp++] = (int)v;
-      prod *= v;
-      q = *end ? end + 1 : end;  // any one separator character
-    }
-    if (jnp >= 2 && prod == n)
-      if (gdsp::JitSpec *j = gdsp::jit_spec_build(dev, jr, jnp, (int)n)) {
-        p->jit = j;
-        return build_mixed(dev, n, std::vector<int>(jr, jr + jnp), p);
-      }
-  }
-#endif
   if (!chirpz && n <= gdsp::kMixedSpecMax && !gdsp::mixed_fixed_radices((int)n, fr, &fnp) &&
       gdsp::jit_enabled()) {
     // smooth length without a compiled specialisation: compile one (hipRTC);
@@ -1197,14 +1165,8 @@ void fourstep_split(int ln, int *lr, int *lc);
 // segments of X). Per 2^27 samples (profiles/r04/fourstep2_ab.txt): 2^15
 // 2.10 -> 1.46 ms, 2^16 2.17 -> 1.55, 2^17 2.16 -> 1.57, 2^18 2.11 -> 1.60,
 // 2^19 2.16 -> 1.88, 2^20 2.21 -> 1.90; BenchmarkFFT's one 2^20 transform
-// 0.039 -> 0.031 ms. (GDSP_FS3=1 / GDSP_FS2_MAX in the development build.)
-bool fourstep2_applies(int ln) {
-  static const int fs2_max = [] {  // development build: GDSP_FS2_MAX, largest log2 N
-    const char *e = gdsp::dev_switch("GDSP_FS2_MAX");
-    return e ? atoi(e) : 20;
-  }();
-  return ln >= 15 && ln <= fs2_max && ln <= 20 && !gdsp::dev_switch("GDSP_FS3");
-}
+// 0.039 -> 0.031 ms.
+bool fourstep2_applies(int ln) { return ln >= 15 && ln <= 20; }
 int fourstep2_lc(int ln) { return ln >= 19 ? 10 : (ln >= 18 ? 9 : 8); }
 
 int exec_fourstep2(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bool inv, int load,
@@ -1250,13 +1212,6 @@ int exec_fourstep(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bo
   if (lc == 13 && lr + 1 <= gdsp::kColMaxLog2 && (batch << lr) <= 256) {
     lc = 12;
     lr += 1;
-  }
-  if (const char *e = gdsp::dev_switch("GDSP_FS_LC")) {  // experiment: force the row length
-    const int f = atoi(e);
-    if (f >= 4 && f <= 13 && ln - f >= gdsp::kColMinLog2 && ln - f <= gdsp::kColMaxLog2) {
-      lc = f;
-      lr = ln - f;
-    }
   }
   if (depth >= 4) return fail(GDSP_ERR_UNSUPPORTED, "transform too long");
   gdsp_plan *pr = nullptr, *pcol = nullptr;
@@ -2122,15 +2077,31 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
   gdsp_plan *p = nullptr;
   STCHK(get_plan(flen, &p));
   const int64_t nseg = seg_end - seg_begin;
+#ifndef GDSP_PWW_OFF
+  if (p->kind == KIND_LDS && gdsp::pwelch_wave_applies(p->log2n)) {
+    // 64 <= F <= 1024: wave-resident transforms, no workgroup barriers
+    // (pwelch_wave.hip), every wave a persistent worker over pair groups
+    int64_t gpw = 0, nblk = 0, nrows = 0;
+    gdsp::pwelch_wave_geometry(p->log2n, nseg, &gpw, &nblk, &nrows);
+    DevBuf part, red;
+    STCHK(part.alloc((size_t)nrows * (size_t)flen * sizeof(double), s, SLOT_PW_PART));
+    STCHK(red.alloc((size_t)gdsp::reduce_scratch_doubles(nrows, flen) * sizeof(double), s,
+                    SLOT_PW_RED));
+    const bool half = 2 * noverlap == nfft && flen == nfft;
+    HIPCHK(gdsp::launch_pwelch_wave(p->log2n, half, d_x, nfft, stride, seg_begin, seg_end, gpw,
+                                    nblk, d_win_seg, p->tw, (double *)part.p, s));
+    HIPCHK(gdsp::launch_reduce_partials((const double *)part.p, nrows, flen, d_acc,
+                                        (double *)red.p, s));
+    return GDSP_OK;
+  }
+#endif
   if (p->kind == KIND_LDS && p->log2n >= 4) {
     // fused path: packed segment pairs, persistent workers over contiguous
     // pair ranges (the 50 % overlap of consecutive pairs is re-read from L2)
     const int64_t npairs = (nseg + 1) / 2;
-    static const int64_t wmul = [] {  // workers per workgroup slot (development tuning switch)
-      const char *e = gdsp::dev_switch("GDSP_PW_WORKERS");
-      const int64_t v = e ? (int64_t)atoll(e) : 0;
-      return v >= 1 ? v : (int64_t)2048;
-    }();
+    // workers per workgroup slot: 512 / 1024 / 4096 measured 2.86 / 2.81 /
+    // 2.77 against 2.76 ms for 2048 (BASELINE configs[4])
+    constexpr int64_t wmul = 2048;
     int64_t target = wmul * (int64_t)gdsp::pwelch_workers_per_block(p->log2n);
     if (target > npairs) target = npairs;
     const int64_t ppw = (npairs + target - 1) / target;

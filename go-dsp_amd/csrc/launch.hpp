@@ -61,6 +61,13 @@ hipError_t launch_fft_lds12(bool inv, int load, bool split, const void *in, cd *
 hipError_t launch_pwelch_mixed(const MixedDesc &d, const double *x, int64_t nfft, int64_t stride,
                                int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,
                                const double *win, const cd *tw, double *partial, hipStream_t s);
+// fused Pwelch with wave-resident transforms (pwelch_wave.hip), 64 <= F <= 1024:
+// the launch geometry (groups of pairs per wave, workgroups, partial rows)
+bool pwelch_wave_applies(int log2f);
+void pwelch_wave_geometry(int log2f, int64_t nsegs, int64_t *gpw, int64_t *nblk, int64_t *nrows);
+hipError_t launch_pwelch_wave(int log2f, bool half, const double *x, int64_t nfft, int64_t stride,
+                              int64_t seg_begin, int64_t seg_end, int64_t gpw, int64_t nblk,
+                              const double *win, const cd *tw, double *partial, hipStream_t s);
 // fused Pwelch on a compiled specialisation (d = the plan's specialisation
 // descriptor, d.n = max(pad, nfft)); workers per block, 0 if d is none
 int pwelch_fixed_workers_per_block(const MixedDesc &d);

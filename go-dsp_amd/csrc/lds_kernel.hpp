@@ -27,11 +27,7 @@ struct Stage {
   __device__ __forceinline__ static int pad(int i) { return i + i / G::E; }
 };
 
-// DMA (development build, one complex row per workgroup): the row comes in by
-// LDS-DMA (buffer_load ... lds, nt) instead of register loads — 1: the whole
-// row into a row-sized buffer (the exchange buffer inside it), 2: in two
-// halves through the exchange buffer
-template <int LOG2N, bool INV, int LOAD, bool SPLIT, int LOG2E = 4, int DMA = 0>
+template <int LOG2N, bool INV, int LOAD, bool SPLIT, int LOG2E = 4>
 __global__ __launch_bounds__((Geo<LOG2N, LOG2E>::WG),
                              (LOG2N >= 13 && SPLIT ? (LOG2E == 4 ? 4 : 2) : 1)) void
 fft_lds_kernel(const void *__restrict__ in, cd *__restrict__ out, int64_t batch,
@@ -39,8 +35,7 @@ fft_lds_kernel(const void *__restrict__ in, cd *__restrict__ out, int64_t batch,
   using G = Geo<LOG2N, LOG2E>;
   using S = Stage<LOG2N>;
   constexpr int XD = (SPLIT ? 1 : 2) * G::LDS_DOUBLES;
-  constexpr int XD1 = DMA == 1 && 2 * G::N > XD ? 2 * G::N : XD;
-  __shared__ double lds[XD1 > S::DOUBLES ? XD1 : S::DOUBLES];
+  __shared__ double lds[XD > S::DOUBLES ? XD : S::DOUBLES];
   const int lt = threadIdx.x;
   const int slot = lt / G::T;
   const int t = lt & (G::T - 1);
@@ -89,33 +84,6 @@ fft_lds_kernel(const void *__restrict__ in, cd *__restrict__ out, int64_t batch,
       }
     }
     __syncthreads();  // the exchanges below reuse the buffer
-  } else if constexpr (LOAD == LOAD_COMPLEX && DMA > 0) {
-    static_assert(G::TPW == 1 && G::T % 64 == 0, "one row per workgroup");
-    constexpr int HALVES = DMA == 1 ? 1 : 2;
-    constexpr int HB = G::N * 16 / HALVES;  // bytes per DMA round
-    static_assert(HB <= (int)sizeof(lds), "the round fits the buffer");
-    constexpr int NW = G::T / 64, PIECES = HB / 1024;
-    const rsrc_t r = make_rsrc(reinterpret_cast<const cd *>(in) + gl * G::N, G::N * 16);
-    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-    const uint32_t lane16 = (uint32_t)(t & 63) * 16u;
-#pragma unroll
-    for (int h = 0; h < HALVES; ++h) {
-      if (h) __syncthreads();  // the previous round's reads are done
-#pragma unroll
-      for (int i = 0; i < PIECES / NW; ++i) {
-        const int p = w + i * NW;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            r, (__attribute__((address_space(3))) void *)((char *)lds + p * 1024), 16, lane16,
-            __builtin_amdgcn_readfirstlane(h * HB + p * 1024), 0, 2);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < G::E / HALVES; ++k) {
-        v[h * (G::E / HALVES) + k] = reinterpret_cast<const cd *>(lds)[t + k * G::T];
-        if constexpr (INV) v[h * (G::E / HALVES) + k].y = -v[h * (G::E / HALVES) + k].y;
-      }
-    }
   } else if constexpr (LOAD == LOAD_COMPLEX) {
     const cd *src = reinterpret_cast<const cd *>(in) + gl * G::N;
 #pragma unroll
@@ -128,8 +96,7 @@ fft_lds_kernel(const void *__restrict__ in, cd *__restrict__ out, int64_t batch,
 #pragma unroll
     for (int k = 0; k < G::E; ++k) v[k] = {ld_nt(&src[t + k * G::T]), 0.0};
   }
-  // (after a DMA the first exchange must wait for every read of the row)
-  fft_regs<LOG2N, SPLIT, 0, LOG2E>(v, t, tw, lre, lim, DMA == 0);
+  fft_regs<LOG2N, SPLIT, 0, LOG2E>(v, t, tw, lre, lim, true);
   if constexpr (S::ON) {
     const int64_t base = blk * G::TPW * G::N, total = batch * G::N;
     double tmp[2][G::E];
@@ -171,16 +138,12 @@ inline hipError_t launch_lds_t(const void *in, cd *out, int64_t batch, const cd 
   // N = 16384: one 139 KiB workgroup per CU either way; 32 points per thread
   // (512 threads, three passes) 0.918-0.930 against 0.966-0.969 ms per 2^27
   // samples for 16 (1024 threads, four passes), alternating runs
-  // (GDSP_LDS14_E16=1 to compare)
   if constexpr (LOG2N == 14) {
-    static const bool e32 = dev_switch("GDSP_LDS14_E16") == nullptr;
-    if (e32) {
-      using G5 = Geo<LOG2N, 5>;
-      const int64_t nb5 = (batch + G5::TPW - 1) / G5::TPW;
-      hipLaunchKernelGGL((fft_lds_kernel<LOG2N, INV, LOAD, SPLIT, 5>), dim3((unsigned)nb5),
-                         dim3(G5::WG), 0, s, in, out, batch, tw, scale);
-      return hipGetLastError();
-    }
+    using G5 = Geo<LOG2N, 5>;
+    const int64_t nb5 = (batch + G5::TPW - 1) / G5::TPW;
+    hipLaunchKernelGGL((fft_lds_kernel<LOG2N, INV, LOAD, SPLIT, 5>), dim3((unsigned)nb5),
+                       dim3(G5::WG), 0, s, in, out, batch, tw, scale);
+    return hipGetLastError();
   }
   using G = Geo<LOG2N>;
   const int64_t nblk = (batch + G::TPW - 1) / G::TPW;

@@ -590,21 +590,54 @@ __global__ __launch_bounds__((RaderGeo<R0, RS...>::WG)) void rader_fixed_kernel(
   const int64_t lrow = valid ? row : batch - 1;  // a slot past the batch reads a valid row
   double *ld = lds + sub * RG::DPT;
   cd *lc = reinterpret_cast<cd *>(ld);
-  // 1. the row, natural order
-  cd xr[NQ];
+  // 1. the row, natural order. TPW > 1 (short rows: few threads per
+  // transform) loads the workgroup's TPW contiguous rows as one chunk, every
+  // thread a lane of one coalesced stream (threads-per-row loads would touch
+  // 64 / T1 rows per wave-instruction; at P = 17, T1 = 1, a lane per row).
+  constexpr int CH = RG::TPW * P, NC = (CH + RG::WG - 1) / RG::WG;
+  const int64_t c0 = xcd_remap(blockIdx.x, gridDim.x) * (int64_t)CH, cend = batch * P;
+  auto chunk_slot = [&](int e) -> cd * {  // chunk element e -> its row's staging slot
+    const int s2 = e / P;
+    return reinterpret_cast<cd *>(lds + s2 * RG::DPT) + (e - s2 * P);
+  };
+  cd xr[RG::TPW > 1 ? 1 : NQ];
+  if constexpr (RG::TPW > 1) {
+    static_assert(!SPLIT, "several rows per workgroup only with complex staging");
+    cd xc[NC];
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const int i = tl + q * T1;
-    if (q * T1 + T1 <= P || i < P) {
-      if constexpr (LOAD == LOAD_REAL) {
-        xr[q] = {ld_nt(reinterpret_cast<const double *>(in) + lrow * P + i), 0.0};
-      } else {
-        xr[q] = ld_nt(reinterpret_cast<const cd *>(in) + lrow * P + i);
-        if constexpr (INV) xr[q].y = -xr[q].y;
+    for (int q = 0; q < NC; ++q) {
+      const int e = (int)threadIdx.x + q * RG::WG;
+      xc[q] = {0.0, 0.0};
+      if ((q + 1) * RG::WG <= CH || e < CH) {
+        if (c0 + e < cend) {
+          if constexpr (LOAD == LOAD_REAL) {
+            xc[q] = {ld_nt(reinterpret_cast<const double *>(in) + c0 + e), 0.0};
+          } else {
+            xc[q] = ld_nt(reinterpret_cast<const cd *>(in) + c0 + e);
+            if constexpr (INV) xc[q].y = -xc[q].y;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const int e = (int)threadIdx.x + q * RG::WG;
+      if ((q + 1) * RG::WG <= CH || e < CH) *chunk_slot(e) = xc[q];
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int i = tl + q * T1;
+      if (q * T1 + T1 <= P || i < P) {
+        if constexpr (LOAD == LOAD_REAL) {
+          xr[q] = {ld_nt(reinterpret_cast<const double *>(in) + lrow * P + i), 0.0};
+        } else {
+          xr[q] = ld_nt(reinterpret_cast<const cd *>(in) + lrow * P + i);
+          if constexpr (INV) xr[q].y = -xr[q].y;
+        }
       }
     }
   }
-  const cd y0 = xr[0];  // (meaningful in the thread with tl = 0: element 0)
   // 2. gather a[q] = y[gpow[q]] into the first pass's registers
   First p0;
   int gi[First::J][R0];
@@ -614,7 +647,9 @@ __global__ __launch_bounds__((RaderGeo<R0, RS...>::WG)) void rader_fixed_kernel(
 #pragma unroll
     for (int r = 0; r < R0; ++r) gi[jj][r] = First::act(j, true) ? gpow[j + r * First::NB] : 0;
   }
+  cd y0;  // element 0 of the row (X[0] = y0 + A[0]; y0 is added to every other output)
   if constexpr (SPLIT) {
+    y0 = xr[0];  // (meaningful in the thread with tl = 0)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       if (h) __syncthreads();  // the real parts' gathers are done
@@ -637,12 +672,15 @@ __global__ __launch_bounds__((RaderGeo<R0, RS...>::WG)) void rader_fixed_kernel(
       }
     }
   } else {
+    if constexpr (RG::TPW == 1) {
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int i = tl + q * T1;
-      if (q * T1 + T1 <= P || i < P) lc[i] = xr[q];
+      for (int q = 0; q < NQ; ++q) {
+        const int i = tl + q * T1;
+        if (q * T1 + T1 <= P || i < P) lc[i] = xr[q];
+      }
     }
     __syncthreads();
+    y0 = lc[0];
 #pragma unroll
     for (int jj = 0; jj < First::J; ++jj) {
       const int j = tl + jj * T1;
@@ -722,7 +760,7 @@ __global__ __launch_bounds__((RaderGeo<R0, RS...>::WG)) void rader_fixed_kernel(
   }
   const cd x0 = y0 + a0;
   cd *dst = out + lrow * P;
-  cd res[NQ];
+  cd res[RG::TPW > 1 ? NC : NQ];
 #pragma unroll
   for (int h = 0; h < (SPLIT ? 2 : 1); ++h) {
     __syncthreads();  // the previous LDS reads are done
@@ -743,20 +781,38 @@ __global__ __launch_bounds__((RaderGeo<R0, RS...>::WG)) void rader_fixed_kernel(
       else lc[0] = x0;
     }
     __syncthreads();
+    if constexpr (RG::TPW > 1) {
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int i = t2 + q * T1;
-      if (q * T1 + T1 <= P || i < P) {
-        if constexpr (SPLIT) {
-          if (h) res[q].y = ld[i];
-          else res[q].x = ld[i];
-        } else {
-          res[q] = lc[i];
+      for (int q = 0; q < NC; ++q) {
+        const int e = (int)threadIdx.x + q * RG::WG;
+        if ((q + 1) * RG::WG <= CH || e < CH) res[q] = *chunk_slot(e);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int i = t2 + q * T1;
+        if (q * T1 + T1 <= P || i < P) {
+          if constexpr (SPLIT) {
+            if (h) res[q].y = ld[i];
+            else res[q].x = ld[i];
+          } else {
+            res[q] = lc[i];
+          }
         }
       }
     }
   }
-  if (valid) {
+  if constexpr (RG::TPW > 1) {
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const int e = (int)threadIdx.x + q * RG::WG;
+      if (((q + 1) * RG::WG <= CH || e < CH) && c0 + e < cend) {
+        cd y = res[q];
+        if constexpr (INV) y = {y.x * scale, -y.y * scale};
+        st_nt(out + c0 + e, y);
+      }
+    }
+  } else if (valid) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int i = t2 + q * T1;

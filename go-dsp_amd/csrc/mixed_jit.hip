@@ -421,13 +421,11 @@ JitCol *jit_col_build(int dev, const int *rad, int np) {
   // 1024 threads. The exchanges go as real / imaginary halves (SPLIT), which
   // doubles the width the LDS allows. Per 2^27 samples, 16 complex-exchange
   // columns -> this: 390625 3.15 -> 2.73 ms, 3^13 3.18 -> 2.98, 10^6 2.80
-  // both (GDSP_COL_LDS / GDSP_COL_SPLIT=0 to compare)
+  // both
   const int sl = ((L + 7) & ~7) + 1;
-  int lds_max = 81920;
-  if (const char *e = dev_switch("GDSP_COL_LDS")) lds_max = atoi(e);
-  const char *se = dev_switch("GDSP_COL_SPLIT");
-  const bool split = !(se && se[0] == '0');
-  const int bytes = split ? 8 : 16;
+  const int lds_max = 81920;
+  const bool split = true;
+  const int bytes = 8;
   int w = 64;
   while (w > 1 && (w * sl * bytes > lds_max || w * t1 > 1024)) w >>= 1;
   if (w * sl * bytes > 163840 || w * t1 > 1024) return nullptr;

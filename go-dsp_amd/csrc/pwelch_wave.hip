@@ -1,0 +1,160 @@
+// pwelch_wave.hip — the fused Pwelch accumulation (spectral/pwelch.go:104-122)
+// for FFT lengths F = max(Pad, NFFT) from 64 to 1024, where a packed segment
+// pair's transform (16 points per thread, T = F / 16 threads) fits inside one
+// 64-lane wave. Same arithmetic as pwelch_half_kernel / pwelch_kernel: z =
+// w x_s + i w x_(s+1), Z = FFT_F(z), each thread accumulating |Z_k|^2 of its
+// own bins in registers; the k / F - k fold is done once in finalise.
+//
+// What is different is the synchronisation. Those kernels run 256-thread
+// workgroups of several transforms and meet at a workgroup barrier around
+// every exchange, so all four waves of a workgroup stall together at each
+// LDS round trip. Here every transform lives in one wave and exchanges
+// through an LDS region of its own, so an exchange needs no barrier (xsync:
+// a wave's LDS instructions execute in order) and the waves of a SIMD
+// interleave freely. Each wave is a persistent worker over a contiguous range
+// of pair groups: the S = 64 / T slots of the wave take S consecutive pairs
+// per iteration, so a worker's pair range, its loop and its tests are wave-
+// uniform. With HALF (Noverlap = NFFT / 2, Pad = NFFT) segment s + 1's first
+// half is segment s's second half: 24 loads per pair instead of 32 (the
+// half-block a slot shares with its neighbour comes from L2). PF: the next
+// group's samples are loaded into registers while this group's FFT runs.
+#include "fft_device.hpp"
+#include "launch.hpp"
+
+namespace gdsp {
+
+constexpr int kPwWaves = 4;  // waves per workgroup
+#ifndef GDSP_PWW_PF
+#define GDSP_PWW_PF 1
+#endif
+
+template <int LOG2F, bool HALF, bool PF>
+__global__ __launch_bounds__(64 * kPwWaves) void pwelch_wave_kernel(
+    const double *__restrict__ x, int64_t nfft, int64_t stride, int64_t seg_begin,
+    int64_t seg_end, int64_t groups_per_wave, const double *__restrict__ win,
+    const cd *__restrict__ tw, double *__restrict__ partial) {
+  using G = Geo<LOG2F>;
+  constexpr int E = G::E, T = G::T, F = G::N, H = E / 2;
+  static_assert(E == 16 && T <= 64 && 64 % T == 0, "one transform inside one wave");
+  constexpr int S = 64 / T;          // transforms (pairs) per wave
+  constexpr int XS = G::STRIDE;      // exchange doubles per transform
+  __shared__ double lds[kPwWaves * S * XS + F];
+  const int lt = (int)threadIdx.x;
+  const int w = lt >> 6, lane = lt & 63, s = lane / T, t = lane % T;
+  double *const lre = lds + (w * S + s) * XS;
+  double *const wl = lds + kPwWaves * S * XS;
+  for (int i = lt; i < F; i += 64 * kPwWaves) wl[i] = win[i];
+  __syncthreads();
+  // the worker (wave) and its group range: wave-uniform
+  const int64_t wave = (int64_t)blockIdx.x * kPwWaves + __builtin_amdgcn_readfirstlane(w);
+  const int64_t npairs = (seg_end - seg_begin + 1) / 2;
+  const int64_t ngroups = (npairs + S - 1) / S;
+  const int64_t g0 = wave * groups_per_wave;
+  const int64_t gend = g0 + groups_per_wave < ngroups ? g0 + groups_per_wave : ngroups;
+  double acc[E];
+#pragma unroll
+  for (int k = 0; k < E; ++k) acc[k] = 0.0;
+  // samples of group g for this slot: a[k] = segment s0's element t + k T,
+  // b[k] = segment s0 + 1's (HALF: b[k] = a[k + H] for k < H, so only b[H..E)
+  // is loaded); zero past the signal's segments and past nfft (Pad > NFFT)
+  constexpr int NB = HALF ? H : E;
+  auto load = [&](int64_t g, double (&a)[E], double (&b)[NB]) {
+    const int64_t p = g * S + s;
+    const bool active = g < gend && p < npairs;
+    const int64_t s0 = seg_begin + 2 * (active ? p : 0);
+    const bool has1 = active && s0 + 1 < seg_end;
+    const double *xa = opaque_ptr(x) + s0 * stride;
+    const double *xb = xa + stride;
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+      const int i = t + k * T;
+      a[k] = (active && (HALF || i < nfft)) ? xa[i] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int i = t + (HALF ? k + H : k) * T;
+      b[k] = (has1 && (HALF || i < nfft)) ? xb[i] : 0.0;
+    }
+  };
+  double na[E], nb[NB];
+  if constexpr (PF) load(g0, na, nb);
+  for (int64_t g = g0; g < gend; ++g) {
+    double a[E], b[NB];
+    if constexpr (PF) {
+#pragma unroll
+      for (int k = 0; k < E; ++k) a[k] = na[k];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) b[k] = nb[k];
+      if (g + 1 < gend) load(g + 1, na, nb);
+    } else {
+      load(g, a, b);
+    }
+    const bool active = g * S + s < npairs;
+    const int tt = opaque_int(t);
+    cd v[E];
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+      const double wk = wl[tt + k * T];
+      const double bk = HALF ? (k < H ? a[k + H] : b[k - H]) : b[k];
+      v[k] = {a[k] * wk, bk * wk};
+    }
+    fft_regs<LOG2F, true, 1, 4, 0, 0, const cd *, 0, 0, NoEpi, 0, 16, true>(v, tt, tw, lre, lre,
+                                                                           g == g0);
+    if (active) {
+#pragma unroll
+      for (int k = 0; k < E; ++k) acc[k] = fma(v[k].y, v[k].y, fma(v[k].x, v[k].x, acc[k]));
+    }
+  }
+  // every slot writes its row (zeros for a slot with no pairs): the reduce
+  // sums all of them
+  double *dst = partial + (wave * S + s) * (int64_t)F;
+#pragma unroll
+  for (int k = 0; k < E; ++k) dst[t + k * T] = acc[k];
+}
+
+template <int LOG2F, bool HALF, bool PF>
+static hipError_t launch_pww_t(const double *x, int64_t nfft, int64_t stride, int64_t seg_begin,
+                               int64_t seg_end, int64_t gpw, int64_t nblk, const double *win,
+                               const cd *tw, double *partial, hipStream_t s) {
+  hipLaunchKernelGGL((pwelch_wave_kernel<LOG2F, HALF, PF>), dim3((unsigned)nblk),
+                     dim3(64 * kPwWaves), 0, s, x, nfft, stride, seg_begin, seg_end, gpw, win, tw,
+                     partial);
+  return hipGetLastError();
+}
+
+// Geometry of a launch: pairs per group S = 64 / T (T = F / 16), groups per
+// wave, workgroups, and the partial rows the reduce sums (one per slot).
+bool pwelch_wave_applies(int log2f) { return log2f >= 6 && log2f <= 10; }
+
+void pwelch_wave_geometry(int log2f, int64_t nsegs, int64_t *gpw, int64_t *nblk,
+                          int64_t *nrows) {
+  const int S = 64 / ((1 << log2f) / 16);
+  const int64_t npairs = (nsegs + 1) / 2;
+  const int64_t ngroups = (npairs + S - 1) / S;
+  // about 2048 waves (8 per CU: two per SIMD, the kernel's register budget)
+  const int64_t target = 2048;
+  const int64_t g = ngroups < 1 ? 1 : (ngroups + target - 1) / target;
+  const int64_t waves = ngroups < 1 ? 1 : (ngroups + g - 1) / g;
+  *gpw = g;
+  *nblk = (waves + kPwWaves - 1) / kPwWaves;
+  *nrows = *nblk * kPwWaves * S;
+}
+
+hipError_t launch_pwelch_wave(int log2f, bool half, const double *x, int64_t nfft, int64_t stride,
+                              int64_t seg_begin, int64_t seg_end, int64_t gpw, int64_t nblk,
+                              const double *win, const cd *tw, double *partial, hipStream_t s) {
+  if (nblk < 1 || nblk > 0x7fffffff) return hipErrorInvalidValue;
+  switch (log2f) {
+#define GDSP_PWW(L)                                                                               \
+  case L:                                                                                       \
+    return half ? launch_pww_t<L, true, GDSP_PWW_PF>(x, nfft, stride, seg_begin, seg_end, gpw,  \
+                                                     nblk, win, tw, partial, s)                 \
+                : launch_pww_t<L, false, GDSP_PWW_PF>(x, nfft, stride, seg_begin, seg_end, gpw, \
+                                                      nblk, win, tw, partial, s);
+    GDSP_PWW(6) GDSP_PWW(7) GDSP_PWW(8) GDSP_PWW(9) GDSP_PWW(10)
+#undef GDSP_PWW
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace gdsp
