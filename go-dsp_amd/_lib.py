@@ -94,8 +94,10 @@ SIGNATURES = {
 # include/gdsp_fft_dev.h: bound only when the loaded library is the
 # development build (the product library does not export them)
 DEV_SIGNATURES = {
-    "gdsp_plan_wave_q": (_I, [_P]),
-    "gdsp_plan_shfl": (_I, [_P]),
+    "gdsp_dev_chirpz_wave_q": (_I, [_I64]),
+    "gdsp_dev_fft_batch_chirpz_wave": (_I, [_I64, _P, _P, _I64, _I, _P]),
+    "gdsp_dev_fft_batch_chirpz_shfl": (_I, [_I64, _P, _P, _I64, _I, _P]),
+    "gdsp_dev_pwelch4096_shfl_accumulate": (_I, [_P, _I64, _I64, _I64, _P, _P, _P]),
 }
 
 _lib = None
@@ -173,7 +175,7 @@ def check(status: int, what: str = "") -> None:
 
 def is_dev_build() -> bool:
     """True when the loaded library is the development build."""
-    return hasattr(lib(), "gdsp_plan_wave_q")
+    return hasattr(lib(), "gdsp_dev_chirpz_wave_q")
 
 
 def device_count() -> int:

@@ -22,8 +22,7 @@
 // four and sixteen. Measured slower (chirp-z 3000: 3.53 against 3.32 ms; the
 // DPP and permlane moves take VALU issue slots the block kernel spends on
 // nothing), so gdsp_api.hip takes it only under GDSP_BLU_SHFL=1.
-#include "fft_device.hpp"
-#include "launch.hpp"
+#include "dev.hpp"
 #include "shfl.hpp"
 
 namespace gdsp {

@@ -29,8 +29,7 @@
 //      as real and imaginary halves (three workgroup barriers per transform);
 //      only p with n' + 2048 p < n is computed;
 //   4. X = r * conj(w) (the chirp), first n.
-#include "fft_device.hpp"
-#include "launch.hpp"
+#include "dev.hpp"
 
 namespace gdsp {
 

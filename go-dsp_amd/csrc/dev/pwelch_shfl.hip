@@ -21,8 +21,7 @@
 //   per dword pair);
 //   pass 3: DFT_16 over D0 -> K2; bin K = K0 + 16 K1 + 256 K2.
 // Four workgroup barriers per pair instead of eight.
-#include "fft_device.hpp"
-#include "launch.hpp"
+#include "dev.hpp"
 #include "shfl.hpp"
 
 namespace gdsp {

@@ -5,7 +5,7 @@
 // (pwelch_shfl.hip, bluestein_shfl.hip); tools/swap_probe.hip checks the
 // primitives on the GPU.
 #pragma once
-#include "fft_device.hpp"
+#include "../fft_device.hpp"
 
 namespace gdsp {
 

@@ -19,9 +19,6 @@
 
 #include "fft_device.hpp"
 #include "gdsp_fft.h"
-#ifdef GDSP_DEV_BUILD
-#include "gdsp_fft_dev.h"
-#endif
 #include "launch.hpp"
 #include "api_internal.hpp"
 
@@ -331,15 +328,6 @@ struct gdsp_plan {
   gdsp_plan *mplan = nullptr;
   cd *chirp = nullptr;
   cd *bhat = nullptr;
-  // wave-resident chirp-z (fft_wave.hip) for 512 < n <= 4096: Q = M / 2048
-  // waves per transform; bhatw[q 2048 + k] = bhat[Q k + q], wbase[q 65 + j] =
-  // W_M^(q j) (j <= 64); t2048 = T_2048
-  int wq = 0;
-  cd *bhatw = nullptr, *wbase = nullptr;
-  const cd *t2048 = nullptr;
-  // shuffle chirp-z (bluestein_shfl.hip) for M = 8192: bhat in the kernel's
-  // register order, bhats[r 256 + t] = bhat[bluestein_shfl_bin(t, r)]
-  cd *bhats = nullptr;
   // output-split chirp-z (bluestein_kernel PARTS): n in (8192, 16384] whose
   // NextPowerOf2(2n-1) = 32768 exceeds one kernel runs as `parts` fused
   // convolutions of M = 16384, each giving kpart outputs; bhat holds parts * M
@@ -689,72 +677,6 @@ bool mixrows_build(int dev, int64_t n, gdsp_plan *p) {
   return false;
 }
 
-#ifdef GDSP_DEV_BUILD
-// ---- measured and rejected chirp-z kernels (development build) ----
-// The wave-resident chirp-z kernel (fft_wave.hip) for 512 < n <= 4096, when
-// GDSP_BLU_WAVE=1. Measured slower than the block-wide bluestein_kernel at
-// every Q (chirp-z 3000: 3.83 against 3.35 ms), so it is opt-in.
-bool wave_chirpz_enabled() {
-  static const bool on = [] {
-    const char *e = gdsp::dev_switch("GDSP_BLU_WAVE");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-// Plan tables of the wave-resident chirp-z kernel (see gdsp_plan::wq): bhat
-// permuted per wave, and the DIF/DIT twiddle bases W_M^(q j), j <= 64.
-int build_wave_tables(int dev, gdsp_plan *p) {
-  const int64_t n = p->n, M = p->m;
-  const int Q = gdsp::bluestein_wave_q(n, M);
-  if (!Q) return GDSP_OK;
-  gdsp_plan *p2048 = nullptr;
-  STCHK(get_plan_locked(dev, 2048, &p2048));
-  hipStream_t s = thread_stream(dev);
-  std::vector<cd> bh((size_t)M), bw((size_t)M), wb((size_t)(Q * 65));
-  HIPCHK(hipStreamSynchronize(s));
-  HIPCHK(hipMemcpy(bh.data(), p->bhat, (size_t)M * sizeof(cd), hipMemcpyDeviceToHost));
-  const long double tau = 2.0L * 3.141592653589793238462643383279502884L;
-  for (int q = 0; q < Q; ++q) {
-    for (int64_t k = 0; k < 2048; ++k) bw[(size_t)(q * 2048 + k)] = bh[(size_t)(Q * k + q)];
-    for (int j = 0; j <= 64; ++j) {
-      const long double a = -tau * (long double)(q * j) / (long double)M;
-      wb[(size_t)(q * 65 + j)] = {(double)cosl(a), (double)sinl(a)};
-    }
-  }
-  HIPCHK(hipMalloc((void **)&p->bhatw, bw.size() * sizeof(cd)));
-  HIPCHK(hipMalloc((void **)&p->wbase, wb.size() * sizeof(cd)));
-  STCHK(copy_h2d(p->bhatw, bw.data(), bw.size() * sizeof(cd), s));
-  STCHK(copy_h2d(p->wbase, wb.data(), wb.size() * sizeof(cd), s));
-  HIPCHK(hipStreamSynchronize(s));
-  p->t2048 = p2048->tw;
-  p->wq = Q;
-  return GDSP_OK;
-}
-
-// The M = 8192 chirp-z kernel whose FFTs keep one exchange in the wave
-// (bluestein_shfl.hip), when GDSP_BLU_SHFL=1.
-bool shfl_chirpz_enabled() {
-  static const bool on = [] {
-    const char *e = gdsp::dev_switch("GDSP_BLU_SHFL");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-int build_shfl_tables(gdsp_plan *p) {
-  hipStream_t s = thread_stream(p->device);
-  std::vector<cd> bh((size_t)p->m), bs((size_t)p->m);
-  HIPCHK(hipStreamSynchronize(s));
-  HIPCHK(hipMemcpy(bh.data(), p->bhat, (size_t)p->m * sizeof(cd), hipMemcpyDeviceToHost));
-  for (int r = 0; r < 32; ++r)
-    for (int t = 0; t < 256; ++t) bs[(size_t)(r * 256 + t)] = bh[(size_t)gdsp::bluestein_shfl_bin(t, r)];
-  HIPCHK(hipMalloc((void **)&p->bhats, bs.size() * sizeof(cd)));
-  STCHK(copy_h2d(p->bhats, bs.data(), bs.size() * sizeof(cd), s));
-  HIPCHK(hipStreamSynchronize(s));
-  return GDSP_OK;
-}
-#endif  // GDSP_DEV_BUILD
 
 bool fourstep2_applies(int ln);  // (exec_fourstep2 below)
 
@@ -1005,10 +927,6 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
     }
   }
   bool c6k_ok = !(plan_flags() & GDSP_ALGO_CHIRPZ_POW2);
-#ifdef GDSP_DEV_BUILD
-  // the rejected M = 8192 / 2048 Q kernels, when switched on, keep their M
-  if (wave_chirpz_enabled() || shfl_chirpz_enabled()) c6k_ok = false;
-#endif
   if (p->kind == KIND_BLUESTEIN && p->parts == 1 && gdsp::chirpz6k_m(n) && c6k_ok) {
     // 2049 <= n <= 3072 (1025 <= n <= 1536): bluestein.go:70 pads the
     // convolution to 8192 (4096); M = 6144 (3072) = 16 * RB * 16 gives the
@@ -1066,13 +984,6 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
     if (e != hipSuccess) st = fail(GDSP_ERR_HIP, hipGetErrorString(e));
   }
   (void)hipFree(db);
-#ifdef GDSP_DEV_BUILD
-  if (st == GDSP_OK && wave_chirpz_enabled() && gdsp::bluestein_wave_q(n, p->m))
-    st = build_wave_tables(dev, p);
-  if (st == GDSP_OK && !p->wq && shfl_chirpz_enabled() && p->kind == KIND_BLUESTEIN &&
-      p->m == 8192 && 2 * n <= p->m)
-    st = build_shfl_tables(p);
-#endif
   return st;
 }
 
@@ -1524,18 +1435,6 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
         HIPCHK(gdsp::launch_real_to_complex((const double *)in, (cd *)tmp.p, batch * p->n, s));
         src = (const cd *)tmp.p;
       }
-#ifdef GDSP_DEV_BUILD
-      if (p->kind == KIND_BLUESTEIN && p->wq) {
-        HIPCHK(gdsp::launch_bluestein_wave(p->wq, inv, src, out, p->n, batch, p->t2048, p->wbase,
-                                           p->bhatw, p->chirp, scale, s));
-        return GDSP_OK;
-      }
-      if (p->kind == KIND_BLUESTEIN && p->bhats) {
-        HIPCHK(gdsp::launch_bluestein_shfl(inv, src, out, p->n, batch, p->mplan->tw, p->chirp,
-                                           p->bhats, scale, s));
-        return GDSP_OK;
-      }
-#endif
       if (p->kind == KIND_BLUESTEIN && p->parts > 1) {
         // the parts of a row run in different workgroups, so a part may
         // write the row before another has read it: in place (the four-step
@@ -1644,14 +1543,6 @@ const char *knob(Knob k) {
                                       "GDSP_JIT_INCLUDE", "GDSP_JIT_CACHE",     "GDSP_JIT_VERBOSE",
                                       "XDG_CACHE_HOME",  "HOME"};
   return (int)k >= 0 && (int)k < (int)(sizeof names / sizeof names[0]) ? getenv(names[k]) : nullptr;
-}
-const char *dev_switch(const char *name) {
-#ifdef GDSP_DEV_BUILD
-  return getenv(name);
-#else
-  (void)name;
-  return nullptr;
-#endif
 }
 unsigned algo_flags() { return g_algo.load(std::memory_order_relaxed); }
 }  // namespace gdsp
@@ -2019,11 +1910,6 @@ int gdsp_plan_create_chirpz(int64_t n, gdsp_plan **plan) {
 int gdsp_plan_destroy(gdsp_plan *) { return GDSP_OK; }
 
 int gdsp_plan_kind(const gdsp_plan *plan) { return plan ? plan->kind : -1; }
-#ifdef GDSP_DEV_BUILD
-// include/gdsp_fft_dev.h: queries of the development build's kernels only
-int gdsp_plan_wave_q(const gdsp_plan *plan) { return plan ? plan->wq : 0; }
-int gdsp_plan_shfl(const gdsp_plan *plan) { return plan && plan->bhats ? 1 : 0; }
-#endif
 int gdsp_plan_parts(const gdsp_plan *plan) { return plan ? plan->parts : 0; }
 
 int gdsp_plan_info(const gdsp_plan *plan, int64_t *n, int64_t *m, int64_t *n1, int64_t *n2,

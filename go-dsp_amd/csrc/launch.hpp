@@ -43,10 +43,6 @@ enum Knob {
   KNOB_HOME,
 };
 const char *knob(Knob k);
-// Experiment switches of the development build (make DEV=1, GDSP_DEV_BUILD):
-// the switch's value there; nullptr in the default build, whose paths are the
-// measured ones.
-const char *dev_switch(const char *name);
 // Algorithm selection flags (gdsp_set_algorithm, include/gdsp_fft.h) in
 // force when a plan is built.
 unsigned algo_flags();
@@ -124,27 +120,6 @@ hipError_t launch_chirpz6k(int64_t m, bool inv, int load, const void *in, cd *ou
 hipError_t launch_bluestein_parts(int log2m, bool inv, const cd *in, cd *out, int64_t n,
                                   int64_t batch, int parts, int64_t kpart, const cd *twm,
                                   const cd *chirp, const cd *bhat, double scale, hipStream_t s);
-#ifdef GDSP_DEV_BUILD
-// ---- measured and rejected kernels (development build only) ----
-// wave-resident chirp-z (fft_wave.hip): waves per transform Q = M / 2048 for
-// 512 < n <= 1024 Q, 2n - 1 <= M (0: not this kernel's case)
-int bluestein_wave_q(int64_t n, int64_t m);
-// wbase[q 65 + j] = W_M^(q j) (j <= 64), bhatw[q 2048 + k] = bhat[Q k + q]
-hipError_t launch_bluestein_wave(int q, bool inv, const cd *in, cd *out, int64_t n, int64_t batch,
-                                 const cd *t2048, const cd *wbase, const cd *bhatw, const cd *chirp,
-                                 double scale, hipStream_t s);
-// M = 8192 chirp-z with in-wave exchanges (bluestein_shfl.hip), 2049 <= n <=
-// 4096: bhatp[r 256 + t] = bhat[bluestein_shfl_bin(t, r)], twm = T_8192
-int bluestein_shfl_bin(int t, int r);
-hipError_t launch_bluestein_shfl(bool inv, const cd *in, cd *out, int64_t n, int64_t batch,
-                                 const cd *twm, const cd *chirp, const cd *bhatp, double scale,
-                                 hipStream_t s);
-// NFFT = 4096 half overlap with the in-wave second exchange (pwelch_shfl.hip);
-// same arguments and partial layout as launch_pwelch_half(12, ...)
-hipError_t launch_pwelch4096_shfl(const double *x, int64_t seg_begin, int64_t seg_end, int64_t ppw,
-                                  int64_t nworkers, const double *win, const cd *tw,
-                                  double *partial, hipStream_t s);
-#endif  // GDSP_DEV_BUILD
 hipError_t launch_global_pass(int radix, bool conj_in, int load, bool conj_scale_out,
                               const void *in, cd *out, const cd *tw, int log2n, int log2ns,
                               int64_t batch, double scale, hipStream_t s);
@@ -156,13 +131,6 @@ hipError_t launch_pwelch(int log2f, const double *x, int64_t nfft, int64_t strid
 hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int64_t seg_end,
                               int64_t ppw, int64_t nworkers, const double *win, const cd *tw,
                               double *partial, hipStream_t s);
-#ifdef GDSP_DEV_BUILD
-// round-4 occupancy variants of the row kernel (pwelch_rowx.hip, dev build)
-hipError_t launch_pwelch_rowx4096(int variant, const double *x, int64_t seg_begin,
-                                  int64_t seg_end, int64_t ppw, int64_t nworkers,
-                                  const double *win, const cd *tw, double *partial,
-                                  hipStream_t s);
-#endif
 // the row kernel (pwelch_row.hip) behind launch_pwelch_half(12, ...)
 hipError_t launch_pwelch_row4096(const double *x, int64_t seg_begin, int64_t seg_end, int64_t ppw,
                                  int64_t nworkers, const double *win, const cd *tw,

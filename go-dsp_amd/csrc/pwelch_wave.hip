@@ -89,13 +89,17 @@ __global__ __launch_bounds__(64 * kPwWaves) void pwelch_wave_kernel(
     } else {
       load(g, a, b);
     }
-    const bool active = g * S + s < npairs;
+    const int64_t p = g * S + s;
+    const bool active = p < npairs;
+    // (HALF: a partnerless last pair, odd segment count, takes zeros for its
+    // second segment's first half too, not segment s0's second half)
+    const bool has1 = active && seg_begin + 2 * p + 1 < seg_end;
     const int tt = opaque_int(t);
     cd v[E];
 #pragma unroll
     for (int k = 0; k < E; ++k) {
       const double wk = wl[tt + k * T];
-      const double bk = HALF ? (k < H ? a[k + H] : b[k - H]) : b[k];
+      const double bk = HALF ? (k < H ? (has1 ? a[k + H] : 0.0) : b[k - H]) : b[k];
       v[k] = {a[k] * wk, bk * wk};
     }
     fft_regs<LOG2F, true, 1, 4, 0, 0, const cd *, 0, 0, NoEpi, 0, 16, true>(v, tt, tw, lre, lre,

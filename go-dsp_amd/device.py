@@ -51,12 +51,6 @@ class Plan:
         # chirp-z convolution length; four-step split; runtime-compiled?
         self.m, self.n1, self.n2 = v[1].value, v[2].value, v[3].value
         self.runtime_compiled = bool(rc.value)
-        # waves per transform of the wave-resident chirp-z kernel (0: another kernel)
-        # (development build only: the product library runs neither kernel)
-        L = lib()
-        self.wave_q = int(L.gdsp_plan_wave_q(self.handle)) if hasattr(L, "gdsp_plan_wave_q") else 0
-        # 1: the M = 8192 chirp-z kernel with in-wave exchanges (GDSP_BLU_SHFL=1)
-        self.shfl = int(L.gdsp_plan_shfl(self.handle)) if hasattr(L, "gdsp_plan_shfl") else 0
         # output parts of the chirp-z kernel (> 1: n in (8192, 14563] on M = 16384)
         self.parts = int(lib().gdsp_plan_parts(self.handle))
 

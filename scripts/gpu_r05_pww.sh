@@ -4,8 +4,8 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/r05
 export GDSP_JIT_CACHE=$GRAFT_REPO_ROOT/gpurun_out/jitcache
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
-  -k "pwelch or Pwelch or rader" > gpurun_out/r05/pytest_pww.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  > gpurun_out/r05/pytest_pww.log 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -3 gpurun_out/r05/pytest_pww.log; [ $rc -eq 0 ] || exit $rc
 CASES="64:32 128:64 256:0 256:128 512:256 1024:0 1024:512 2048:1024 4096:2048"
 for r in 1 2; do

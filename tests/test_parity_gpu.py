@@ -865,7 +865,7 @@ def _dev_lib() -> str:
 
 
 # the wave-resident chirp-z kernel (fft_wave.hip, development build,
-# GDSP_BLU_WAVE=1):
+# gdsp_dev_fft_batch_chirpz_wave):
 # Q = M/2048 waves per transform, Q = 1 (n <= 1024), 2, 4; the edges of each
 # range, primes, and batches that leave the last workgroup partly empty (2 or
 # 4 transforms per workgroup at Q = 2, 1). Its exchanges are a wave-local LDS
@@ -873,35 +873,46 @@ def _dev_lib() -> str:
 WAVE_N = [513, 700, 1009, 1023, 1024, 1025, 1500, 2039, 2047, 2048, 2049, 2053, 3000, 3072,
           3073, 4093, 4095, 4096]
 
-
-def test_chirpz_wave_kernel():
-    code = r'''
-import importlib, os, sys
+_DEV_CHIRPZ = r'''
+import ctypes, importlib, os, sys
 sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
 import numpy as np, oracle, torch
-D = importlib.import_module("go-dsp_amd.device")
+L = importlib.import_module("go-dsp_amd._lib")
+assert L.is_dev_build()
+lib = L.lib()
+fn = getattr(lib, os.environ["DEV_FN"])
 def row_nrel(a, b):
     return max(np.linalg.norm(x - y) / np.linalg.norm(y) for x, y in zip(a, b))
-for n in [int(v) for v in os.environ["WAVE_N"].split()]:
-    p = D.plan(n, chirpz=True)
-    m = 1 << (2 * n - 2).bit_length()  # bluestein.go:70
-    assert p.kind == 3 and p.m == m and p.wave_q == m // 2048, (n, p.kind, p.m, p.wave_q)
+def run(x, inverse):
+    xt = torch.from_numpy(x).cuda()
+    yt = torch.empty_like(xt)
+    st = fn(x.shape[1], ctypes.c_void_p(xt.data_ptr()), ctypes.c_void_p(yt.data_ptr()),
+            x.shape[0], int(inverse), None)
+    assert st == 0, st
+    torch.cuda.synchronize()
+    return yt.cpu().numpy()
+for n in [int(v) for v in os.environ["DEV_N"].split()]:
+    if os.environ["DEV_FN"].endswith("wave"):
+        m = 1 << (2 * n - 2).bit_length()  # bluestein.go:70
+        assert lib.gdsp_dev_chirpz_wave_q(n) == m // 2048, n
     rng = np.random.default_rng(9000 + n)
-    for batch in (1, 5):
+    for batch in (1, 5, 7):
         x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
-        xt = torch.from_numpy(x).cuda()
-        e = row_nrel(D.fft_batch(xt, chirpz=True).cpu().numpy(), oracle.fft_rows(x))
-        ei = row_nrel(D.fft_batch(xt, inverse=True, chirpz=True).cpu().numpy(), oracle.ifft_rows(x))
+        e = row_nrel(run(x, False), oracle.fft_rows(x))
+        ei = row_nrel(run(x, True), oracle.ifft_rows(x))
         assert e < 1e-9 and ei < 1e-9, (n, batch, e, ei)
-    # the default plan of the same length takes the wave kernel too when it is chirp-z
-    if D.plan(n).kind == 3:
-        assert D.plan(n).wave_q == m // 2048, n
 print("ok")
 '''
-    env = dict(os.environ, REPO=REPO, GDSP_BLU_WAVE="1", WAVE_N=" ".join(map(str, WAVE_N)),
-               GDSP_LIB=_dev_lib())
+
+
+def _run_dev(code, **env):
+    env = dict(os.environ, REPO=REPO, GDSP_LIB=_dev_lib(), **env)
     r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_chirpz_wave_kernel():
+    _run_dev(_DEV_CHIRPZ, DEV_FN="gdsp_dev_fft_batch_chirpz_wave", DEV_N=" ".join(map(str, WAVE_N)))
 
 
 SHFL_N = [2049, 2500, 3000, 3001, 4095, 4096]
@@ -909,64 +920,38 @@ SHFL_N = [2049, 2500, 3000, 3001, 4095, 4096]
 
 def test_chirpz_shuffle_kernel():
     """The M = 8192 chirp-z kernel whose FFTs keep one exchange inside the
-    wave (bluestein_shfl.hip, opt-in GDSP_BLU_SHFL=1) against the oracle:
-    forward and inverse, batch 1 and a ragged 7, over 2049 <= n <= 4096."""
-    code = r'''
-import importlib, os, sys
-sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
-import numpy as np, oracle, torch
-D = importlib.import_module("go-dsp_amd.device")
-def row_nrel(a, b):
-    return max(np.linalg.norm(x - y) / np.linalg.norm(y) for x, y in zip(a, b))
-for n in [int(v) for v in os.environ["SHFL_N"].split()]:
-    p = D.plan(n, chirpz=True)
-    assert p.kind == 3 and p.m == 8192 and p.shfl == 1, (n, p.kind, p.m, p.shfl)
-    rng = np.random.default_rng(7000 + n)
-    for batch in (1, 7):
-        x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
-        xt = torch.from_numpy(x).cuda()
-        e = row_nrel(D.fft_batch(xt, chirpz=True).cpu().numpy(), oracle.fft_rows(x))
-        ei = row_nrel(D.fft_batch(xt, inverse=True, chirpz=True).cpu().numpy(), oracle.ifft_rows(x))
-        assert e < 1e-9 and ei < 1e-9, (n, batch, e, ei)
-print("ok")
-'''
-    env = dict(os.environ, REPO=REPO, GDSP_BLU_SHFL="1", SHFL_N=" ".join(map(str, SHFL_N)),
-               GDSP_LIB=_dev_lib())
-    r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, env=env)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+    wave (bluestein_shfl.hip, development build) against the oracle: forward
+    and inverse, batch 1 and ragged 5 / 7, over 2049 <= n <= 4096."""
+    _run_dev(_DEV_CHIRPZ, DEV_FN="gdsp_dev_fft_batch_chirpz_shfl", DEV_N=" ".join(map(str, SHFL_N)))
 
 
 def test_pwelch_shuffle_kernel():
     """The NFFT 4096 / 50 % Pwelch kernel with the in-wave second exchange
-    (pwelch_shfl.hip, opt-in GDSP_PW_SHFL=1: DPP row shifts and
-    v_permlane16/32_swap) against the oracle: even and odd segment counts,
-    a one-pair call, and Hann / Hamming windows."""
+    (pwelch_shfl.hip, development build: DPP row shifts and
+    v_permlane16/32_swap) against the oracle: even and odd segment counts, a
+    one-pair call, and Hann / Hamming windows."""
     code = r'''
-import importlib, os, sys
+import ctypes, importlib, os, sys
 sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
-import numpy as np, oracle
+import numpy as np, oracle, torch
 g = importlib.import_module("go-dsp_amd")
+L = g._lib.lib()
+P = lambda t: ctypes.c_void_p(t.data_ptr())
 for n, win in ((40960, "hann"), (38913, "hann"), (6144, "hann"), (100000, "hamming"), (8192, "hann")):
     x = np.random.default_rng(n).standard_normal(n)
-    w = getattr(g.window, win.capitalize())
-    o = g.spectral.PwelchOptions(NFFT=4096, Noverlap=2048, Window=w)
-    p, f = g.spectral.Pwelch(x, 2.0, o)
+    w = getattr(g.window, win.capitalize())(4096)
+    S = g.spectral.segment_count(n, 4096, 2048)
+    xt = torch.from_numpy(x).cuda()
+    wt = torch.tensor(np.asarray(w, np.float64)).cuda()
+    acc = torch.zeros(4096, dtype=torch.float64, device="cuda")
+    assert L.gdsp_dev_pwelch4096_shfl_accumulate(P(xt), n, 0, S, P(wt), P(acc), None) == 0
+    p, f = g.spectral.finalize(acc.cpu().numpy(), S, 4096, 4096, np.asarray(w), 2.0, False)
     pr, fr = oracle.pwelch(x, 2.0, nfft=4096, noverlap=2048, window_kind=win)
     e = np.linalg.norm(p - pr) / np.linalg.norm(pr)
     assert e < 1e-9, (n, win, e)
 print("ok")
 '''
-    env = dict(os.environ, REPO=REPO, GDSP_PW_SHFL="1", GDSP_LIB=_dev_lib())
-    r = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, env=env)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
-
-
-def test_chirpz_block_kernel_default(gdsp):
-    """Without GDSP_BLU_WAVE=1 the fused chirp-z plans run the block-wide
-    bluestein_kernel (the faster of the two, DESIGN.md §3)."""
-    D = __import__("importlib").import_module("go-dsp_amd.device")
-    for n in (1009, 3000):
-        assert D.plan(n, chirpz=True).wave_q == 0
+    _run_dev(code)
 
 
 @pytest.mark.gpu
