@@ -38,12 +38,20 @@ __global__ __launch_bounds__(64 * kPwWaves) void pwelch_wave_kernel(
   static_assert(E == 16 && T <= 64 && 64 % T == 0, "one transform inside one wave");
   constexpr int S = 64 / T;          // transforms (pairs) per wave
   constexpr int XS = G::STRIDE;      // exchange doubles per transform
-  __shared__ double lds[kPwWaves * S * XS + F];
+  // LDS: the exchange regions, the window, and the twiddle table T_F (the
+  // passes' twiddle bases come from LDS, so the samples in flight are the
+  // loop's only global loads: a global twiddle read's wait, vmcnt being in
+  // order, would also wait for the next group's samples)
+  __shared__ double lds[kPwWaves * S * XS + F + 2 * F];
   const int lt = (int)threadIdx.x;
   const int w = lt >> 6, lane = lt & 63, s = lane / T, t = lane % T;
   double *const lre = lds + (w * S + s) * XS;
   double *const wl = lds + kPwWaves * S * XS;
-  for (int i = lt; i < F; i += 64 * kPwWaves) wl[i] = win[i];
+  cd *const twl = reinterpret_cast<cd *>(wl + F);
+  for (int i = lt; i < F; i += 64 * kPwWaves) {
+    wl[i] = win[i];
+    twl[i] = tw[i];
+  }
   __syncthreads();
   // the worker (wave) and its group range: wave-uniform
   const int64_t wave = (int64_t)blockIdx.x * kPwWaves + __builtin_amdgcn_readfirstlane(w);
@@ -58,22 +66,33 @@ __global__ __launch_bounds__(64 * kPwWaves) void pwelch_wave_kernel(
   // b[k] = segment s0 + 1's (HALF: b[k] = a[k + H] for k < H, so only b[H..E)
   // is loaded); zero past the signal's segments and past nfft (Pad > NFFT)
   constexpr int NB = HALF ? H : E;
-  auto load = [&](int64_t g, double (&a)[E], double (&b)[NB]) {
+  // Every load is unconditional, from a clamped address (a slot past the
+  // pairs reads the last pair, a missing partner reads segment s0 again,
+  // elements past nfft read element nfft - 1), and the mask is applied where
+  // the samples are used, not where they are loaded: a load inside a per-lane
+  // branch is waited for inside that branch (s_waitcnt vmcnt(0) per element,
+  // serialising them all), and a select right after a prefetch waits for it.
+  auto seg0 = [&](int64_t g, bool &active, bool &has1) {
     const int64_t p = g * S + s;
-    const bool active = g < gend && p < npairs;
-    const int64_t s0 = seg_begin + 2 * (active ? p : 0);
-    const bool has1 = active && s0 + 1 < seg_end;
+    active = g < gend && p < npairs;
+    const int64_t s0 = seg_begin + 2 * (active ? p : npairs - 1);
+    has1 = active && s0 + 1 < seg_end;
+    return s0;
+  };
+  auto load = [&](int64_t g, double (&a)[E], double (&b)[NB]) {
+    bool active, has1;
+    const int64_t s0 = seg0(g, active, has1);
     const double *xa = opaque_ptr(x) + s0 * stride;
-    const double *xb = xa + stride;
+    const double *xb = has1 ? xa + stride : xa;
 #pragma unroll
     for (int k = 0; k < E; ++k) {
       const int i = t + k * T;
-      a[k] = (active && (HALF || i < nfft)) ? xa[i] : 0.0;
+      a[k] = xa[HALF || i < nfft ? i : nfft - 1];
     }
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
       const int i = t + (HALF ? k + H : k) * T;
-      b[k] = (has1 && (HALF || i < nfft)) ? xb[i] : 0.0;
+      b[k] = xb[HALF || i < nfft ? i : nfft - 1];
     }
   };
   double na[E], nb[NB];
@@ -89,20 +108,23 @@ __global__ __launch_bounds__(64 * kPwWaves) void pwelch_wave_kernel(
     } else {
       load(g, a, b);
     }
-    const int64_t p = g * S + s;
-    const bool active = p < npairs;
-    // (HALF: a partnerless last pair, odd segment count, takes zeros for its
-    // second segment's first half too, not segment s0's second half)
-    const bool has1 = active && seg_begin + 2 * p + 1 < seg_end;
+    bool active, has1;
+    (void)seg0(g, active, has1);
     const int tt = opaque_int(t);
     cd v[E];
 #pragma unroll
     for (int k = 0; k < E; ++k) {
+      // (HALF: a partnerless last pair, odd segment count, takes zeros for
+      // its second segment's first half too, not segment s0's second half)
+      const int i = t + k * T;
+      const bool ina = active && (HALF || i < nfft);
+      const bool inb = has1 && (HALF || i < nfft);
       const double wk = wl[tt + k * T];
-      const double bk = HALF ? (k < H ? (has1 ? a[k + H] : 0.0) : b[k - H]) : b[k];
-      v[k] = {a[k] * wk, bk * wk};
+      const double ak = ina ? a[k] : 0.0;
+      const double bk = inb ? (HALF ? (k < H ? a[k + H] : b[k - H]) : b[k]) : 0.0;
+      v[k] = {ak * wk, bk * wk};
     }
-    fft_regs<LOG2F, true, 1, 4, 0, 0, const cd *, 0, 0, NoEpi, 0, 16, true>(v, tt, tw, lre, lre,
+    fft_regs<LOG2F, true, 2, 4, 0, 0, const cd *, 0, 0, NoEpi, 0, 16, true>(v, tt, twl, lre, lre,
                                                                            g == g0);
     if (active) {
 #pragma unroll
