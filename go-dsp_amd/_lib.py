@@ -98,6 +98,7 @@ DEV_SIGNATURES = {
     "gdsp_dev_fft_batch_chirpz_wave": (_I, [_I64, _P, _P, _I64, _I, _P]),
     "gdsp_dev_fft_batch_chirpz_shfl": (_I, [_I64, _P, _P, _I64, _I, _P]),
     "gdsp_dev_pwelch4096_shfl_accumulate": (_I, [_P, _I64, _I64, _I64, _P, _P, _P]),
+    "gdsp_dev_pwelch4096_row3_accumulate": (_I, [_P, _I64, _I64, _I64, _P, _P, _P]),
 }
 
 _lib = None

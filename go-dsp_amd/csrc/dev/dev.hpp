@@ -27,4 +27,10 @@ hipError_t launch_pwelch4096_shfl(const double *x, int64_t seg_begin, int64_t se
                                   int64_t nworkers, const double *win, const cd *tw,
                                   double *partial, hipStream_t s);
 
+// the row kernel reshaped for three workgroups per CU (pwelch_row3.hip):
+// LDS-DMA stage, half-size exchange; same arguments as launch_pwelch_half(12)
+hipError_t launch_pwelch4096_row3(const double *x, int64_t seg_begin, int64_t seg_end, int64_t ppw,
+                                  int64_t nworkers, const double *win, const cd *tw,
+                                  double *partial, hipStream_t s);
+
 }  // namespace gdsp

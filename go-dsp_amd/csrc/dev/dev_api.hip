@@ -176,10 +176,12 @@ int gdsp_dev_fft_batch_chirpz_shfl(int64_t n, const void *d_in, void *d_out, int
              : GDSP_ERR_HIP;
 }
 
-int gdsp_dev_pwelch4096_shfl_accumulate(const double *d_x, int64_t n, int64_t seg_begin,
-                                        int64_t seg_end, const double *d_win, double *d_acc,
-                                        void *stream) {
-  // the product's half-overlap geometry (gdsp_pwelch_accumulate_device)
+// the half-overlap NFFT 4096 accumulation of gdsp_pwelch_accumulate_device
+// on one of the rejected kernels (same worker geometry: 2048 workers)
+static int pw4096_dev(hipError_t (*launch)(const double *, int64_t, int64_t, int64_t, int64_t,
+                                           const double *, const cd *, double *, hipStream_t),
+                      const double *d_x, int64_t n, int64_t seg_begin, int64_t seg_end,
+                      const double *d_win, double *d_acc, void *stream) {
   if (!d_x || !d_win || !d_acc || seg_begin < 0 || seg_end < seg_begin ||
       (seg_end > seg_begin && (seg_end - 1) * 2048 + 4096 > n))
     return GDSP_ERR_INVALID;
@@ -199,13 +201,26 @@ int gdsp_dev_pwelch4096_shfl_accumulate(const double *d_x, int64_t n, int64_t se
   DCHK(hipMalloc((void **)&part, (size_t)nworkers * 4096 * sizeof(double)));
   DCHK(hipMalloc((void **)&red,
                  (size_t)gdsp::reduce_scratch_doubles(nworkers, 4096) * sizeof(double)));
-  hipError_t e = gdsp::launch_pwelch4096_shfl(d_x, seg_begin, seg_end, ppw, nworkers, d_win, tw,
-                                              part, s);
+  hipError_t e = launch(d_x, seg_begin, seg_end, ppw, nworkers, d_win, tw, part, s);
   if (e == hipSuccess) e = gdsp::launch_reduce_partials(part, nworkers, 4096, d_acc, red, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   (void)hipFree(part);
   (void)hipFree(red);
   return e == hipSuccess ? GDSP_OK : GDSP_ERR_HIP;
+}
+
+int gdsp_dev_pwelch4096_shfl_accumulate(const double *d_x, int64_t n, int64_t seg_begin,
+                                        int64_t seg_end, const double *d_win, double *d_acc,
+                                        void *stream) {
+  return pw4096_dev(gdsp::launch_pwelch4096_shfl, d_x, n, seg_begin, seg_end, d_win, d_acc,
+                    stream);
+}
+
+int gdsp_dev_pwelch4096_row3_accumulate(const double *d_x, int64_t n, int64_t seg_begin,
+                                        int64_t seg_end, const double *d_win, double *d_acc,
+                                        void *stream) {
+  return pw4096_dev(gdsp::launch_pwelch4096_row3, d_x, n, seg_begin, seg_end, d_win, d_acc,
+                    stream);
 }
 
 }  // extern "C"

@@ -24,37 +24,50 @@
 namespace gdsp {
 
 constexpr int kPwWaves = 4;  // waves per workgroup
-#ifndef GDSP_PWW_PF
-#define GDSP_PWW_PF 1
-#endif
+
+// Workers: with T <= 64 a wave (S = 64 / T transforms side by side, four
+// waves per workgroup, wave-synchronised exchanges); with T = 128 (F = 2048)
+// a two-wave workgroup of one transform, whose barriers meet only its own two
+// waves (pwelch_half_kernel's 256-thread workgroups meet four).
+template <int LOG2F>
+struct PwwGeo {
+  using G = Geo<LOG2F>;
+  static constexpr int T = G::T;
+  static constexpr bool WAVE = T <= 64;
+  static constexpr int S = WAVE ? 64 / T : 1;       // transforms (pairs) per worker
+  static constexpr int WPB = WAVE ? kPwWaves : 1;   // workers per workgroup
+  static constexpr int BLOCK = WAVE ? 64 * kPwWaves : T;
+  // twiddle bases the passes read: T_F[k], k < F / (last radix)
+  static constexpr int TWN = G::N / G::radix(G::NPASS - 1);
+};
 
 template <int LOG2F, bool HALF, bool PF>
-__global__ __launch_bounds__(64 * kPwWaves) void pwelch_wave_kernel(
+__global__ __launch_bounds__((PwwGeo<LOG2F>::BLOCK)) void pwelch_wave_kernel(
     const double *__restrict__ x, int64_t nfft, int64_t stride, int64_t seg_begin,
     int64_t seg_end, int64_t groups_per_wave, const double *__restrict__ win,
     const cd *__restrict__ tw, double *__restrict__ partial) {
   using G = Geo<LOG2F>;
+  using W = PwwGeo<LOG2F>;
   constexpr int E = G::E, T = G::T, F = G::N, H = E / 2;
-  static_assert(E == 16 && T <= 64 && 64 % T == 0, "one transform inside one wave");
-  constexpr int S = 64 / T;          // transforms (pairs) per wave
-  constexpr int XS = G::STRIDE;      // exchange doubles per transform
-  // LDS: the exchange regions, the window, and the twiddle table T_F (the
-  // passes' twiddle bases come from LDS, so the samples in flight are the
-  // loop's only global loads: a global twiddle read's wait, vmcnt being in
-  // order, would also wait for the next group's samples)
-  __shared__ double lds[kPwWaves * S * XS + F + 2 * F];
+  static_assert(E == 16 && (T <= 64 ? 64 % T == 0 : T == 128), "one transform per wave or two waves");
+  constexpr int S = W::S;
+  constexpr int XS = G::STRIDE;  // exchange doubles per transform
+  // LDS: the exchange regions, the window, and the twiddle bases (from LDS,
+  // so the samples in flight are the loop's only global loads: a global
+  // twiddle read's wait, vmcnt being in order, would also wait for the next
+  // group's samples)
+  __shared__ double lds[W::WPB * S * XS + F + 2 * W::TWN];
   const int lt = (int)threadIdx.x;
-  const int w = lt >> 6, lane = lt & 63, s = lane / T, t = lane % T;
+  const int w = W::WAVE ? lt >> 6 : 0, lane = W::WAVE ? lt & 63 : lt;
+  const int s = lane / T, t = lane % T;
   double *const lre = lds + (w * S + s) * XS;
-  double *const wl = lds + kPwWaves * S * XS;
+  double *const wl = lds + W::WPB * S * XS;
   cd *const twl = reinterpret_cast<cd *>(wl + F);
-  for (int i = lt; i < F; i += 64 * kPwWaves) {
-    wl[i] = win[i];
-    twl[i] = tw[i];
-  }
+  for (int i = lt; i < F; i += W::BLOCK) wl[i] = win[i];
+  for (int i = lt; i < W::TWN; i += W::BLOCK) twl[i] = tw[i];
   __syncthreads();
-  // the worker (wave) and its group range: wave-uniform
-  const int64_t wave = (int64_t)blockIdx.x * kPwWaves + __builtin_amdgcn_readfirstlane(w);
+  // the worker and its group range: uniform over its waves
+  const int64_t wave = (int64_t)blockIdx.x * W::WPB + __builtin_amdgcn_readfirstlane(w);
   const int64_t npairs = (seg_end - seg_begin + 1) / 2;
   const int64_t ngroups = (npairs + S - 1) / S;
   const int64_t g0 = wave * groups_per_wave;
@@ -124,8 +137,8 @@ __global__ __launch_bounds__(64 * kPwWaves) void pwelch_wave_kernel(
       const double bk = inb ? (HALF ? (k < H ? a[k + H] : b[k - H]) : b[k]) : 0.0;
       v[k] = {ak * wk, bk * wk};
     }
-    fft_regs<LOG2F, true, 2, 4, 0, 0, const cd *, 0, 0, NoEpi, 0, 16, true>(v, tt, twl, lre, lre,
-                                                                           g == g0);
+    fft_regs<LOG2F, true, 2, 4, 0, 0, const cd *, 0, 0, NoEpi, 0, 16, W::WAVE>(v, tt, twl, lre,
+                                                                              lre, g == g0);
     if (active) {
 #pragma unroll
       for (int k = 0; k < E; ++k) acc[k] = fma(v[k].y, v[k].y, fma(v[k].x, v[k].x, acc[k]));
@@ -143,27 +156,30 @@ static hipError_t launch_pww_t(const double *x, int64_t nfft, int64_t stride, in
                                int64_t seg_end, int64_t gpw, int64_t nblk, const double *win,
                                const cd *tw, double *partial, hipStream_t s) {
   hipLaunchKernelGGL((pwelch_wave_kernel<LOG2F, HALF, PF>), dim3((unsigned)nblk),
-                     dim3(64 * kPwWaves), 0, s, x, nfft, stride, seg_begin, seg_end, gpw, win, tw,
-                     partial);
+                     dim3(PwwGeo<LOG2F>::BLOCK), 0, s, x, nfft, stride, seg_begin, seg_end, gpw,
+                     win, tw, partial);
   return hipGetLastError();
 }
 
-// Geometry of a launch: pairs per group S = 64 / T (T = F / 16), groups per
-// wave, workgroups, and the partial rows the reduce sums (one per slot).
-bool pwelch_wave_applies(int log2f) { return log2f >= 6 && log2f <= 10; }
+// Geometry of a launch: pairs per group (S), groups per worker, workgroups,
+// and the partial rows the reduce sums (one per transform slot).
+bool pwelch_wave_applies(int log2f) { return log2f >= 6 && log2f <= 11; }
 
 void pwelch_wave_geometry(int log2f, int64_t nsegs, int64_t *gpw, int64_t *nblk,
                           int64_t *nrows) {
-  const int S = 64 / ((1 << log2f) / 16);
+  const int T = (1 << log2f) / 16;
+  const bool wave = T <= 64;
+  const int S = wave ? 64 / T : 1, wpb = wave ? kPwWaves : 1;
   const int64_t npairs = (nsegs + 1) / 2;
   const int64_t ngroups = (npairs + S - 1) / S;
-  // about 2048 waves (8 per CU: two per SIMD, the kernel's register budget)
-  const int64_t target = 2048;
+  // about 2048 waves in all (8 per CU: two per SIMD, the kernel's register
+  // budget): 2048 one-wave workers, or 1024 two-wave ones
+  const int64_t target = wave ? 2048 : 1024;
   const int64_t g = ngroups < 1 ? 1 : (ngroups + target - 1) / target;
-  const int64_t waves = ngroups < 1 ? 1 : (ngroups + g - 1) / g;
+  const int64_t workers = ngroups < 1 ? 1 : (ngroups + g - 1) / g;
   *gpw = g;
-  *nblk = (waves + kPwWaves - 1) / kPwWaves;
-  *nrows = *nblk * kPwWaves * S;
+  *nblk = (workers + wpb - 1) / wpb;
+  *nrows = *nblk * wpb * S;
 }
 
 hipError_t launch_pwelch_wave(int log2f, bool half, const double *x, int64_t nfft, int64_t stride,
@@ -171,13 +187,18 @@ hipError_t launch_pwelch_wave(int log2f, bool half, const double *x, int64_t nff
                               const double *win, const cd *tw, double *partial, hipStream_t s) {
   if (nblk < 1 || nblk > 0x7fffffff) return hipErrorInvalidValue;
   switch (log2f) {
-#define GDSP_PWW(L)                                                                               \
-  case L:                                                                                       \
-    return half ? launch_pww_t<L, true, GDSP_PWW_PF>(x, nfft, stride, seg_begin, seg_end, gpw,  \
-                                                     nblk, win, tw, partial, s)                 \
-                : launch_pww_t<L, false, GDSP_PWW_PF>(x, nfft, stride, seg_begin, seg_end, gpw, \
-                                                      nblk, win, tw, partial, s);
-    GDSP_PWW(6) GDSP_PWW(7) GDSP_PWW(8) GDSP_PWW(9) GDSP_PWW(10)
+// PF for the half-overlap case only: there it measured 0.571 against 0.58
+// ms (256 / 128), 0.664 against 0.69 (1024 / 512) and 0.53 against 0.56 (64 /
+// 32) per 2^28 samples; without overlap all 32 samples of a pair are new and
+// the prefetch costs more registers than it hides (1024 / 0: 0.454 against
+// 0.43 ms; at F = 2048 it leaves one wave per SIMD)
+#define GDSP_PWW(L)                                                                           \
+  case L:                                                                                   \
+    return half ? launch_pww_t<L, true, true>(x, nfft, stride, seg_begin, seg_end, gpw, nblk, \
+                                              win, tw, partial, s)                          \
+                : launch_pww_t<L, false, false>(x, nfft, stride, seg_begin, seg_end, gpw,     \
+                                                nblk, win, tw, partial, s);
+    GDSP_PWW(6) GDSP_PWW(7) GDSP_PWW(8) GDSP_PWW(9) GDSP_PWW(10) GDSP_PWW(11)
 #undef GDSP_PWW
     default: return hipErrorInvalidValue;
   }

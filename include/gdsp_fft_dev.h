@@ -37,6 +37,12 @@ int gdsp_dev_fft_batch_chirpz_shfl(int64_t n, const void *d_in, void *d_out, int
 int gdsp_dev_pwelch4096_shfl_accumulate(const double *d_x, int64_t n, int64_t seg_begin,
                                         int64_t seg_end, const double *d_win, double *d_acc,
                                         void *stream);
+/* The same on the row kernel reshaped for three workgroups per CU
+ * (pwelch_row3.hip: the next pair by LDS-DMA, a half-size exchange buffer,
+ * 168 VGPRs of which 42 spill). */
+int gdsp_dev_pwelch4096_row3_accumulate(const double *d_x, int64_t n, int64_t seg_begin,
+                                        int64_t seg_end, const double *d_win, double *d_acc,
+                                        void *stream);
 
 #ifdef __cplusplus
 }

@@ -930,7 +930,10 @@ def test_pwelch_shuffle_kernel():
     (pwelch_shfl.hip, development build: DPP row shifts and
     v_permlane16/32_swap) against the oracle: even and odd segment counts, a
     one-pair call, and Hann / Hamming windows."""
-    code = r'''
+    _run_dev(_PW_DEV, DEV_FN="gdsp_dev_pwelch4096_shfl_accumulate")
+
+
+_PW_DEV = r'''
 import ctypes, importlib, os, sys
 sys.path.insert(0, os.environ["REPO"]); sys.path.insert(0, os.path.join(os.environ["REPO"], "oracle"))
 import numpy as np, oracle, torch
@@ -944,14 +947,21 @@ for n, win in ((40960, "hann"), (38913, "hann"), (6144, "hann"), (100000, "hammi
     xt = torch.from_numpy(x).cuda()
     wt = torch.tensor(np.asarray(w, np.float64)).cuda()
     acc = torch.zeros(4096, dtype=torch.float64, device="cuda")
-    assert L.gdsp_dev_pwelch4096_shfl_accumulate(P(xt), n, 0, S, P(wt), P(acc), None) == 0
+    assert getattr(L, os.environ["DEV_FN"])(P(xt), n, 0, S, P(wt), P(acc), None) == 0
     p, f = g.spectral.finalize(acc.cpu().numpy(), S, 4096, 4096, np.asarray(w), 2.0, False)
     pr, fr = oracle.pwelch(x, 2.0, nfft=4096, noverlap=2048, window_kind=win)
     e = np.linalg.norm(p - pr) / np.linalg.norm(pr)
     assert e < 1e-9, (n, win, e)
 print("ok")
 '''
-    _run_dev(code)
+
+
+def test_pwelch_three_wave_kernel():
+    """The NFFT 4096 / 50 % row kernel reshaped for three workgroups per CU
+    (pwelch_row3.hip, development build: the next pair by LDS-DMA, a half-size
+    exchange, 42 spilled VGPRs at the 168-VGPR cap) against the oracle, on the
+    same cases as the shuffle kernel."""
+    _run_dev(_PW_DEV, DEV_FN="gdsp_dev_pwelch4096_row3_accumulate")
 
 
 @pytest.mark.gpu
