@@ -91,8 +91,8 @@ __device__ __forceinline__ void r3_dma(const double *x, int64_t seg_begin, int64
   for (int i = 0; i < 8; ++i) {
     const int piece = w + 4 * i;  // 1 KiB piece
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
-        r, (__attribute__((address_space(3))) void *)((char *)stage + piece * 1024), 16, lane16,
-        __builtin_amdgcn_readfirstlane(piece * 1024), 0, 0);
+        r, (__attribute__((address_space(3))) void *)((char *)stage + piece * 1024), 16,
+        (uint32_t)piece * 1024u + lane16, 0, 0, 0);  // (soffset is not range-checked)
   }
 }
 }  // namespace
