@@ -140,10 +140,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
     }
     bare_sync();  // every thread has read the stage
     if (p + 1 < pend) r3_dma(x, seg_begin, p + 1, p + 1 < nfull, stage, tt);
+    const bool partner = p < nfull;  // (else the second segment is zeros: c2 by the descriptor)
     cd v[kR3E];
 #pragma unroll
     for (int k = 0; k < kR3H; ++k) {
-      v[k] = {carry[k] * wv[k], a2[k] * wv[k]};
+      v[k] = {carry[k] * wv[k], partner ? a2[k] * wv[k] : 0.0};
       v[kR3H + k] = {a2[k] * wv[kR3H + k], c2[k] * wv[kR3H + k]};
       carry[k] = c2[k];
     }
