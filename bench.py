@@ -52,6 +52,7 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (tools/fp64peak.hip measures 
 SQ_KERNELS = {"radix4096": ["fft_lds_kernel<12"], "bluestein3000": ["fft_mixed_fixed_kernel"],
               "prime3001": ["rader_fixed_kernel"],
               "chirpz3000": ["chirpz6k_kernel"], "pwelch": ["pwelch_row_kernel<12"],
+              "pwelch_default": ["pwelch_wave_kernel<8"],
               "fft2_8192": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"],
               "fft2_dist": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"]}
 SQ_ROUNDS = ("r04", "r03", "r02")  # SQ counter passes quoted: the newest round that has the kernel
@@ -68,6 +69,7 @@ PROFILED_ALG_BYTES = {"radix4096": 32 * 4096 * 65536, "bluestein3000": 32 * 3000
                       "chirpz3000": 32 * 3000 * 65536, "prime3001": 32 * 3001 * 65536,
                       "fft2_8192": 4 * 16 * 8192 * 8192,
                       "fft2_dist": 4 * 16 * 8192 * 8192, "pwelch": 8 * (1 << 30),
+                      "pwelch_default": 8 * (1 << 30),
                       "fftn_512": 3 * 2 * 16 * 512 ** 3, "wav_decode": 10 * (1 << 30),
                       "fft_2p20": 32 * (1 << 20)}
 
@@ -92,11 +94,12 @@ def parse():
 
 
 WORKLOADS = ["radix4096", "bluestein3000", "chirpz3000", "prime3001", "fft2_8192", "fft2_dist",
-             "pwelch",
+             "pwelch", "pwelch_default",
              "fftn_512", "wav_decode", "fft_2p20", "fftreal1024"]
 # the BASELINE configs nested in the default line: configs[2] (production
 # dispatch and the reference's chirp-z algorithm), configs[3], configs[4]
-NESTED = ["bluestein3000", "chirpz3000", "prime3001", "fft2_8192", "pwelch", "fftreal1024"]
+NESTED = ["bluestein3000", "chirpz3000", "prime3001", "fft2_8192", "pwelch", "pwelch_default",
+          "fftreal1024"]
 HEADLINE_METRIC = "Gsamples/s + % HBM roofline, batched N=4096 complex128 FFT at 1/2/4/8 GPUs"
 
 
@@ -267,8 +270,12 @@ def setup(w: str, c: Ctx, weak: bool = False) -> dict:
                     cfg={"workload": "wav.ReadFloats PCM16 -> float64 Pwelch input, 2^30 "
                                      "samples (wav.go:135-161)", "samples": count,
                          "format": "PCM16", "parallelism": f"replicas{world}"})
-    # pwelch: 2^30 samples total, NFFT 4096, 50 % overlap, Hann (strong scaling)
-    nfft, nov = 4096, 2048
+    # pwelch: 2^30 samples total, NFFT 4096, 50 % overlap, Hann (strong
+    # scaling); pwelch_default: the same stream with the reference's
+    # PwelchOptions{} defaults, NFFT 256, Noverlap 0, Pad = NFFT, Hann
+    # (spectral/pwelch.go:85-95), what pwelch_test.go and every zero-valued
+    # options caller get
+    nfft, nov = (256, 0) if w == "pwelch_default" else (4096, 2048)
     total = 1 << 30
     sh = Dd.plan_pwelch(total, world, rank, nfft, 0, nov)
     x = torch.empty(sh.sample_hi - sh.sample_lo, dtype=torch.float64, device=dev)
@@ -279,6 +286,17 @@ def setup(w: str, c: Ctx, weak: bool = False) -> dict:
     def step():
         result["pxx"], _ = Dd.pwelch(x, 1.0, opts, sh, stream=stream)
 
+    if w == "pwelch_default":
+        return dict(step=step, x=x, shard=sh, opts=opts, result=result, total_samples=total,
+                    rank_samples=total // world,
+                    alg_bytes=8 * x.numel(), kernel="pwelch_wave_kernel<8, false, false>",
+                    metric="Gsamples/s, spectral.Pwelch 2^30 samples, PwelchOptions{} defaults "
+                           "(NFFT 256, Noverlap 0)",
+                    scaling="strong",
+                    cfg={"workload": "spectral.Pwelch 2^30-sample stream, the reference's "
+                                     "default options: Hann NFFT 256, Noverlap 0, Pad 256",
+                         "segments_total": sh.nsegs_total,
+                         "parallelism": f"segments{world}+allreduce"})
     return dict(step=step, x=x, shard=sh, opts=opts, result=result, total_samples=total,
                 rank_samples=total // world,
                 alg_bytes=8 * x.numel(), kernel="pwelch_row_kernel<12>",
@@ -368,7 +386,7 @@ def parity(w: str, wl: dict, c: Ctx):
         return {"samples": m, "bit_exact": bool(np.array_equal(got, ref.astype(np.float64)))}
     if w == "fft2_8192" and "y" in wl:
         return parity_fft2(wl, np, oracle)
-    if w == "pwelch":
+    if w in ("pwelch", "pwelch_default"):
         return parity_pwelch(wl, c, np, oracle)
     return None
 
@@ -1019,13 +1037,14 @@ def _cpu_baseline(workload: str, seconds: float, cores: int, pool: str, np, orac
                 "kind": "port", "us_per_call": round(dt / done * 1e6, 2),
                 "sample": f"{done} fft.FFTReal calls of N=1024 ({dt:.1f} s), one thread, "
                           f"called from Python (ctypes) like the GPU line"}
-    if workload == "pwelch":
+    if workload in ("pwelch", "pwelch_default"):
+        nfft, nov = (256, 0) if workload == "pwelch_default" else (4096, 2048)
         n = 1 << 20
         t0 = time.perf_counter()
         while True:
             x = oracle.fill_uniform(n, SEED)
             t1 = time.perf_counter()
-            oracle.pwelch_threaded(x, 1.0, 4096, 2048, cores)
+            oracle.pwelch_threaded(x, 1.0, nfft, nov, cores)
             dt = time.perf_counter() - t1
             if dt > seconds / 3 or time.perf_counter() - t0 > seconds:
                 break
@@ -1033,7 +1052,7 @@ def _cpu_baseline(workload: str, seconds: float, cores: int, pool: str, np, orac
         return {"value": round(n / dt / 1e9, 6), "unit": "Gsamples/s", "cores": cores,
                 "kind": "port",
                 "sample": f"spectral.Pwelch on a {n}-sample prefix of the stream "
-                          f"(NFFT 4096, 50% overlap, {dt:.1f} s), {pool}"}
+                          f"(NFFT {nfft}, Noverlap {nov}, {dt:.1f} s), {pool}"}
     if workload == "wav_decode":
         # wav.ReadFloats's conversion restated (oracle/oracle.c), one thread
         raw = oracle.fill_uniform(1 << 21, SEED).view(np.uint8)

@@ -722,6 +722,12 @@ int64_t primitive_root(int64_t p) {
 bool rader_radices(int64_t N, std::vector<int> &rad) {
   rad.clear();
   if (N < 2 || N > gdsp::kMixedSpecMax) return false;
+#ifdef GDSP_RADER_3000  // (temporary A/B of radix lists for N = 3000)
+  if (N == 3000) {
+    rad = {GDSP_RADER_3000};
+    return true;
+  }
+#endif
   if (is_pow2(N)) {
     int a = ilog2(N);
     while (a >= 4) {
@@ -1963,7 +1969,6 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
   gdsp_plan *p = nullptr;
   STCHK(get_plan(flen, &p));
   const int64_t nseg = seg_end - seg_begin;
-#ifndef GDSP_PWW_OFF
   if (p->kind == KIND_LDS && gdsp::pwelch_wave_applies(p->log2n)) {
     // 64 <= F <= 1024: wave-resident transforms, no workgroup barriers
     // (pwelch_wave.hip), every wave a persistent worker over pair groups
@@ -1980,7 +1985,6 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
                                         (double *)red.p, s));
     return GDSP_OK;
   }
-#endif
   if (p->kind == KIND_LDS && p->log2n >= 4) {
     // fused path: packed segment pairs, persistent workers over contiguous
     // pair ranges (the 50 % overlap of consecutive pairs is re-read from L2)
