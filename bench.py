@@ -55,11 +55,11 @@ SQ_KERNELS = {"radix4096": ["fft_lds_kernel<12"], "bluestein3000": ["fft_mixed_f
               "pwelch_default": ["pwelch_wave_kernel<8"],
               "fft2_8192": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"],
               "fft2_dist": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"]}
-SQ_ROUNDS = ("r04", "r03", "r02")  # SQ counter passes quoted: the newest round that has the kernel
+SQ_ROUNDS = ("r05", "r04", "r03", "r02")  # SQ counter passes quoted: the newest round that has the kernel
 # rocprofv3 --kernel-trace --stats summaries quoted beside the event timing
 # (profiles/<round>/<workload>_kernel_stats.csv, the closing session's runs of
 # `bench.py --workload <w>`): the newest round that has the workload
-STATS_ROUNDS = ("r04", "r03", "r02")
+STATS_ROUNDS = ("r05", "r04", "r03", "r02")
 SEED = 0x5EED
 WARM_S = 0.06  # untimed GPU work before the timed steps (steady clocks; measure())
 # algorithmic bytes of one launch in the N=1 full-size configuration the

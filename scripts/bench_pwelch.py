@@ -14,8 +14,9 @@ gdsp = importlib.import_module("go-dsp_amd")
 D = importlib.import_module("go-dsp_amd.device")
 Dd = importlib.import_module("go-dsp_amd.distributed")
 
-CASES = [(256, 0), (256, 128), (1024, 512), (4096, 0), (4096, 2048), (16384, 8192), (1000, 500),
-         (3000, 1500), (4096, 1024)]
+CASES = [(64, 32), (128, 0), (256, 0), (256, 128), (512, 256), (1024, 0), (1024, 512), (2048, 0),
+         (2048, 1024), (4096, 0), (4096, 2048), (4096, 1024), (8192, 4096), (16384, 8192),
+         (1000, 500), (3000, 1500)]
 
 if __name__ == "__main__":
     torch.cuda.set_device(0)

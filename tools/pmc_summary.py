@@ -15,6 +15,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {"radix4096": "fft_lds_kernel<12", "bluestein3000": "fft_mixed_fixed_kernel",
            "chirpz3000": "chirpz6k_kernel",
            "pwelch": "pwelch_row_kernel<12",
+           "pwelch_default": "pwelch_wave_kernel<8",
+           "prime3001": "rader_fixed_kernel",
            # one FFT2 step = row pass + the two column-tile launches: summed
            "fft2_8192": ["fft_lds_kernel<13", "colfft_tile_kernel<7", "colfft_tile_kernel<6"],
            # one FFTN step = the row pass + two column-tile axes
