@@ -71,6 +71,13 @@ __device__ __forceinline__ double buf_ld1(rsrc_t r, uint32_t off) {
   __builtin_memcpy(&v, &q, sizeof(double));
   return v;
 }
+// soff: a wave-uniform byte offset (SGPR) added outside the range check
+__device__ __forceinline__ double buf_ld1s(rsrc_t r, uint32_t off, int soff) {
+  const auto q = __builtin_amdgcn_raw_buffer_load_b64(r, off, soff, 0);
+  double v;
+  __builtin_memcpy(&v, &q, sizeof(double));
+  return v;
+}
 // nontemporal store (aux bit 1: nt)
 __device__ __forceinline__ void buf_st_nt(rsrc_t r, uint32_t off, cd v) {
   decltype(__builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 0)) q;

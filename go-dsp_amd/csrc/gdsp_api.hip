@@ -756,6 +756,11 @@ int rader_try(int dev, int64_t n, gdsp_plan *p, bool *built) {
   const int64_t N = n - 1;
   std::vector<int> rad;
   if (!rader_radices(N, rad)) return GDSP_OK;
+  // a radix-29 or -31 pass (dft_odd's long constant tables) costs more than
+  // the chirp-z it would replace: 2729 (2728 = 8 11 31) 1.82 against 1.74 ms
+  // per 2^27 samples (profiles/r05/rader_sweep.jsonl)
+  for (int r : rad)
+    if (r > 25) return GDSP_OK;
   gdsp::JitRader *j = gdsp::jit_rader_build(dev, rad.data(), (int)rad.size());
   if (!j) return GDSP_OK;
   gdsp_plan *pn = nullptr;  // FFT_N for bhat
@@ -1968,14 +1973,15 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
   const int64_t nseg = seg_end - seg_begin;
   if (p->kind == KIND_LDS && gdsp::pwelch_wave_applies(p->log2n)) {
     // 64 <= F <= 1024: wave-resident transforms, no workgroup barriers
-    // (pwelch_wave.hip), every wave a persistent worker over pair groups
+    // (pwelch_wave.hip), every wave a persistent worker over pair groups;
+    // F = 2048: two-wave workgroups
+    const bool half = 2 * noverlap == nfft && flen == nfft;
     int64_t gpw = 0, nblk = 0, nrows = 0;
-    gdsp::pwelch_wave_geometry(p->log2n, nseg, &gpw, &nblk, &nrows);
+    gdsp::pwelch_wave_geometry(p->log2n, half, nseg, &gpw, &nblk, &nrows);
     DevBuf part, red;
     STCHK(part.alloc((size_t)nrows * (size_t)flen * sizeof(double), s, SLOT_PW_PART));
     STCHK(red.alloc((size_t)gdsp::reduce_scratch_doubles(nrows, flen) * sizeof(double), s,
                     SLOT_PW_RED));
-    const bool half = 2 * noverlap == nfft && flen == nfft;
     HIPCHK(gdsp::launch_pwelch_wave(p->log2n, half, d_x, nfft, stride, seg_begin, seg_end, gpw,
                                     nblk, d_win_seg, p->tw, (double *)part.p, s));
     HIPCHK(gdsp::launch_reduce_partials((const double *)part.p, nrows, flen, d_acc,
@@ -2001,6 +2007,10 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
       // half overlap: each sample loaded once, window in LDS
       HIPCHK(gdsp::launch_pwelch_half(p->log2n, d_x, seg_begin, seg_end, ppw, nworkers, d_win_seg,
                                       p->tw, (double *)part.p, s));
+    } else if (p->log2n == 12 && flen == nfft) {
+      // any other overlap at 4096: the row kernel's structure without the carry
+      HIPCHK(gdsp::launch_pwelch_rowg4096(d_x, stride, seg_begin, seg_end, ppw, nworkers,
+                                          d_win_seg, p->tw, (double *)part.p, s));
     } else {
       HIPCHK(gdsp::launch_pwelch(p->log2n, d_x, nfft, stride, seg_begin, seg_end, ppw, nworkers,
                                  d_win_seg, p->tw, (double *)part.p, s));

@@ -60,7 +60,8 @@ hipError_t launch_pwelch_mixed(const MixedDesc &d, const double *x, int64_t nfft
 // fused Pwelch with wave-resident transforms (pwelch_wave.hip), 64 <= F <= 1024:
 // the launch geometry (groups of pairs per wave, workgroups, partial rows)
 bool pwelch_wave_applies(int log2f);
-void pwelch_wave_geometry(int log2f, int64_t nsegs, int64_t *gpw, int64_t *nblk, int64_t *nrows);
+void pwelch_wave_geometry(int log2f, bool half, int64_t nsegs, int64_t *gpw, int64_t *nblk,
+                          int64_t *nrows);
 hipError_t launch_pwelch_wave(int log2f, bool half, const double *x, int64_t nfft, int64_t stride,
                               int64_t seg_begin, int64_t seg_end, int64_t gpw, int64_t nblk,
                               const double *win, const cd *tw, double *partial, hipStream_t s);
@@ -132,6 +133,11 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
                               int64_t ppw, int64_t nworkers, const double *win, const cd *tw,
                               double *partial, hipStream_t s);
 // the row kernel (pwelch_row.hip) behind launch_pwelch_half(12, ...)
+// any other overlap at F = 4096, Pad = NFFT (pwelch_rowg_kernel)
+hipError_t launch_pwelch_rowg4096(const double *x, int64_t stride, int64_t seg_begin,
+                                  int64_t seg_end, int64_t ppw, int64_t nworkers,
+                                  const double *win, const cd *tw, double *partial,
+                                  hipStream_t s);
 hipError_t launch_pwelch_row4096(const double *x, int64_t seg_begin, int64_t seg_end, int64_t ppw,
                                  int64_t nworkers, const double *win, const cd *tw,
                                  double *partial, hipStream_t s);

@@ -379,7 +379,7 @@ struct FixedLast {
 };
 
 template <bool SWZ, int R0, int... RS>
-__global__ __launch_bounds__((FixedGeo<R0, RS...>::WG)) void pwelch_fixed_kernel(
+__global__ __launch_bounds__((FixedGeo<R0, RS...>::WG)) __attribute__((amdgpu_waves_per_eu(2))) void pwelch_fixed_kernel(
     const double *__restrict__ x, int64_t nfft, int64_t stride, int64_t seg_begin,
     int64_t seg_end, int64_t pairs_per_worker, const double *__restrict__ win,
     const cd *__restrict__ tw, double *__restrict__ partial) {
@@ -394,6 +394,8 @@ __global__ __launch_bounds__((FixedGeo<R0, RS...>::WG)) void pwelch_fixed_kernel
   const int64_t worker = (int64_t)blockIdx.x * G::TPW + sub;
   double *ld = lds + sub * (SPL ? 1 : 2) * G::SLOTS;
   const int64_t npairs = (seg_end - seg_begin + 1) / 2;
+  const int64_t nfull = (seg_end - seg_begin) / 2;  // pairs with both segments
+  const bool nopad = nfft == G::N;
   const int64_t p0 = worker * pairs_per_worker;
   double acc[L::Pass::J][L::R];
 #pragma unroll
@@ -405,7 +407,8 @@ __global__ __launch_bounds__((FixedGeo<R0, RS...>::WG)) void pwelch_fixed_kernel
     const bool active = p < npairs;
     const int64_t s0 = seg_begin + 2 * (active ? p : 0);
     const bool has1 = active && s0 + 1 < seg_end;
-    const double *x0 = opaque_ptr(x) + s0 * stride, *x1 = x0 + stride;
+    const double *x0 = opaque_ptr(x) + s0 * stride;
+    const double *x1 = has1 ? x0 + stride : x0;  // (a missing partner: loaded, not used)
     // laundered per pair: otherwise the compiler hoists the loop-invariant
     // window values and twiddle power chains out of the loop, and the
     // registers they pin halve the occupancy
@@ -413,20 +416,59 @@ __global__ __launch_bounds__((FixedGeo<R0, RS...>::WG)) void pwelch_fixed_kernel
     const cd *twp = opaque_ptr(tw);
     const int tt = opaque_int(tl);
     First f0;
+    // Loads are unconditional: a full pair without padding (every pair but
+    // the signal's last, whenever Pad = NFFT; wave-uniform with one worker
+    // per workgroup) takes its samples as they are; otherwise the index is
+    // clamped and the mask applied where the samples are used. A load inside
+    // a per-lane branch is waited for inside it, one s_waitcnt per element:
+    // per 2^28 samples 480 / 240 1.82 -> 1.11 ms, 1000 / 500 1.37 -> 1.10,
+    // 1536 / 768 1.40 -> 0.99, 2000 / 1000 4.27 -> 2.84, 3000 / 1500 2.84 ->
+    // 1.90. Above 4096 points (re/im exchange halves) the branch form stays:
+    // 6000 / 3000 2.80 against 3.10 ms.
+    if constexpr (SPL) {
 #pragma unroll
-    for (int jj = 0; jj < First::J; ++jj) {
-      const int j = tt + jj * G::T1;
-      if (First::act(j, true)) {
+      for (int jj = 0; jj < First::J; ++jj) {
+        const int j = tt + jj * G::T1;
+        if (First::act(j, true)) {
 #pragma unroll
-        for (int r = 0; r < R0; ++r) {
-          const int i = j + r * First::NB;
-          double a = 0.0, b = 0.0;
-          if (active && i < nfft) {
-            const double wi = w[i];
-            a = wi * x0[i];
-            if (has1) b = wi * x1[i];
+          for (int r = 0; r < R0; ++r) {
+            const int i = j + r * First::NB;
+            double a = 0.0, b = 0.0;
+            if (active && i < nfft) {
+              const double wi = w[i];
+              a = wi * x0[i];
+              if (has1) b = wi * x1[i];
+            }
+            f0.v[jj][r] = {a, b};
           }
-          f0.v[jj][r] = {a, b};
+        }
+      }
+    } else if (p < nfull && nopad) {
+#pragma unroll
+      for (int jj = 0; jj < First::J; ++jj) {
+        const int j = tt + jj * G::T1;
+        if (First::act(j, true)) {
+#pragma unroll
+          for (int r = 0; r < R0; ++r) {
+            const int i = j + r * First::NB;
+            const double wi = w[i];
+            f0.v[jj][r] = {wi * x0[i], wi * x1[i]};
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < First::J; ++jj) {
+        const int j = tt + jj * G::T1;
+        if (First::act(j, true)) {
+#pragma unroll
+          for (int r = 0; r < R0; ++r) {
+            const int i = j + r * First::NB;
+            const bool in = i < nfft;
+            const int ic = in ? i : (int)nfft - 1;
+            const double wi = w[ic], a = x0[ic], b = x1[ic];
+            f0.v[jj][r] = {active && in ? wi * a : 0.0, has1 && in ? wi * b : 0.0};
+          }
         }
       }
     }

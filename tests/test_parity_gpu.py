@@ -385,6 +385,35 @@ def test_pwelch_vs_oracle(gdsp, oracle, n, nfft, nov, pad, win):
     assert nrel(f, fr) == 0.0
 
 
+def _wave_cases():
+    # pwelch_wave_kernel (F = 64 ... 2048): half overlap with odd and even
+    # segment counts (the last group partial: S = 64 / T slots per wave), no
+    # overlap, another overlap, and Pad > NFFT (the clamped, masked loop)
+    out = []
+    for lf in range(6, 12):
+        f = 1 << lf
+        segs = 3 + 4000 // (f // 64)
+        out += [(f, f // 2, 0, segs | 1, "hann"), (f, f // 2, 0, segs & ~1, "hamming"),
+                (f, 0, 0, segs + 2, "blackman"), (f, f // 4, 0, segs + 1, "hann"),
+                (f - 5, (f - 5) // 2, f, segs | 1, "bartlett")]
+    # several groups per worker (more groups than the launch's workers)
+    return out + [(256, 128, 0, 32767, "hann"), (1024, 0, 0, 8193, "hann")]
+
+
+@pytest.mark.parametrize("nfft,nov,pad,segs,win", _wave_cases())
+def test_pwelch_wave_kernels_vs_oracle(gdsp, oracle, nfft, nov, pad, segs, win):
+    rng = np.random.default_rng(nfft * 7 + nov + segs)
+    stride = nfft - nov
+    n = (segs - 1) * stride + nfft + int(rng.integers(0, stride))  # tail shorter than a stride
+    x = rng.uniform(-1, 1, n)
+    o = gdsp.spectral.PwelchOptions(NFFT=nfft, Noverlap=nov, Pad=pad,
+                                    Window=getattr(gdsp.window, WINDOWS[win]))
+    p, f = gdsp.spectral.Pwelch(x, 1.0, o)
+    pr, fr = oracle.pwelch(x, 1.0, nfft=nfft, pad=pad, noverlap=nov, window_kind=win)
+    assert nrel(p, pr) < TOL
+    assert nrel(f, fr) == 0.0
+
+
 # ---- edge cases and conventions --------------------------------------------------
 def test_edge_cases(gdsp):
     F = gdsp.fft
@@ -1123,9 +1152,9 @@ def test_chirpz_output_parts_in_place_large_batch(gdsp, oracle):
 # primes whose n - 1 has a radix list: small (one pass: 17 -> 16; TPW > 1 with
 # ragged last blocks), power-of-2 n - 1 (257), compiled-specialisation lists
 # (3001 -> 25*15*8, 1201 -> 1200), runtime-compiled ones (2053 -> 2052 = 4 *
-# 27 * 19, 2729 -> 2728 = 8 * 11 * 31), and n - 1 above 4096 (re/im LDS
+# 27 * 19, 2377 -> 2376 = 8 * 27 * 11), and n - 1 above 4096 (re/im LDS
 # halves: 6007, 7681, 8009, 8191)
-RADER = [17, 19, 23, 29, 31, 37, 41, 61, 97, 101, 257, 641, 1009, 1201, 1531, 2053, 2311, 2729,
+RADER = [17, 19, 23, 29, 31, 37, 41, 61, 97, 101, 257, 641, 1009, 1201, 1531, 2053, 2311, 2377,
          3001, 6007, 7681, 8009, 8191]
 
 
@@ -1165,9 +1194,10 @@ def test_rader_vs_oracle(gdsp, oracle, n):
     assert row_nrel(yc, oracle.fft_rows(x)) < TOL
 
 
-@pytest.mark.parametrize("n", [1031, 2039, 3067, 4099])
+@pytest.mark.parametrize("n", [1031, 2039, 3067, 4099, 59, 2729])
 def test_primes_without_radix_list_stay_chirpz(gdsp, oracle, n):
     # n - 1 with a prime factor above 31 (1030 = 2 * 5 * 103, 2038 = 2 * 1019, ...)
+    # or whose list needs radix 29 / 31 (58 = 2 * 29, 2728 = 8 * 11 * 31)
     D = __import__("importlib").import_module("go-dsp_amd.device")
     assert D.plan(n).kind == 3
     rng = np.random.default_rng(n)
