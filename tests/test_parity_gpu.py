@@ -370,6 +370,12 @@ WINDOWS = {"hann": "Hann", "hamming": "Hamming", "rectangular": "Rectangular",
     (70001, 1536, 768, 0, "blackman"),
     (50000, 1000, 0, 0, "rectangular"),
     (3001, 12, 5, 0, "bartlett"),      # two tiny passes
+    # radix-25 first passes (the LDS-DMA form): odd strides (segments 8-byte
+    # but not 16-byte aligned), odd segment counts, Pad > NFFT
+    (30011, 3000, 1499, 0, "hann"),
+    (40000, 2000, 999, 0, "hamming"),
+    (25001, 2900, 1000, 3000, "blackman"),
+    (60001, 2275, 1100, 0, "hann"),    # runtime-compiled (hipRTC) list
     # materialised path: a single-radix length, and a Bluestein length
     (5000, 7, 3, 0, "hann"),
     (100000, 5000, 2500, 0, "flattop"),
