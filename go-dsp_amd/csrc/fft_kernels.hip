@@ -418,12 +418,17 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_kernel(
 // E = 16 forced to 168 / 128 VGPRs (MINW 3 / 4) spills: 4.85 / 6.07 ms;
 // window re-read from L1/L2 (WMODE 1) with the split exchange 3.48 ms, with
 // a complex (two-buffer) exchange 3.45 ms.
-// Exchange slot layout of the Pwelch kernels: XOR-swizzled (conflict-free);
-// the linear padded layout (fewer address instructions, 2-way conflicted
-// reads at E = 16) measured 3.08-3.09 against 3.03-3.05 ms; the row kernel
-// below takes XOR for its first exchange and a block-padded layout for the
-// second (LAYOUT 2, fft_device.hpp).
-constexpr int kPwLinear = 0;
+// Exchange slot layout of the half-overlap kernels: the linear padded layout
+// (slot i + i / E: a per-thread base plus compile-time offsets, and paired
+// ds_read2 / ds_write2, at the cost of 2-way conflicted reads at E = 16).
+// Against XOR-swizzled slots (conflict-free, an address computation per
+// element) it measured slower on the round-2 NFFT 4096 kernel (3.08-3.09
+// against 3.03-3.05 ms) and faster on the ones left here in round 5: 16384 /
+// 8192 1.88 against 2.01 ms per 2^28 samples, 8192 / 4096 equal
+// (profiles/r05/pwelch_layout_ab.txt). NFFT 4096 runs on the row kernels
+// (XOR for the first exchange, a block-padded layout for the second: LAYOUT
+// 2, fft_device.hpp), 64 ... 2048 on the wave kernels (pwelch_wave.hip).
+constexpr int kPwLinear = 1;
 // PF: the pass twiddle bases (T_N[0 .. N/R_last)) live in LDS, so the only
 // global loads in the loop are the samples, and the next pair's samples are
 // prefetched while this pair's FFT runs (vmcnt then covers only them)
@@ -1270,18 +1275,16 @@ static hipError_t launch_pwh_t(const double *x, int64_t seg_begin, int64_t seg_e
 hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int64_t seg_end,
                               int64_t ppw, int64_t nworkers, const double *win, const cd *tw,
                               double *partial, hipStream_t s) {
+  // (F = 64 ... 2048 run on the wave kernels, pwelch_wave.hip, since round 5)
   switch (log2f) {
-#define GDSP_PWH(L) \
-  case L: return launch_pwh_t<L>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
-    GDSP_PWH(5) GDSP_PWH(6) GDSP_PWH(7) GDSP_PWH(8) GDSP_PWH(9) GDSP_PWH(10) GDSP_PWH(11)
-    // F = 4096 (the BASELINE configuration): twiddle bases in LDS and the
-    // next pair prefetched (3.16 -> 3.11 ms; 244 VGPRs, still 2 waves/SIMD)
+    case 5: return launch_pwh_t<5>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
     case 12: {
-      // the row kernel: 2.81-2.84 against 3.13-3.14 ms for pwelch_half_kernel
+      // the BASELINE configuration, on the row kernel: 2.81-2.84 against
+      // 3.13-3.14 ms for pwelch_half_kernel<12> (which with twiddle bases in
+      // LDS and the next pair prefetched had gone 3.16 -> 3.11 ms)
       return launch_pwelch_row4096(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
     }
-    GDSP_PWH(13)
-#undef GDSP_PWH
+    case 13: return launch_pwh_t<13>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
     // F = 16384: the exchange buffer alone takes 136 KiB, so the window is
     // re-read from L1/L2 instead of living in LDS
     case 14: {
@@ -1306,11 +1309,12 @@ int pwelch_workers_per_block(int log2f) {
 hipError_t launch_pwelch(int log2f, const double *x, int64_t nfft, int64_t stride,
                          int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,
                          const double *win, const cd *tw, double *partial, hipStream_t s) {
+  // (F = 64 ... 2048 run on the wave kernels; 4096 with Pad = NFFT on the
+  // row kernel's general-overlap form, pwelch_row.hip)
   switch (log2f) {
 #define GDSP_PWC(L) \
   case L: return launch_pw_t<L>(x, nfft, stride, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
-    GDSP_PWC(4) GDSP_PWC(5) GDSP_PWC(6) GDSP_PWC(7) GDSP_PWC(8) GDSP_PWC(9) GDSP_PWC(10)
-    GDSP_PWC(11) GDSP_PWC(12) GDSP_PWC(13) GDSP_PWC(14)
+    GDSP_PWC(4) GDSP_PWC(5) GDSP_PWC(12) GDSP_PWC(13) GDSP_PWC(14)
 #undef GDSP_PWC
     default: return hipErrorInvalidValue;
   }

@@ -104,8 +104,13 @@ __attribute__((amdgpu_waves_per_eu(PwwGeo<LOG2F>::wpe(HALF)))) void pwelch_wave_
       v[k] = {ak * wk, bk * wk};
     }
     // (every exchange but the kernel's first waits for the previous
-    // transform's reads: a fence inside a wave, a barrier across two)
-    fft_regs<LOG2F, true, 2, 4, 0, 0, const cd *, 0, 0, NoEpi, 0, 16, W::WAVE>(v, tt, twl, lre,
+    // transform's reads: a fence inside a wave, a barrier across two.) The
+    // exchange slots are linear padded (LAYOUT 1, i + i / 16: per-thread base
+    // plus compile-time offsets, paired ds_read2 / ds_write2) where T >= 32:
+    // 1024 / 512 0.566 against 0.534 ms per 2^28 samples with XOR-swizzled
+    // slots, 512 / 256 0.529 / 0.516, 2048 / 0 0.390 / 0.379 (the loop's non-
+    // FP64 VALU 150 -> 28 at F = 1024; profiles/r05/pwelch_layout_ab.txt)
+    fft_regs<LOG2F, true, 2, 4, 0, 0, const cd *, 1, 0, NoEpi, 0, 16, W::WAVE>(v, tt, twl, lre,
                                                                               lre, false);
 #pragma unroll
     for (int k = 0; k < E; ++k) acc[k] = fma(v[k].y, v[k].y, fma(v[k].x, v[k].x, acc[k]));
