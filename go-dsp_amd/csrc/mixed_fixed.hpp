@@ -817,6 +817,9 @@ __global__ __launch_bounds__((RaderGeo<R0, RS...>::WG)) void rader_fixed_kernel(
       if ((q + 1) * RG::WG <= CH || e < CH) *chunk_slot(e) = xc[q];
     }
   } else {
+    // (An L2 touch-ahead of the row the block 16 places later on this XCD
+    // will load, as the chirp-z kernel does, made 65 536 x 3001 slower: 1.74-
+    // 1.76 against 1.68-1.69 ms, profiles/r05/rader_pf_ab.txt.)
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int i = tl + q * T1;
