@@ -2,15 +2,25 @@
 // Each Spec is a radix list (first pass .. last pass); the batched transform
 // and fused Pwelch kernels for it are instantiated here (mixed_fixed.hpp).
 // Radix lists: as few passes as the radices <= 25 allow, full waves where
-// possible, a power-of-2 radix last.
+// possible, a power-of-2 radix last — and, since round 5, no pass with far
+// more butterflies than the others: the fused Pwelch is compute-bound, and a
+// list whose middle radix is small (25 5 16: 400 threads per transform for
+// the radix-5 pass, 80 of them busy in the radix-25 one) leaves most of its
+// waves idle in the other passes. Per 2^28 samples, fused Pwelch / batched
+// FFT (scripts/gpu_r05_specb.sh, profiles/r05/radix_lists_ab.txt): 2000
+// 25 5 16 -> 25 20 4: 2.33 -> 1.36 ms (Noverlap 0: 1.22 -> 0.76) / 0.766 ->
+// 0.745-0.751; 2400 25 6 16 -> 20 15 8: 1.90 -> 1.57 / 0.745 -> 0.748; 800
+// 25 2 16 -> 25 8 4: 1.83 -> 1.30 / 0.824-0.839 -> 0.802-0.805. 1200 keeps
+// 25 3 16: 25 12 4 made the batched FFT 4 % faster but the Pwelch 20 % and
+// Rader's 1201 (which uses this list for 1200) 9 % slower.
 #include "mixed_fixed.hpp"
 
 GDSP_SPEC_GROUP(specs0,
                 Spec<25, 15, 8>,  // 3000
                 Spec<10, 10, 10>,  // 1000
-                Spec<25, 5, 16>,  // 2000
+                Spec<25, 20, 4>,  // 2000 (25 5 16 until round 5, see above)
                 Spec<15, 10, 10>,  // 1500
-                Spec<25, 6, 16>,  // 2400
+                Spec<20, 15, 8>,  // 2400 (25 6 16 until round 5)
                 Spec<25, 3, 16>,  // 1200
                 Spec<15, 8, 8>,  // 960
                 Spec<15, 16, 8>,  // 1920

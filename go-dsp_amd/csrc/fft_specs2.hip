@@ -9,7 +9,7 @@ GDSP_SPEC_GROUP(specs2,
                 Spec<20, 9, 4>,  // 720
                 Spec<25, 5, 6>,  // 750
                 Spec<16, 6, 8>,  // 768
-                Spec<25, 2, 16>,  // 800
+                Spec<25, 8, 4>,  // 800 (25 2 16 until round 5, fft_specs0.hip)
                 Spec<15, 15, 4>,  // 900
                 Spec<15, 9, 8>,  // 1080
                 Spec<16, 9, 8>,  // 1152
