@@ -21,7 +21,7 @@
 // Two LDS exchanges and eight workgroup barriers per transform instead of
 // four and sixteen. Measured slower (chirp-z 3000: 3.53 against 3.32 ms; the
 // DPP and permlane moves take VALU issue slots the block kernel spends on
-// nothing), so gdsp_api.hip takes it only under GDSP_BLU_SHFL=1.
+// nothing); the development build runs it through gdsp_dev_fft_batch_chirpz_shfl.
 #include "dev.hpp"
 #include "shfl.hpp"
 
