@@ -12,7 +12,9 @@
 // 0.745-0.751; 2400 25 6 16 -> 20 15 8: 1.90 -> 1.57 / 0.745 -> 0.748; 800
 // 25 2 16 -> 25 8 4: 1.83 -> 1.30 / 0.824-0.839 -> 0.802-0.805. 1200 keeps
 // 25 3 16: 25 12 4 made the batched FFT 4 % faster but the Pwelch 20 % and
-// Rader's 1201 (which uses this list for 1200) 9 % slower.
+// Rader's 1201 (which uses this list for 1200) 9 % slower; 1000 25 20 2 and
+// 1500 25 15 4 were slower for both (Pwelch 1.15 -> 1.50, 1.26 -> 1.49 ms;
+// FFT 0.78 -> 0.87, 0.76 -> 0.81).
 #include "mixed_fixed.hpp"
 
 GDSP_SPEC_GROUP(specs0,
