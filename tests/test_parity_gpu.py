@@ -291,7 +291,7 @@ def test_batch_3000_vs_oracle(gdsp, oracle):
     assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL
 
 
-@pytest.mark.parametrize("n", [2, 5, 16, 1000, 4096])
+@pytest.mark.parametrize("n", [2, 5, 16, 1000, 4096, 257, 3001])  # (257, 3001: Rader)
 def test_convolve(gdsp, oracle, n):
     rng = np.random.default_rng(n)
     x = rng.standard_normal(n) + 1j * rng.standard_normal(n)
@@ -303,7 +303,10 @@ def test_convolve(gdsp, oracle, n):
                                    (6, 10), (100, 7), (128, 256), (512, 300), (1024, 1024),
                                    (16, 1000), (2048, 48), (4096, 33), (65536, 8), (32, 5),
                                    # a dimension on the output-split chirp-z (in-place rows)
-                                   (3, 8209), (8209, 2)])
+                                   (3, 8209), (8209, 2),
+                                   # prime dimensions on Rader's algorithm (rows; columns
+                                   # through the transposes)
+                                   (17, 3001), (3001, 16), (37, 41)])
 def test_fft2_vs_oracle(gdsp, oracle, shape):
     rng = np.random.default_rng(shape[0] * 1000 + shape[1])
     x = rng.uniform(-1, 1, shape) + 1j * rng.uniform(-1, 1, shape)
@@ -467,7 +470,7 @@ def test_plan_kinds(gdsp):
     # four-step rows on the output-split chirp-z (power-of-2 / single-radix columns)
     assert (D.plan(64 * 8209).kind, D.plan(64 * 8209).n2) == (6, 8209)
     assert (D.plan(2 * 10007).kind, D.plan(2 * 10007).n2) == (6, 10007)
-    assert D.plan(8191 * 64).kind == 6  # power-of-2 columns, Rader rows of 8191
+    assert D.plan(8191 * 64).kind == 6  # power-of-2 columns, chirp-z rows of 8191
     assert (D.plan(3001).kind, D.plan(3001).m) == (7, 3000)  # prime: Rader on 25 * 15 * 8
     assert D.plan(3067).kind == 3  # prime, 3066 = 2 * 3 * 7 * 73: no radix list, chirp-z
     assert D.plan(3000, chirpz=True).kind == 3
@@ -666,7 +669,8 @@ def test_TestFFTN(gdsp, refvec):
 
 @pytest.mark.parametrize("dims", [[2, 2, 3], [5], [16, 16], [3, 5, 7], [64, 1, 32], [32, 16, 8, 4],
                                   [1024, 16], [2048, 9], [7, 100, 3], [4, 4096], [2, 3, 3000],
-                                  [600, 20], [2, 1, 1, 2], [8209, 2], [2, 3, 8209]])
+                                  [600, 20], [2, 1, 1, 2], [8209, 2], [2, 3, 8209],
+                                  [3, 257, 4], [37, 41]])  # (prime axes: Rader)
 def test_fftn_vs_oracle(gdsp, oracle, dims):
     rng = np.random.default_rng(sum(dims))
     n = int(np.prod(dims))
@@ -846,7 +850,7 @@ def test_random_large_smooth_lengths(gdsp, oracle):
 
 @pytest.mark.parametrize("n,kind", [(810, 5), (1001, 5), (4095, 5), (4320, 5), (5400, 5),
                                     (6144, 5), (7000, 5), (7680, 5), (8190, 5), (6561, 5),
-                                    (7290, 5), (4802, 5), (7938, 5), (8191, 7),
+                                    (7290, 5), (4802, 5), (7938, 5), (8191, 3),
                                     # radices 17, 19, 23 (runtime-compiled lists only)
                                     (323, 5), (529, 5), (4352, 5), (7600, 5), (6900, 5),
                                     (7429, 5), (899, 5), (7936, 5), (6293, 5)])
@@ -856,7 +860,7 @@ def test_jit_specialisations(gdsp, oracle, n, kind):
     # be Bluestein. 8190 = 13 * 10 * 9 * 7, 6561 = 9^4 and 7290 = 10 * 9^3 need
     # 630-910 threads per transform (radix 9/13 passes); 4802 = 2 * 7^4 and
     # 7938 = 2 * 3^4 * 7^2 have no list shorter than five passes; 8191 is prime
-    # (Rader on 8190's list, kind 7).
+    # (8190's list needs 910 threads per transform: chirp-z, kind 3).
     D = __import__("importlib").import_module("go-dsp_amd.device")
     assert D.plan(n).kind == kind, n
     rng = np.random.default_rng(4000 + n)
@@ -1159,9 +1163,9 @@ def test_chirpz_output_parts_in_place_large_batch(gdsp, oracle):
 # ragged last blocks), power-of-2 n - 1 (257), compiled-specialisation lists
 # (3001 -> 25*15*8, 1201 -> 1200), runtime-compiled ones (2053 -> 2052 = 4 *
 # 27 * 19, 2377 -> 2376 = 8 * 27 * 11), and n - 1 above 4096 (re/im LDS
-# halves: 6007, 7681, 8009, 8191)
+# halves: 4801, 6007, 7681)
 RADER = [17, 19, 23, 29, 31, 37, 41, 61, 97, 101, 257, 641, 1009, 1201, 1531, 2053, 2311, 2377,
-         3001, 6007, 7681, 8009, 8191]
+         3001, 4801, 6007, 7681]
 
 
 @pytest.mark.parametrize("n", RADER)
@@ -1200,10 +1204,11 @@ def test_rader_vs_oracle(gdsp, oracle, n):
     assert row_nrel(yc, oracle.fft_rows(x)) < TOL
 
 
-@pytest.mark.parametrize("n", [1031, 2039, 3067, 4099, 59, 2729])
+@pytest.mark.parametrize("n", [1031, 2039, 3067, 4099, 59, 2729, 8009, 8191])
 def test_primes_without_radix_list_stay_chirpz(gdsp, oracle, n):
-    # n - 1 with a prime factor above 31 (1030 = 2 * 5 * 103, 2038 = 2 * 1019, ...)
-    # or whose list needs radix 29 / 31 (58 = 2 * 29, 2728 = 8 * 11 * 31)
+    # n - 1 with a prime factor above 31 (1030 = 2 * 5 * 103, 2038 = 2 * 1019, ...),
+    # or whose list needs radix 29 / 31 (58 = 2 * 29, 2728 = 8 * 11 * 31) or
+    # more than 512 threads per transform (8008, 8190)
     D = __import__("importlib").import_module("go-dsp_amd.device")
     assert D.plan(n).kind == 3
     rng = np.random.default_rng(n)
