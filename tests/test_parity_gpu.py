@@ -423,6 +423,40 @@ def test_pwelch_wave_kernels_vs_oracle(gdsp, oracle, nfft, nov, pad, segs, win):
     assert nrel(f, fr) == 0.0
 
 
+def _random_pwelch_cases(count=36, seed=20261018):
+    # options drawn across every Pwelch kernel family: powers of 2 from 8 to
+    # 16384 (wave, row, half and general kernels), smooth NFFTs (compiled and
+    # runtime-compiled mixed radix), a prime (materialised path); Noverlap
+    # anywhere below NFFT (the half-overlap case on purpose a quarter of the
+    # time); Pad 0, below NFFT (the pwelch.go:108 quirk) or above it
+    rng = np.random.default_rng(seed)
+    nffts = [8, 32, 64, 100, 128, 256, 480, 512, 1000, 1024, 1500, 2000, 2048, 2400, 3000, 4096,
+             1031, 8192, 16384]
+    out = []
+    for _ in range(count):
+        nfft = int(rng.choice(nffts))
+        nov = nfft // 2 if rng.random() < 0.25 else int(rng.integers(0, nfft))
+        r = rng.random()
+        pad = 0 if r < 0.5 else (nfft // 2 if r < 0.6 else nfft + int(rng.integers(1, nfft + 1)))
+        nseg = int(rng.integers(1, 40))
+        n = (nseg - 1) * (nfft - nov) + nfft + int(rng.integers(0, nfft))
+        win = str(rng.choice(list(WINDOWS)))
+        out.append((n, nfft, nov, pad, win))
+    return out
+
+
+@pytest.mark.parametrize("n,nfft,nov,pad,win", _random_pwelch_cases())
+def test_pwelch_random_options_vs_oracle(gdsp, oracle, n, nfft, nov, pad, win):
+    rng = np.random.default_rng(n * 31 + nfft)
+    x = rng.standard_normal(n)
+    o = gdsp.spectral.PwelchOptions(NFFT=nfft, Noverlap=nov, Pad=pad,
+                                    Window=getattr(gdsp.window, WINDOWS[win]))
+    p, f = gdsp.spectral.Pwelch(x, 3.0, o)
+    pr, fr = oracle.pwelch(x, 3.0, nfft=nfft, pad=pad, noverlap=nov, window_kind=win)
+    assert nrel(p, pr) < TOL
+    assert nrel(f, fr) == 0.0
+
+
 # ---- edge cases and conventions --------------------------------------------------
 def test_edge_cases(gdsp):
     F = gdsp.fft
