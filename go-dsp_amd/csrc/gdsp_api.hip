@@ -761,16 +761,18 @@ int rader_try(int dev, int64_t n, gdsp_plan *p, bool *built) {
   // per 2^27 samples (profiles/r05/rader_sweep.jsonl)
   for (int r : rad)
     if (r > 25) return GDSP_OK;
-  // nor does a list needing more than 512 threads per transform (the largest
+  // nor does a list needing more than 640 threads per transform (the largest
   // pass count over the butterflies a thread takes, as FixedGeo): 8191 (8190
-  // = 13 10 9 7, 910 threads) 2.10-2.12 against 2.03-2.04 ms, 8009 (572) a tie
+  // = 15 13 7 6, 683 threads) 2.10-2.12 against 2.03-2.04 ms per 2^27
+  // samples, 8009 (8008 = 13 11 7 8, 728 threads) ties (2.03-2.06 against
+  // 2.08-2.17); 6007 (6006 = 13 11 7 6, 546 threads) gains 7 %
   {
     int t1 = 1;
     for (int r : rad) {
       const int64_t nb = N / r, jm = r > 16 ? 1 : 16 / r, need = (nb + jm - 1) / jm;
       if (need > t1) t1 = (int)need;
     }
-    if (t1 > 512) return GDSP_OK;
+    if (t1 > 640) return GDSP_OK;
   }
   gdsp::JitRader *j = gdsp::jit_rader_build(dev, rad.data(), (int)rad.size());
   if (!j) return GDSP_OK;

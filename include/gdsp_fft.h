@@ -259,7 +259,7 @@ int gdsp_plan_create_chirpz(int64_t n, gdsp_plan **plan);
  * n <= 4096 whose prime factors are all <= 13), 6 mixed four-step (such n
  * above 8192 = n1*n2 with one-kernel factors: transposes + row kernels),
  * 7 Rader (a prime 17 <= n <= 8193 whose n - 1 has a list of radices <= 25
- * within 512 threads per transform: the DFT as
+ * within 640 threads per transform: the DFT as
  * a cyclic convolution of length n - 1, two FFTs of n - 1 points in one
  * runtime-compiled kernel; GDSP_ALGO_NO_RADER keeps such primes on kind 3). */
 int gdsp_plan_kind(const gdsp_plan *plan);

@@ -891,10 +891,10 @@ def test_random_large_smooth_lengths(gdsp, oracle):
 def test_jit_specialisations(gdsp, oracle, n, kind):
     # smooth lengths without a compiled specialisation get one compiled at
     # plan creation (mixed_jit.hip, hipRTC); above 4096 they would otherwise
-    # be Bluestein. 8190 = 13 * 10 * 9 * 7, 6561 = 9^4 and 7290 = 10 * 9^3 need
-    # 630-910 threads per transform (radix 9/13 passes); 4802 = 2 * 7^4 and
+    # be Bluestein. 8190 = 15 * 13 * 7 * 6, 6561 = 9^4 and 7290 = 10 * 9^3 need
+    # 683-810 threads per transform (radix 6/9/13 passes); 4802 = 2 * 7^4 and
     # 7938 = 2 * 3^4 * 7^2 have no list shorter than five passes; 8191 is prime
-    # (8190's list needs 910 threads per transform: chirp-z, kind 3).
+    # (8190's list needs 683 threads per transform: chirp-z, kind 3).
     D = __import__("importlib").import_module("go-dsp_amd.device")
     assert D.plan(n).kind == kind, n
     rng = np.random.default_rng(4000 + n)
@@ -1242,7 +1242,8 @@ def test_rader_vs_oracle(gdsp, oracle, n):
 def test_primes_without_radix_list_stay_chirpz(gdsp, oracle, n):
     # n - 1 with a prime factor above 31 (1030 = 2 * 5 * 103, 2038 = 2 * 1019, ...),
     # or whose list needs radix 29 / 31 (58 = 2 * 29, 2728 = 8 * 11 * 31) or
-    # more than 512 threads per transform (8008, 8190)
+    # more than 640 threads per transform (8008 = 13 * 11 * 7 * 8: 728; 8190 =
+    # 15 * 13 * 7 * 6: 683)
     D = __import__("importlib").import_module("go-dsp_amd.device")
     assert D.plan(n).kind == 3
     rng = np.random.default_rng(n)
