@@ -10,11 +10,16 @@
 // FFT (scripts/gpu_r05_specb.sh, profiles/r05/radix_lists_ab.txt): 2000
 // 25 5 16 -> 25 20 4: 2.33 -> 1.36 ms (Noverlap 0: 1.22 -> 0.76) / 0.766 ->
 // 0.745-0.751; 2400 25 6 16 -> 20 15 8: 1.90 -> 1.57 / 0.745 -> 0.748; 800
-// 25 2 16 -> 25 8 4: 1.83 -> 1.30 / 0.824-0.839 -> 0.802-0.805. 1200 keeps
-// 25 3 16: 25 12 4 made the batched FFT 4 % faster but the Pwelch 20 % and
-// Rader's 1201 (which uses this list for 1200) 9 % slower; 1000 25 20 2 and
-// 1500 25 15 4 were slower for both (Pwelch 1.15 -> 1.50, 1.26 -> 1.49 ms;
-// FFT 0.78 -> 0.87, 0.76 -> 0.81).
+// 25 2 16 -> 25 8 4: 1.83 -> 1.30 / 0.824-0.839 -> 0.802-0.805. 1200: 25 12 4
+// made the batched FFT 4 % faster but the Pwelch 20 % and Rader's 1201
+// (which uses this list for 1200) 9 % slower; 15 5 16 (late in round 5,
+// scripts/gpu_r05_specd.sh: tools/spec_candidates.py's ranking, two lists per
+// length against the default, two alternating rounds) is faster for all
+// three: 1.42 -> 1.16 ms, 0.781-0.797 -> 0.743, 1201 1.52-1.59 -> 1.34-1.44
+// ms per 2^27 samples. 1000 25 20 2 and 1500 25 15 4 were slower for both
+// (Pwelch 1.15 -> 1.50, 1.26 -> 1.49 ms; FFT 0.78 -> 0.87, 0.76 -> 0.81).
+// The other lists changed that way: fft_specs1..3.hip and
+// profiles/r05/radix_lists_ab.txt.
 #include "mixed_fixed.hpp"
 
 GDSP_SPEC_GROUP(specs0,
@@ -23,7 +28,7 @@ GDSP_SPEC_GROUP(specs0,
                 Spec<25, 20, 4>,  // 2000 (25 5 16 until round 5, see above)
                 Spec<15, 10, 10>,  // 1500
                 Spec<20, 15, 8>,  // 2400 (25 6 16 until round 5)
-                Spec<25, 3, 16>,  // 1200
+                Spec<15, 5, 16>,  // 1200
                 Spec<15, 8, 8>,  // 960
                 Spec<15, 16, 8>,  // 1920
                 Spec<15, 8, 4>,  // 480

@@ -40,6 +40,11 @@ def collect(w):
         m["f64_flop"] = 64 * f64
         m["f64_inst_share_of_valu"] = (m.get("SQ_INSTS_VALU_FMA_F64", 0) + m.get("SQ_INSTS_VALU_ADD_F64", 0)
                                        + m.get("SQ_INSTS_VALU_MUL_F64", 0)) / max(1, m.get("SQ_INSTS_VALU", 1))
+        # the VALU pipe's busy share: every wave64 VALU instruction holds a
+        # 16-lane SIMD for 4 cycles; GRBM_GUI_ACTIVE is summed over the 8 XCDs
+        # (MI355X_MICROARCH.md), each XCD 32 CUs x 4 SIMDs
+        if m.get("GRBM_GUI_ACTIVE"):
+            m["valu_pipe"] = 4 * m.get("SQ_INSTS_VALU", 0) / (m["GRBM_GUI_ACTIVE"] / 8 * 1024)
         out[k] = m
     return out
 
