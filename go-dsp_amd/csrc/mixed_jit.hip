@@ -92,7 +92,47 @@ struct Choice {
   int rad[5], np = 0;
   double eff = 0;
   bool pow2last = false, wide = false;  // wide: more than 512 threads per transform
+  double cost = 0;                      // lane_cost
 };
+
+// F64 instructions per point of dft_any<R> (mixed_core.hpp, counted by hand;
+// odd primes by dft_odd's 3 (R - 1) + H (4 H + 4), H = (R - 1) / 2)
+double dft_cost(int r) {
+  switch (r) {
+    case 2: return 2.0;
+    case 4: return 4.0;
+    case 6: return 8.0;
+    case 8: return 6.5;
+    case 9: return 11.1;
+    case 10: return 10.8;
+    case 12: return 10.7;
+    case 15: return 14.0;
+    case 16: return 9.4;
+    case 20: return 13.6;
+    case 25: return 17.0;
+    default: {
+      const int h = (r - 1) / 2;
+      return (3.0 * (r - 1) + h * (4.0 * h + 4.0)) / r;
+    }
+  }
+}
+
+// Cost model of a list's passes (tools/spec_candidates.py): each pass's DFT
+// plus twiddle chain per point, over the share of the transform's T1
+// threads its butterflies keep busy. A pass with few butterflies (a radix-25
+// first pass of 80 beside a radix-5 pass of 400) idles most lanes of the
+// compute-bound kernels (the fused Pwelch above all).
+double lane_cost(const int *rad, int np, int t1) {
+  int n = 1;
+  for (int q = 0; q < np; ++q) n *= rad[q];
+  double c = 0;
+  for (int q = 0; q < np; ++q) {
+    const int nb = n / rad[q], jj = (nb + t1 - 1) / t1;
+    const double use = (double)nb / ((double)jj * t1);
+    c += (dft_cost(rad[q]) + (q ? 8.0 * (rad[q] - 1) / rad[q] : 0.0)) / use;
+  }
+  return c;
+}
 
 bool better(const Choice &a, const Choice &b) {  // a before b?
   if (a.wide != b.wide) return !a.wide;
@@ -102,7 +142,9 @@ bool better(const Choice &a, const Choice &b) {  // a before b?
   return a.rad[0] > b.rad[0];
 }
 
-void search(int n, int depth, int maxdepth, Choice &cur, Choice &best) {
+// best: by better(); cheap: the lowest lane_cost among the lists of this
+// depth (narrow ones first)
+void search(int n, int depth, int maxdepth, Choice &cur, Choice &best, Choice &cheap) {
   if (depth == maxdepth) {
     if (n != 1) return;
     int t1 = 0, tpw = 0;
@@ -115,13 +157,17 @@ void search(int n, int depth, int maxdepth, Choice &cur, Choice &best) {
     c.eff = (double)wg / (waves * 64);
     const int last = cur.rad[depth - 1];
     c.pow2last = (last & (last - 1)) == 0;
+    c.cost = lane_cost(cur.rad, depth, t1);
     if (best.np == 0 || better(c, best)) best = c;
+    if (cheap.np == 0 || c.wide < cheap.wide ||
+        (c.wide == cheap.wide && c.cost < cheap.cost))
+      cheap = c;
     return;
   }
   for (int r : kRadices) {
     if (n % r) continue;
     cur.rad[depth] = r;
-    search(n / r, depth + 1, maxdepth, cur, best);
+    search(n / r, depth + 1, maxdepth, cur, best, cheap);
   }
 }
 
@@ -262,11 +308,17 @@ bool jit_enabled() {
 bool jit_radices(int n, int *rad, int *npass) {
   if (n < 2 || n > kMixedSpecMax || (n & (n - 1)) == 0) return false;
   Choice cur, best;
-  for (int k = 2; k <= 4; ++k) search(n, 0, k, cur, best);
+  Choice cheap[6];
+  for (int k = 2; k <= 4; ++k) search(n, 0, k, cur, best, cheap[k]);
   // five passes only where no shorter list exists (2 * 7^4 = 4802, 2 * 3^4
   // * 7^2 = 7938, ...: chirp-z otherwise)
-  if (best.np == 0) search(n, 0, 5, cur, best);
+  if (best.np == 0) search(n, 0, 5, cur, best, cheap[5]);
   if (best.np == 0) return false;
+  // the cheapest list of as many passes, where the model expects it at least
+  // 15 % faster (its ranking is not reliable closer than that: round 5's
+  // A/B of the compiled lists, profiles/r05/radix_lists_ab.txt)
+  const Choice &ch = cheap[best.np];
+  if (ch.np == best.np && ch.wide == best.wide && ch.cost < 0.85 * best.cost) best = ch;
   for (int q = 0; q < best.np; ++q) rad[q] = best.rad[q];
   *npass = best.np;
   return true;

@@ -38,12 +38,15 @@ def nrel(y, r):
 
 
 if __name__ == "__main__":
-    lo, hi = (int(sys.argv[1]), int(sys.argv[2])) if len(sys.argv) > 2 else (2, 8192)
+    # "--lengths n ...": exactly those lengths (e.g. the ones whose radix list
+    # a chooser change moved); else [lo, hi] (default 2 .. 8192)
+    listed = [int(a) for a in sys.argv[2:]] if sys.argv[1:2] == ["--lengths"] else None
+    lo, hi = (int(sys.argv[1]), int(sys.argv[2])) if len(sys.argv) > 2 and not listed else (2, 8192)
     rng = np.random.default_rng(1)
     worst, count, kinds, t_build = 0.0, 0, {}, 0.0
-    for n in range(lo, hi + 1):
-        if not smooth(n) or n & (n - 1) == 0 or (os.environ.get("SWEEP23") and all(
-                n % p for p in BIG)):
+    for n in listed or range(lo, hi + 1):
+        if not listed and (not smooth(n) or n & (n - 1) == 0 or (os.environ.get("SWEEP23") and all(
+                n % p for p in BIG))):
             continue
         t0 = time.perf_counter()
         k = D.plan(n).kind
