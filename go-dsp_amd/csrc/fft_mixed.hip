@@ -379,8 +379,16 @@ bool mixed_fixed_radices(int n, int *rad, int *npass) {
          specs2_find(n, rad, npass) || specs3_find(n, rad, npass);
 }
 
+// A list for n's fused Pwelch other than its FFT list (the specspw group,
+// fft_specs0.hip), if there is one.
+bool pwelch_fixed_radices(int n, int *rad, int *npass) {
+  if (algo_flags() & GDSP_ALGO_GENERIC_MIXED) return false;
+  return specspw_find(n, rad, npass);
+}
+
 int pwelch_fixed_workers_per_block(const MixedDesc &d) {
-  int t = specs0_pw_tpw(d);
+  int t = specspw_pw_tpw(d);
+  if (!t) t = specs0_pw_tpw(d);
   if (!t) t = specs1_pw_tpw(d);
   if (!t) t = specs2_pw_tpw(d);
   if (!t) t = specs3_pw_tpw(d);
@@ -393,7 +401,8 @@ hipError_t launch_pwelch_fixed(const MixedDesc &d, const double *x, int64_t nfft
   if (nworkers <= 0 || nworkers > 0x7fffffff) return hipErrorInvalidValue;
 #define GDSP_PWG(G) \
   G##_pw_launch(d, x, nfft, stride, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s)
-  if (!(GDSP_PWG(specs0) || GDSP_PWG(specs1) || GDSP_PWG(specs2) || GDSP_PWG(specs3)))
+  if (!(GDSP_PWG(specspw) || GDSP_PWG(specs0) || GDSP_PWG(specs1) || GDSP_PWG(specs2) ||
+        GDSP_PWG(specs3)))
     return hipErrorInvalidValue;
 #undef GDSP_PWG
   return hipGetLastError();

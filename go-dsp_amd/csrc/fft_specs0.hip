@@ -18,6 +18,11 @@
 // three: 1.42 -> 1.16 ms, 0.781-0.797 -> 0.743, 1201 1.52-1.59 -> 1.34-1.44
 // ms per 2^27 samples. 1000 25 20 2 and 1500 25 15 4 were slower for both
 // (Pwelch 1.15 -> 1.50, 1.26 -> 1.49 ms; FFT 0.78 -> 0.87, 0.76 -> 0.81).
+// Then (scripts/gpu_r05_specp.sh, six lists each) 2000 25 20 4 -> 10 10 20
+// (Pwelch 1.37-1.38 -> 1.25 ms, FFT equal), 2400 20 15 8 -> 15 16 10 (1.51
+// -> 1.26, FFT -1 %) and 1500 15 10 10 -> 15 20 5 (1.20-1.21 -> 1.08-1.09,
+// FFT equal); 3000 keeps 25 15 8 for the FFT (every other list 5-15 % slower
+// there) and gives the fused Pwelch its own list (specspw below).
 // The other lists changed that way: fft_specs1..3.hip and
 // profiles/r05/radix_lists_ab.txt.
 #include "mixed_fixed.hpp"
@@ -25,9 +30,9 @@
 GDSP_SPEC_GROUP(specs0,
                 Spec<25, 15, 8>,  // 3000
                 Spec<10, 10, 10>,  // 1000
-                Spec<25, 20, 4>,  // 2000 (25 5 16 until round 5, see above)
-                Spec<15, 10, 10>,  // 1500
-                Spec<20, 15, 8>,  // 2400 (25 6 16 until round 5)
+                Spec<10, 10, 20>,  // 2000 (25 5 16, then 25 20 4 in round 5, see above)
+                Spec<15, 20, 5>,  // 1500 (15 10 10 until late round 5)
+                Spec<15, 16, 10>,  // 2400 (25 6 16, then 20 15 8 in round 5)
                 Spec<15, 5, 16>,  // 1200
                 Spec<15, 8, 8>,  // 960
                 Spec<15, 16, 8>,  // 1920
@@ -37,3 +42,13 @@ GDSP_SPEC_GROUP(specs0,
                 Spec<9, 7, 7>,  // 441 (44.1 kHz audio frames)
                 Spec<15, 7, 7>,  // 735 (44.1 kHz audio frames)
                 Spec<9, 3, 7, 7>)  // 1323 (44.1 kHz audio frames)
+
+// Fused-Pwelch-only lists (pwelch_fixed_radices, fft_mixed.hip): the batched
+// FFT of these lengths keeps the list above, the fused Pwelch takes this one.
+// 3000: 15 5 5 8 (four passes, 200 threads, every pass >= 94 % busy) runs the
+// Pwelch at half overlap in 1.32-1.33 against 1.68 ms per 2^28 samples, but
+// the batched FFT in 0.845 against 0.803-0.809 ms per 2^27 samples (HBM-bound
+// there, where the extra exchange costs and the idle lanes do not)
+// (scripts/gpu_r05_specp.sh, profiles/r05/radix_lists_ab.txt).
+GDSP_SPEC_GROUP(specspw,
+                Spec<15, 5, 5, 8>)  // 3000 (fused Pwelch)

@@ -307,6 +307,10 @@ struct gdsp_plan {
   gdsp::MixedDesc md{};
   gdsp::MixedDesc md_gen{};  // generic radix list (runtime-radix kernels)
   cd *tw_gen = nullptr;
+  // the fused Pwelch's own compiled list where it differs from md's
+  // (pwelch_fixed_radices; md_pw.n = 0: none)
+  gdsp::MixedDesc md_pw{};
+  cd *tw_pw = nullptr;
   gdsp::JitSpec *jit = nullptr;  // runtime-compiled specialisation of md (mixed_jit.hip)
   // mixed four-step (KIND_MIXED4): n = n1 * n2, one-kernel sub-plans, tw = T_n;
   // pow2col: n1 is a power of 2 in [16, 512], so the column DFT runs on
@@ -457,6 +461,11 @@ int make_mixed_desc(int dev, int64_t n, const std::vector<int> &rad, gdsp::Mixed
 int build_mixed(int dev, int64_t n, const std::vector<int> &rad, gdsp_plan *p) {
   p->kind = KIND_MIXED;
   STCHK(make_mixed_desc(dev, n, rad, p->md, &p->tw));
+  {
+    int pr[16], pnp = 0;
+    if (gdsp::pwelch_fixed_radices((int)n, pr, &pnp))
+      STCHK(make_mixed_desc(dev, n, std::vector<int>(pr, pr + pnp), p->md_pw, &p->tw_pw));
+  }
   // the runtime-radix kernels (fused Pwelch) take the generic list: radices
   // <= 16, no composites (a compiled specialisation's list may hold them)
   std::vector<int> gen;
@@ -2034,9 +2043,13 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
   }
   if (p->kind == KIND_MIXED && (p->jit || gdsp::pwelch_fixed_workers_per_block(p->md) > 0) &&
       !(gdsp::algo_flags() & GDSP_ALGO_GENERIC_MIXED)) {
-    // fused path on a compiled specialisation (e.g. NFFT 1000, 3000)
+    // fused path on a compiled specialisation (e.g. NFFT 1000, 3000), on the
+    // Pwelch's own list where it has one (md_pw)
+    const bool own = p->md_pw.n > 0 && !p->jit;
+    const gdsp::MixedDesc &pmd = own ? p->md_pw : p->md;
+    const cd *ptw = own ? p->tw_pw : p->tw;
     const int64_t npairs = (nseg + 1) / 2;
-    const int wpb = p->jit ? gdsp::jit_pw_tpw(p->jit) : gdsp::pwelch_fixed_workers_per_block(p->md);
+    const int wpb = p->jit ? gdsp::jit_pw_tpw(p->jit) : gdsp::pwelch_fixed_workers_per_block(pmd);
     int64_t target = 2048 * (int64_t)wpb;
     if (target > npairs) target = npairs;
     const int64_t ppw = (npairs + target - 1) / target;
@@ -2049,8 +2062,8 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
       HIPCHK(gdsp::jit_launch_pwelch(p->jit, d_x, nfft, stride, seg_begin, seg_end, ppw, nworkers,
                                      d_win_seg, p->tw, (double *)part.p, s));
     else
-      HIPCHK(gdsp::launch_pwelch_fixed(p->md, d_x, nfft, stride, seg_begin, seg_end, ppw,
-                                       nworkers, d_win_seg, p->tw, (double *)part.p, s));
+      HIPCHK(gdsp::launch_pwelch_fixed(pmd, d_x, nfft, stride, seg_begin, seg_end, ppw,
+                                       nworkers, d_win_seg, ptw, (double *)part.p, s));
     HIPCHK(gdsp::launch_reduce_partials((const double *)part.p, nworkers, flen, d_acc,
                                         (double *)red.p, s));
     return GDSP_OK;

@@ -103,6 +103,8 @@ hipError_t jit_launch_pwelch(const JitSpec *j, const double *x, int64_t nfft, in
                              const double *win, const cd *tw, double *partial, hipStream_t s);
 // radix list of a compiled specialisation for n (false: use the generic list)
 bool mixed_fixed_radices(int n, int *rad, int *npass);
+// the fused Pwelch's own list for n where it differs from the FFT's (fft_mixed.hip)
+bool pwelch_fixed_radices(int n, int *rad, int *npass);
 hipError_t launch_fft_mixed(const MixedDesc &d, bool inv, int load, const void *in, cd *out,
                             int64_t batch, const cd *tw, double scale, hipStream_t s);
 hipError_t launch_bluestein(int log2m, bool inv, const cd *in, cd *out, int64_t n,

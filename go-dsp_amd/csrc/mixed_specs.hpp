@@ -17,5 +17,6 @@ GDSP_DECL_SPEC_GROUP(specs0)
 GDSP_DECL_SPEC_GROUP(specs1)
 GDSP_DECL_SPEC_GROUP(specs2)
 GDSP_DECL_SPEC_GROUP(specs3)
+GDSP_DECL_SPEC_GROUP(specspw)  // fused-Pwelch-only lists (fft_specs0.hip)
 #undef GDSP_DECL_SPEC_GROUP
 }  // namespace gdsp

@@ -373,11 +373,14 @@ WINDOWS = {"hann": "Hann", "hamming": "Hamming", "rectangular": "Rectangular",
     (70001, 1536, 768, 0, "blackman"),
     (50000, 1000, 0, 0, "rectangular"),
     (3001, 12, 5, 0, "bartlett"),      # two tiny passes
-    # radix-25 first passes (the LDS-DMA form): odd strides (segments 8-byte
-    # but not 16-byte aligned), odd segment counts, Pad > NFFT
+    # odd strides (segments 8-byte but not 16-byte aligned), odd segment
+    # counts, Pad > NFFT: on 3000's own Pwelch list (15 5 5 8, specspw), on
+    # 2000's 10 10 20, and in the radix-25-first LDS-DMA form (3200's 25 8 16,
+    # 2275's runtime-compiled 25 13 7)
     (30011, 3000, 1499, 0, "hann"),
     (40000, 2000, 999, 0, "hamming"),
     (25001, 2900, 1000, 3000, "blackman"),
+    (50001, 3200, 1599, 0, "hann"),
     (60001, 2275, 1100, 0, "hann"),    # runtime-compiled (hipRTC) list
     # materialised path: a single-radix length, and a Bluestein length
     (5000, 7, 3, 0, "hann"),
@@ -392,6 +395,42 @@ def test_pwelch_vs_oracle(gdsp, oracle, n, nfft, nov, pad, win):
     pr, fr = oracle.pwelch(x, 2.5, nfft=nfft, pad=pad, noverlap=nov, window_kind=win)
     assert nrel(p, pr) < TOL
     assert nrel(f, fr) == 0.0
+
+
+def _spec_lengths():
+    # every compiled specialisation (go-dsp_amd/csrc/fft_specs*.hip), read from
+    # the sources so a changed or added radix list is covered without editing
+    # this file
+    import math
+    import re
+    from pathlib import Path
+    csrc = Path(__file__).resolve().parent.parent / "go-dsp_amd" / "csrc"
+    out = set()
+    for f in csrc.glob("fft_specs*.hip"):
+        for m in re.finditer(r"Spec<([\d, ]+)>", f.read_text()):
+            out.add(math.prod(int(v) for v in m.group(1).split(",")))
+    return sorted(out)
+
+
+@pytest.mark.parametrize("nfft", _spec_lengths())
+def test_pwelch_every_specialisation(gdsp, oracle, nfft):
+    """The fused Pwelch (pwelch_fixed_kernel) of each compiled radix list at
+    half overlap with an odd segment count (a partnerless last pair) and at
+    Noverlap 0, against the reference restatement (spectral/pwelch.go:104-122),
+    and the list's batched FFT forward / inverse."""
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    assert D.plan(nfft).kind == 5, nfft
+    rng = np.random.default_rng(nfft)
+    for nov, nseg in ((nfft // 2, 7), (0, 4)):
+        n = (nseg - 1) * (nfft - nov) + nfft + 3
+        x = rng.standard_normal(n)
+        o = gdsp.spectral.PwelchOptions(NFFT=nfft, Noverlap=nov)
+        p, f = gdsp.spectral.Pwelch(x, 3.0, o)
+        pr, fr = oracle.pwelch(x, 3.0, nfft=nfft, noverlap=nov)
+        assert nrel(p, pr) < TOL and nrel(f, fr) == 0.0, (nfft, nov)
+    xb = rng.uniform(-1, 1, (3, nfft)) + 1j * rng.uniform(-1, 1, (3, nfft))
+    assert row_nrel(gdsp.fft.FFTBatch(xb), oracle.fft_rows(xb)) < TOL
+    assert row_nrel(gdsp.fft.FFTBatch(xb, inverse=True), oracle.ifft_rows(xb)) < TOL
 
 
 def _wave_cases():
