@@ -50,5 +50,11 @@ GDSP_SPEC_GROUP(specs0,
 // the batched FFT in 0.845 against 0.803-0.809 ms per 2^27 samples (HBM-bound
 // there, where the extra exchange costs and the idle lanes do not)
 // (scripts/gpu_r05_specp.sh, profiles/r05/radix_lists_ab.txt).
+// Four-pass lists for the others measured (scripts/gpu_r05_specq.sh, three
+// each, two alternating rounds): 6000 15 5 5 16 2.45 against 2.77-2.78 ms,
+// 4000 10 10 10 4 1.53 against 1.74-1.75 ms; 4500, 800, 2880, 3200, 1536 and
+// 2400 were slower or within 3 % and keep their FFT list.
 GDSP_SPEC_GROUP(specspw,
-                Spec<15, 5, 5, 8>)  // 3000 (fused Pwelch)
+                Spec<15, 5, 5, 8>,    // 3000 (fused Pwelch)
+                Spec<10, 10, 10, 4>,  // 4000 (fused Pwelch)
+                Spec<15, 5, 5, 16>)   // 6000 (fused Pwelch)
