@@ -733,7 +733,10 @@ bool rader_radices(int64_t N, std::vector<int> &rad) {
   if (N < 2 || N > gdsp::kMixedSpecMax) return false;
   // (N = 3000: the specialisation's 25 15 8, 1.66 ms per 65 536 x 3001;
   // 8 15 25, 20 15 10, 10 10 3 10, 12 10 25 and 15 10 20 took 2.2-3.8 ms,
-  // profiles/r05/rader_radix_ab.txt)
+  // profiles/r05/rader_radix_ab.txt; the fused Pwelch's own four-pass lists
+  // are slower here too: 3001 on 15 5 5 8 1.41-1.42 against 1.30-1.31 ms per
+  // 2^27 samples, 4001 on 10 10 10 4 1.63 against 1.40-1.41,
+  // scripts/gpu_r05_raderpw.sh)
   if (is_pow2(N)) {
     int a = ilog2(N);
     while (a >= 4) {
