@@ -1286,7 +1286,10 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
     }
     case 13: return launch_pwh_t<13>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
     // F = 16384: the exchange buffer alone takes 136 KiB, so the window is
-    // re-read from L1/L2 instead of living in LDS
+    // re-read from L1/L2 instead of living in LDS; 32 points per thread (256 VGPRs, 123
+    // spilled, two waves per SIMD) 1.91 against 2.00-2.01 ms per 2^28 samples
+    // for 16 (1024 threads, 128 VGPRs, 67 spilled, four waves per SIMD;
+    // scripts/gpu_r05_h16.sh)
     case 14: {
       // 32 points per thread (512 threads): 2.25-2.27 against 2.37-2.40 ms at
       // 2^28 samples for 16 (1024 threads); both spill
