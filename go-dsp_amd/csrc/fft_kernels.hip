@@ -1286,13 +1286,13 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
     }
     case 13: return launch_pwh_t<13>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
     // F = 16384: the exchange buffer alone takes 136 KiB, so the window is
-    // re-read from L1/L2 instead of living in LDS; 32 points per thread (256 VGPRs, 123
-    // spilled, two waves per SIMD) 1.91 against 2.00-2.01 ms per 2^28 samples
-    // for 16 (1024 threads, 128 VGPRs, 67 spilled, four waves per SIMD;
-    // scripts/gpu_r05_h16.sh)
+    // re-read from L1/L2 instead of living in LDS
     case 14: {
       // 32 points per thread (512 threads): 2.25-2.27 against 2.37-2.40 ms at
-      // 2^28 samples for 16 (1024 threads); both spill
+      // 2^28 samples for 16 (1024 threads); both spill (re-measured at the end
+      // of round 5 on the linear exchange slots: 256 VGPRs, 123 spilled, two
+      // waves per SIMD, 1.91 ms, against 128 VGPRs, 67 spilled, four waves,
+      // 2.00-2.01 ms; scripts/gpu_r05_h16.sh)
       return launch_pwh_t<14, 1, 1, 5>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
     }
     default: return hipErrorInvalidValue;
