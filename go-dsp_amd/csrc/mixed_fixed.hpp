@@ -425,6 +425,22 @@ struct FixedTwN {
 // The other lists measured slower this way (1500 / 700, 15 10 10: 1.21 ->
 // 1.33; 2205 / 1102: 1.24 -> 1.55), as did staging each pair through the
 // exchange buffer without the DMA (10 10 10, 12 16 8, 15 8 4: 7-20 %).
+// Lists whose fused Pwelch is faster held to more waves per SIMD than the
+// compiler's natural count, measured per list: 6000 15 5 5 16 (the fused
+// Pwelch's own list; seven-wave workgroups) at four waves per SIMD — 128
+// VGPRs, 32 spilled, two workgroups per CU — runs 2.16-2.17 against
+// 2.45-2.46 ms per 2^28 samples at its natural 142 VGPRs (one workgroup per
+// CU); the other lists above 4096 spill 140-510 VGPRs held that way
+// (scripts/gpu_r05_w4.sh, profiles/r05/pwelch_wpe_ab.txt). 0: no override.
+template <int... RS>
+struct PwWpe {
+  static constexpr int v = 0;
+};
+template <>
+struct PwWpe<15, 5, 5, 16> {
+  static constexpr int v = 4;
+};
+
 template <int R0, int... RS>
 struct PwfDma {
   using G = FixedGeo<R0, RS...>;
@@ -437,7 +453,9 @@ struct PwfDma {
   // against 1.90 at the compiler's choice, one wave with AGPRs); elsewhere it
   // helps or is neutral (1500 / 700, 15 10 10: 1.18 against 1.47 ms;
   // profiles/r05/pwelch_fixed_dma_ab.txt)
-  static constexpr int wpe() { return on || R0 != 25 ? 2 : 1; }
+  static constexpr int wpe() {
+    return PwWpe<R0, RS...>::v ? PwWpe<R0, RS...>::v : on || R0 != 25 ? 2 : 1;
+  }
 };
 
 template <bool SWZ, int R0, int... RS>
