@@ -426,18 +426,28 @@ struct FixedTwN {
 // 1.33; 2205 / 1102: 1.24 -> 1.55), as did staging each pair through the
 // exchange buffer without the DMA (10 10 10, 12 16 8, 15 8 4: 7-20 %).
 // Lists whose fused Pwelch is faster held to more waves per SIMD than the
-// compiler's natural count, measured per list: 6000 15 5 5 16 (the fused
-// Pwelch's own list; seven-wave workgroups) at four waves per SIMD — 128
-// VGPRs, 32 spilled, two workgroups per CU — runs 2.16-2.17 against
-// 2.45-2.46 ms per 2^28 samples at its natural 142 VGPRs (one workgroup per
-// CU); the other lists above 4096 spill 140-510 VGPRs held that way
-// (scripts/gpu_r05_w4.sh, profiles/r05/pwelch_wpe_ab.txt). 0: no override.
+// compiler's natural count, measured per list (scripts/gpu_r05_w4.sh, w5.sh,
+// profiles/r05/pwelch_wpe_ab.txt); it pays where it adds a resident workgroup
+// per CU for few spills:
+//  - 6000 15 5 5 16 (the fused Pwelch's own list; seven-wave workgroups) at
+//    four waves per SIMD — 128 VGPRs, 32 spilled, two workgroups per CU
+//    instead of one — 2.16-2.17 against 2.45-2.46 ms per 2^28 samples;
+//  - 4500 15 20 15 (five-wave workgroups) at four — 128 VGPRs, 30 spilled,
+//    three workgroups per CU instead of two — 2.36-2.38 against 2.77 ms.
+// Not kept: 2000 10 10 20 at four (45 spilled) 1.49-1.50 against 1.30 ms,
+// 2400 15 16 10 at three (30 spilled) 1.57 against 1.26-1.28 ms (they had
+// two or more workgroups per CU already); the other lists above 4096 spill
+// 140-510 VGPRs held to two workgroups per CU. 0: no override.
 template <int... RS>
 struct PwWpe {
   static constexpr int v = 0;
 };
 template <>
 struct PwWpe<15, 5, 5, 16> {
+  static constexpr int v = 4;
+};
+template <>
+struct PwWpe<15, 20, 15> {
   static constexpr int v = 4;
 };
 
