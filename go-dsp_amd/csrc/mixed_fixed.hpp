@@ -437,7 +437,10 @@ struct FixedTwN {
 // Not kept: 2000 10 10 20 at four (45 spilled) 1.49-1.50 against 1.30 ms,
 // 2400 15 16 10 at three (30 spilled) 1.57 against 1.26-1.28 ms (they had
 // two or more workgroups per CU already); the other lists above 4096 spill
-// 140-510 VGPRs held to two workgroups per CU. 0: no override.
+// 140-510 VGPRs held to two workgroups per CU; and of seven more lists with
+// 4-42 spills at the cap that adds a workgroup per CU (160, 150, 1000, 882,
+// 4410, 2880, 2560; scripts/gpu_r05_w6.sh) six lost 2-58 % and 150 gained
+// 2 %. 0: no override.
 template <int... RS>
 struct PwWpe {
   static constexpr int v = 0;
