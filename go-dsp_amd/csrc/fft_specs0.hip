@@ -54,7 +54,21 @@ GDSP_SPEC_GROUP(specs0,
 // each, two alternating rounds): 6000 15 5 5 16 2.45 against 2.77-2.78 ms,
 // 4000 10 10 10 4 1.53 against 1.74-1.75 ms; 4500, 800, 2880, 3200, 1536 and
 // 2400 were slower or within 3 % and keep their FFT list.
+// Then 16 more lengths, two four-pass lists each (scripts/gpu_r05_s12.sh):
+// nine faster, per 2^28 samples: 768 1.27-1.28 -> 0.99-1.01 ms, 1875 1.32
+// -> 1.16, 2250 2.11-2.14 -> 1.45, 2500 1.71 -> 1.07, 3125 1.94 -> 1.65,
+// 3750 2.45 -> 1.54, 5000 3.55 -> 1.44, 6400 2.89 -> 2.46-2.47, 7500 2.58 ->
+// 2.45; 400, 441, 750, 1440, 2160, 2560 and 3072 keep their FFT list.
 GDSP_SPEC_GROUP(specspw,
                 Spec<15, 5, 5, 8>,    // 3000 (fused Pwelch)
                 Spec<10, 10, 10, 4>,  // 4000 (fused Pwelch)
-                Spec<15, 5, 5, 16>)   // 6000 (fused Pwelch)
+                Spec<15, 5, 5, 16>,   // 6000 (fused Pwelch)
+                Spec<12, 4, 4, 4>,    // 768 (fused Pwelch)
+                Spec<15, 5, 5, 5>,    // 1875 (fused Pwelch)
+                Spec<15, 2, 5, 15>,   // 2250 (fused Pwelch)
+                Spec<10, 5, 5, 10>,   // 2500 (fused Pwelch)
+                Spec<5, 5, 5, 25>,    // 3125 (fused Pwelch)
+                Spec<15, 5, 5, 10>,   // 3750 (fused Pwelch)
+                Spec<10, 10, 10, 5>,  // 5000 (fused Pwelch)
+                Spec<5, 5, 16, 16>,   // 6400 (fused Pwelch)
+                Spec<20, 5, 5, 15>)   // 7500 (fused Pwelch)
