@@ -59,6 +59,7 @@ GDSP_SPEC_GROUP(specs0,
 // -> 1.16, 2250 2.11-2.14 -> 1.45, 2500 1.71 -> 1.07, 3125 1.94 -> 1.65,
 // 3750 2.45 -> 1.54, 5000 3.55 -> 1.44, 6400 2.89 -> 2.46-2.47, 7500 2.58 ->
 // 2.45; 400, 441, 750, 1440, 2160, 2560 and 3072 keep their FFT list.
+// (3750, 5000 and 7500 then took those lists for the FFT too: fft_specs3.hip.)
 GDSP_SPEC_GROUP(specspw,
                 Spec<15, 5, 5, 8>,    // 3000 (fused Pwelch)
                 Spec<10, 10, 10, 4>,  // 4000 (fused Pwelch)
@@ -68,7 +69,4 @@ GDSP_SPEC_GROUP(specspw,
                 Spec<15, 2, 5, 15>,   // 2250 (fused Pwelch)
                 Spec<10, 5, 5, 10>,   // 2500 (fused Pwelch)
                 Spec<5, 5, 5, 25>,    // 3125 (fused Pwelch)
-                Spec<15, 5, 5, 10>,   // 3750 (fused Pwelch)
-                Spec<10, 10, 10, 5>,  // 5000 (fused Pwelch)
-                Spec<5, 5, 16, 16>,   // 6400 (fused Pwelch)
-                Spec<20, 5, 5, 15>)   // 7500 (fused Pwelch)
+                Spec<5, 5, 16, 16>)   // 6400 (fused Pwelch)
