@@ -60,6 +60,8 @@ GDSP_SPEC_GROUP(specs0,
 // 3750 2.45 -> 1.54, 5000 3.55 -> 1.44, 6400 2.89 -> 2.46-2.47, 7500 2.58 ->
 // 2.45; 400, 441, 750, 1440, 2160, 2560 and 3072 keep their FFT list.
 // (3750, 5000 and 7500 then took those lists for the FFT too: fft_specs3.hip.)
+// 44.1 kHz frames (scripts/gpu_r05_audio.sh, two lists each): 5880 15 7 7 8
+// 2.44-2.45 against 2.69-2.70 ms; 4410, 2940 and 2646 keep their FFT list.
 GDSP_SPEC_GROUP(specspw,
                 Spec<15, 5, 5, 8>,    // 3000 (fused Pwelch)
                 Spec<10, 10, 10, 4>,  // 4000 (fused Pwelch)
@@ -69,4 +71,5 @@ GDSP_SPEC_GROUP(specspw,
                 Spec<15, 2, 5, 15>,   // 2250 (fused Pwelch)
                 Spec<10, 5, 5, 10>,   // 2500 (fused Pwelch)
                 Spec<5, 5, 5, 25>,    // 3125 (fused Pwelch)
-                Spec<5, 5, 16, 16>)   // 6400 (fused Pwelch)
+                Spec<5, 5, 16, 16>,   // 6400 (fused Pwelch)
+                Spec<15, 7, 7, 8>)    // 5880 (fused Pwelch)
