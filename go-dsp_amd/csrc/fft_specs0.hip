@@ -62,6 +62,11 @@ GDSP_SPEC_GROUP(specs0,
 // (3750, 5000 and 7500 then took those lists for the FFT too: fft_specs3.hip.)
 // 44.1 kHz frames (scripts/gpu_r05_audio.sh, two lists each): 5880 15 7 7 8
 // 2.44-2.45 against 2.69-2.70 ms; 4410, 2940 and 2646 keep their FFT list.
+// Then 14 more (scripts/gpu_r05_t12.sh): 500 10 5 10 0.85-0.87 against
+// 1.57-1.58 ms, 250 10 5 5 0.87 against 1.62, 375 15 5 5 1.02-1.03 against
+// 1.60, 200 10 2 10 0.88 against 1.19, 1152 12 2 4 12 1.02 against 1.32, 625
+// 5 5 25 1.24 against 1.54, 320 16 20 0.93 against 0.99; 4800, 5120, 3600,
+// 1600, 1800, 1920 and 960 keep their FFT list.
 GDSP_SPEC_GROUP(specspw,
                 Spec<15, 5, 5, 8>,    // 3000 (fused Pwelch)
                 Spec<10, 10, 10, 4>,  // 4000 (fused Pwelch)
@@ -72,4 +77,11 @@ GDSP_SPEC_GROUP(specspw,
                 Spec<10, 5, 5, 10>,   // 2500 (fused Pwelch)
                 Spec<5, 5, 5, 25>,    // 3125 (fused Pwelch)
                 Spec<5, 5, 16, 16>,   // 6400 (fused Pwelch)
-                Spec<15, 7, 7, 8>)    // 5880 (fused Pwelch)
+                Spec<15, 7, 7, 8>,    // 5880 (fused Pwelch)
+                Spec<10, 5, 10>,      // 500 (fused Pwelch)
+                Spec<5, 5, 25>,       // 625 (fused Pwelch)
+                Spec<15, 5, 5>,       // 375 (fused Pwelch)
+                Spec<10, 5, 5>,       // 250 (fused Pwelch)
+                Spec<10, 2, 10>,      // 200 (fused Pwelch)
+                Spec<16, 20>,         // 320 (fused Pwelch)
+                Spec<12, 2, 4, 12>)   // 1152 (fused Pwelch)
