@@ -66,7 +66,8 @@ GDSP_SPEC_GROUP(specs0,
 // 1.57-1.58 ms, 250 10 5 5 0.87 against 1.62, 375 15 5 5 1.02-1.03 against
 // 1.60, 200 10 2 10 0.88 against 1.19, 1152 12 2 4 12 1.02 against 1.32, 625
 // 5 5 25 1.24 against 1.54, 320 16 20 0.93 against 0.99; 4800, 5120, 3600,
-// 1600, 1800, 1920 and 960 keep their FFT list.
+// 1600, 1800, 1920 and 960 keep their FFT list. (250 and 500 took theirs for the FFT
+// too: fft_specs1.hip.)
 GDSP_SPEC_GROUP(specspw,
                 Spec<15, 5, 5, 8>,    // 3000 (fused Pwelch)
                 Spec<10, 10, 10, 4>,  // 4000 (fused Pwelch)
@@ -78,10 +79,8 @@ GDSP_SPEC_GROUP(specspw,
                 Spec<5, 5, 5, 25>,    // 3125 (fused Pwelch)
                 Spec<5, 5, 16, 16>,   // 6400 (fused Pwelch)
                 Spec<15, 7, 7, 8>,    // 5880 (fused Pwelch)
-                Spec<10, 5, 10>,      // 500 (fused Pwelch)
                 Spec<5, 5, 25>,       // 625 (fused Pwelch)
                 Spec<15, 5, 5>,       // 375 (fused Pwelch)
-                Spec<10, 5, 5>,       // 250 (fused Pwelch)
                 Spec<10, 2, 10>,      // 200 (fused Pwelch)
                 Spec<16, 20>,         // 320 (fused Pwelch)
                 Spec<12, 2, 4, 12>)   // 1152 (fused Pwelch)

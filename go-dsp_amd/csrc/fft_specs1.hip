@@ -8,6 +8,11 @@
 // 400 (25 16), 600 (25 6 4), 640 (16 10 4) and 1470 (7 5 6 7): fused Pwelch
 // per 2^28 samples -10 to -64 % (600: 2.98 -> 1.06 ms), batched FFT 0 to
 // -11 %; Rader's 101 / 601 -17 / -9 %, 641 +8 %.
+// Last (scripts/gpu_r05_t12.sh, f2.sh), the three-pass lists the fused
+// Pwelch took for 250 and 500 (1.62 -> 0.87 and 1.57 -> 0.86 ms per 2^28
+// samples) as FFT lists too: 250 10 5 5 0.752 against 0.777-0.781 ms per
+// 2^27 samples (Rader's 251 1.16 against 1.26), 500 10 5 10 0.760-0.762
+// against 0.770-0.773.
 #include "mixed_fixed.hpp"
 
 GDSP_SPEC_GROUP(specs1,
@@ -17,12 +22,12 @@ GDSP_SPEC_GROUP(specs1,
                 Spec<10, 16>,  // 160
                 Spec<25, 8>,  // 200
                 Spec<15, 16>,  // 240
-                Spec<25, 10>,  // 250
+                Spec<10, 5, 5>,  // 250 (25 10 until late round 5)
                 Spec<15, 20>,  // 300
                 Spec<20, 16>,  // 320
                 Spec<15, 3, 8>,  // 360
                 Spec<16, 25>,  // 400
-                Spec<25, 20>,  // 500
+                Spec<10, 5, 10>,  // 500 (25 20 until late round 5)
                 Spec<15, 5, 8>,  // 600
                 Spec<16, 8, 5>,  // 640
                 Spec<25, 15>,  // 375 (four-step rows)
