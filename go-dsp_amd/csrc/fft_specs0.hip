@@ -68,6 +68,9 @@ GDSP_SPEC_GROUP(specs0,
 // 5 5 25 1.24 against 1.54, 320 16 20 0.93 against 0.99; 4800, 5120, 3600,
 // 1600, 1800, 1920 and 960 keep their FFT list. (250 and 500 took theirs for the FFT
 // too: fft_specs1.hip.)
+// The short lengths last (scripts/gpu_r05_c12.sh, 17 lengths): 735 7 7 15
+// 1.28-1.29 against 1.35 ms, 900 15 4 15 1.17 against 1.19-1.21; the other 15
+// (100 ... 1764) keep their FFT list.
 GDSP_SPEC_GROUP(specspw,
                 Spec<15, 5, 5, 8>,    // 3000 (fused Pwelch)
                 Spec<10, 10, 10, 4>,  // 4000 (fused Pwelch)
@@ -83,4 +86,6 @@ GDSP_SPEC_GROUP(specspw,
                 Spec<15, 5, 5>,       // 375 (fused Pwelch)
                 Spec<10, 2, 10>,      // 200 (fused Pwelch)
                 Spec<16, 20>,         // 320 (fused Pwelch)
-                Spec<12, 2, 4, 12>)   // 1152 (fused Pwelch)
+                Spec<12, 2, 4, 12>,   // 1152 (fused Pwelch)
+                Spec<7, 7, 15>,       // 735 (fused Pwelch)
+                Spec<15, 4, 15>)      // 900 (fused Pwelch)
