@@ -1284,6 +1284,9 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
       // LDS and the next pair prefetched had gone 3.16 -> 3.11 ms)
       return launch_pwelch_row4096(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
     }
+    // (F = 8192 held to four waves per SIMD with the window read from L1/L2,
+    // two workgroups per CU at 128 VGPRs and 62 spilled: 1.64-1.65 against
+    // 1.16-1.17 ms per 2^28 samples; scripts/gpu_r05_h13.sh)
     case 13: return launch_pwh_t<13>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
     // F = 16384: the exchange buffer alone takes 136 KiB, so the window is
     // re-read from L1/L2 instead of living in LDS
