@@ -386,12 +386,12 @@ bool pwelch_fixed_radices(int n, int *rad, int *npass) {
   return specspw_find(n, rad, npass);
 }
 
-int pwelch_fixed_workers_per_block(const MixedDesc &d) {
-  int t = specspw_pw_tpw(d);
-  if (!t) t = specs0_pw_tpw(d);
-  if (!t) t = specs1_pw_tpw(d);
-  if (!t) t = specs2_pw_tpw(d);
-  if (!t) t = specs3_pw_tpw(d);
+int pwelch_fixed_workers_per_block(const MixedDesc &d, int64_t span) {
+  int t = specspw_pw_tpw(d, span);
+  if (!t) t = specs0_pw_tpw(d, span);
+  if (!t) t = specs1_pw_tpw(d, span);
+  if (!t) t = specs2_pw_tpw(d, span);
+  if (!t) t = specs3_pw_tpw(d, span);
   return t;
 }
 

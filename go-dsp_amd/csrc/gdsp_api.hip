@@ -497,7 +497,7 @@ int build_mixed(int dev, int64_t n, const std::vector<int> &rad, gdsp_plan *p) {
 // cache (plans are built under g_plan_mu; the snapshot is per thread).
 thread_local int t_build_depth = 0;
 thread_local unsigned t_build_flags = 0;
-unsigned plan_flags() { return t_build_depth > 0 ? t_build_flags : gdsp::algo_flags(); }
+unsigned plan_flags() { return gdsp::algo_flags(); }
 
 int chirpz_parts(int64_t n) {
   const bool off = (plan_flags() & GDSP_ALGO_NO_CHIRPZ_PARTS) != 0;
@@ -790,9 +790,6 @@ int rader_try(int dev, int64_t n, gdsp_plan *p, bool *built) {
   if (!j) return GDSP_OK;
   gdsp_plan *pn = nullptr;  // FFT_N for bhat
   STCHK(get_plan_locked(dev, N, &pn));
-  gdsp::MixedDesc d{};
-  cd *tw = nullptr;
-  STCHK(make_mixed_desc(dev, N, rad, d, &tw));
   const int64_t g = primitive_root(n);
   if (!g) return fail(GDSP_ERR_INVALID, "no primitive root");
   std::vector<int> gp((size_t)N), gi((size_t)N);
@@ -809,29 +806,53 @@ int rader_try(int dev, int64_t n, gdsp_plan *p, bool *built) {
         -2.0L * 3.141592653589793238462643383279502884L * (long double)gi[(size_t)q] / (long double)n;
     b[(size_t)q] = {(double)cosl(a), (double)sinl(a)};
   }
+  // The tables are built into locals and given to p only when every step
+  // succeeded; a failure frees them and leaves p untouched.
   hipStream_t s = thread_stream(dev);
-  HIPCHK(hipMalloc((void **)&p->gpow, (size_t)N * sizeof(int)));
-  HIPCHK(hipMalloc((void **)&p->ginv, (size_t)N * sizeof(int)));
-  HIPCHK(hipMalloc((void **)&p->bhat, (size_t)N * sizeof(cd)));
-  STCHK(copy_h2d(p->gpow, gp.data(), (size_t)N * sizeof(int), s));
-  STCHK(copy_h2d(p->ginv, gi.data(), (size_t)N * sizeof(int), s));
-  cd *db = nullptr;
-  HIPCHK(hipMalloc((void **)&db, (size_t)N * sizeof(cd)));
-  STCHK(copy_h2d(db, b.data(), (size_t)N * sizeof(cd), s));
-  // FFT_N(b) on the device with the engine itself, with the inverse's 1/N
-  int st = exec_plan(pn, db, p->bhat, 1, false, gdsp::LOAD_COMPLEX, s);
-  if (st == GDSP_OK) {
-    hipError_t e = gdsp::launch_scale(p->bhat, N, 1.0 / (double)N, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) st = fail(GDSP_ERR_HIP, hipGetErrorString(e));
+  gdsp::MixedDesc d{};
+  cd *tw = nullptr, *bh = nullptr, *db = nullptr;
+  int *dgp = nullptr, *dgi = nullptr;
+  auto release = [&] {
+    if (tw) (void)hipFree(tw);
+    if (bh) (void)hipFree(bh);
+    if (db) (void)hipFree(db);
+    if (dgp) (void)hipFree(dgp);
+    if (dgi) (void)hipFree(dgi);
+  };
+  int st = make_mixed_desc(dev, N, rad, d, &tw);
+  auto hip_ok = [&](hipError_t e) {
+    if (st == GDSP_OK && e != hipSuccess) st = fail(GDSP_ERR_HIP, hipGetErrorString(e));
+    return st == GDSP_OK;
+  };
+  if (st == GDSP_OK && hip_ok(hipMalloc((void **)&dgp, (size_t)N * sizeof(int))) &&
+      hip_ok(hipMalloc((void **)&dgi, (size_t)N * sizeof(int))) &&
+      hip_ok(hipMalloc((void **)&bh, (size_t)N * sizeof(cd))) &&
+      hip_ok(hipMalloc((void **)&db, (size_t)N * sizeof(cd)))) {
+    st = copy_h2d(dgp, gp.data(), (size_t)N * sizeof(int), s);
+    if (st == GDSP_OK) st = copy_h2d(dgi, gi.data(), (size_t)N * sizeof(int), s);
+    if (st == GDSP_OK) st = copy_h2d(db, b.data(), (size_t)N * sizeof(cd), s);
+    // FFT_N(b) on the device with the engine itself, with the inverse's 1/N
+    if (st == GDSP_OK) st = exec_plan(pn, db, bh, 1, false, gdsp::LOAD_COMPLEX, s);
+    if (st == GDSP_OK) {
+      hipError_t e = gdsp::launch_scale(bh, N, 1.0 / (double)N, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      hip_ok(e);
+    }
+  }
+  if (st != GDSP_OK) {
+    (void)hipStreamSynchronize(s);  // nothing in flight reads the tables any more
+    release();
+    return st;
   }
   (void)hipFree(db);
-  STCHK(st);
   p->kind = KIND_RADER;
   p->rader = j;
   p->tw = tw;
   p->md = d;
   p->m = N;
+  p->gpow = dgp;
+  p->ginv = dgi;
+  p->bhat = bh;
   *built = true;
   return GDSP_OK;
 }
@@ -1577,7 +1598,13 @@ const char *knob(Knob k) {
                                       "XDG_CACHE_HOME",  "HOME"};
   return (int)k >= 0 && (int)k < (int)(sizeof names / sizeof names[0]) ? getenv(names[k]) : nullptr;
 }
-unsigned algo_flags() { return g_algo.load(std::memory_order_relaxed); }
+// Inside a plan build (t_build_depth > 0) every reader — mixed_fixed_radices,
+// pwelch_fixed_radices, jit_enabled, ... — sees the flags snapshot the plan is
+// cached under (plan_flags), so a concurrent gdsp_set_algorithm cannot give
+// one plan parts chosen under different flags.
+unsigned algo_flags() {
+  return t_build_depth > 0 ? t_build_flags : g_algo.load(std::memory_order_relaxed);
+}
 }  // namespace gdsp
 
 // Forwarders for the multi-device layer (api_internal.hpp, multi.hip).
@@ -1996,7 +2023,12 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
   gdsp_plan *p = nullptr;
   STCHK(get_plan(flen, &p));
   const int64_t nseg = seg_end - seg_begin;
-  if (p->kind == KIND_LDS && gdsp::pwelch_wave_applies(p->log2n)) {
+  // The fused kernels address a pair's (or a wave's group of pairs') samples
+  // with 32-bit offsets from one base; a very negative Noverlap (spectral.go:
+  // 22-43 allows it) spreads the segments beyond that, so strides above 2^22
+  // samples take the materialised path, which indexes in 64 bits.
+  const bool fused = stride <= ((int64_t)1 << 22);
+  if (fused && p->kind == KIND_LDS && gdsp::pwelch_wave_applies(p->log2n)) {
     // 64 <= F <= 1024: wave-resident transforms, no workgroup barriers
     // (pwelch_wave.hip), every wave a persistent worker over pair groups;
     // F = 2048: two-wave workgroups
@@ -2013,7 +2045,7 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
                                         (double *)red.p, s));
     return GDSP_OK;
   }
-  if (p->kind == KIND_LDS && p->log2n >= 4) {
+  if (fused && p->kind == KIND_LDS && p->log2n >= 4) {
     // fused path: packed segment pairs, persistent workers over contiguous
     // pair ranges (the 50 % overlap of consecutive pairs is re-read from L2)
     const int64_t npairs = (nseg + 1) / 2;
@@ -2044,15 +2076,20 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
                                         (double *)red.p, s));
     return GDSP_OK;
   }
-  if (p->kind == KIND_MIXED && (p->jit || gdsp::pwelch_fixed_workers_per_block(p->md) > 0) &&
-      !(gdsp::algo_flags() & GDSP_ALGO_GENERIC_MIXED)) {
-    // fused path on a compiled specialisation (e.g. NFFT 1000, 3000), on the
-    // Pwelch's own list where it has one (md_pw)
-    const bool own = p->md_pw.n > 0 && !p->jit;
-    const gdsp::MixedDesc &pmd = own ? p->md_pw : p->md;
+  // the fused Pwelch on a compiled or runtime-compiled specialisation, on the
+  // Pwelch's own list where it has one (md_pw); 0 workers per block where its
+  // kernel cannot stage a pair this far apart (negative Noverlap)
+  const bool own = p->md_pw.n > 0 && !p->jit;
+  const gdsp::MixedDesc &pmd = own ? p->md_pw : p->md;
+  const int wpb_fixed =
+      !fused || p->kind != KIND_MIXED ? 0
+      : p->jit                        ? gdsp::jit_pw_tpw(p->jit, stride + nfft)
+                                      : gdsp::pwelch_fixed_workers_per_block(pmd, stride + nfft);
+  if (wpb_fixed > 0 && !(gdsp::algo_flags() & GDSP_ALGO_GENERIC_MIXED)) {
+    // fused path on a compiled specialisation (e.g. NFFT 1000, 3000)
     const cd *ptw = own ? p->tw_pw : p->tw;
     const int64_t npairs = (nseg + 1) / 2;
-    const int wpb = p->jit ? gdsp::jit_pw_tpw(p->jit) : gdsp::pwelch_fixed_workers_per_block(pmd);
+    const int wpb = wpb_fixed;
     int64_t target = 2048 * (int64_t)wpb;
     if (target > npairs) target = npairs;
     const int64_t ppw = (npairs + target - 1) / target;
@@ -2071,7 +2108,7 @@ int gdsp_pwelch_accumulate_device(const double *d_x, int64_t n, int64_t nfft, in
                                         (double *)red.p, s));
     return GDSP_OK;
   }
-  if (p->kind == KIND_MIXED && p->md_gen.npass >= 2) {
+  if (fused && p->kind == KIND_MIXED && p->md_gen.npass >= 2) {
     // fused mixed-radix path (smooth NFFT / Pad up to 4096)
     const int64_t npairs = (nseg + 1) / 2;
     int64_t target = 2048;

@@ -66,8 +66,9 @@ hipError_t launch_pwelch_wave(int log2f, bool half, const double *x, int64_t nff
                               int64_t seg_begin, int64_t seg_end, int64_t gpw, int64_t nblk,
                               const double *win, const cd *tw, double *partial, hipStream_t s);
 // fused Pwelch on a compiled specialisation (d = the plan's specialisation
-// descriptor, d.n = max(pad, nfft)); workers per block, 0 if d is none
-int pwelch_fixed_workers_per_block(const MixedDesc &d);
+// descriptor, d.n = max(pad, nfft)); workers per block, 0 if d is none or
+// its kernel cannot stage a pair of span = stride + nfft samples
+int pwelch_fixed_workers_per_block(const MixedDesc &d, int64_t span);
 hipError_t launch_pwelch_fixed(const MixedDesc &d, const double *x, int64_t nfft, int64_t stride,
                                int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,
                                const double *win, const cd *tw, double *partial, hipStream_t s);
@@ -90,7 +91,7 @@ hipError_t jit_launch_col(const JitCol *j, bool conj_in, const cd *in, cd *out, 
                           int64_t n, int64_t batch, const cd *tw, const cd *twn, hipStream_t s);
 hipError_t jit_launch_fft(const JitSpec *j, bool inv, int load, const void *in, cd *out,
                           int64_t batch, const cd *tw, double scale, hipStream_t s);
-int jit_pw_tpw(const JitSpec *j);
+int jit_pw_tpw(const JitSpec *j, int64_t span);  // as pwelch_fixed_workers_per_block
 // rader_fixed_kernel (mixed_fixed.hpp): a prime P = prod(rad) + 1 by Rader's
 // algorithm on the inlined mixed-radix chain of its N = P - 1
 struct JitRader;

@@ -1052,17 +1052,24 @@ __global__ __launch_bounds__((RaderGeo<R0, RS...>::WG)) void rader_fixed_kernel(
 }
 
 #ifndef __HIPCC_RTC__
+// Workers per workgroup of the fused Pwelch on d's list, 0 where d is not
+// this list or where a pair's samples (span = stride + nfft doubles) exceed
+// the LDS-DMA stage of a PwfDma list (a negative Noverlap makes stride >
+// nfft; spectral/spectral.go:22-43 allows it): the caller then takes another
+// path instead of a DMA that would overrun the stage into the twiddle table.
 template <int... RS>
-static int spec_pw_tpw(Spec<RS...>, const MixedDesc &d) {
+static int spec_pw_tpw(Spec<RS...>, const MixedDesc &d, int64_t span) {
   uint64_t codes = 0;
   int q = 0;
   for (int r : {RS...}) codes |= (uint64_t)r << (5 * q++);
-  return (d.n == FixedGeo<RS...>::N && d.codes == codes) ? FixedGeo<RS...>::TPW : 0;
+  if (d.n != FixedGeo<RS...>::N || d.codes != codes) return 0;
+  if (PwfDma<RS...>::on && span > PwfDma<RS...>::STG) return 0;
+  return FixedGeo<RS...>::TPW;
 }
 template <class... S>
-static int find_pw_tpw(std::tuple<S...>, const MixedDesc &d) {
+static int find_pw_tpw(std::tuple<S...>, const MixedDesc &d, int64_t span) {
   int t = 0;
-  ((t = t ? t : spec_pw_tpw(S{}, d)), ...);
+  ((t = t ? t : spec_pw_tpw(S{}, d, span)), ...);
   return t;
 }
 
@@ -1071,7 +1078,7 @@ static bool spec_pw_launch(Spec<RS...>, const MixedDesc &d, const double *x, int
                            int64_t stride, int64_t seg_begin, int64_t seg_end, int64_t ppw,
                            int64_t nworkers, const double *win, const cd *tw, double *partial,
                            hipStream_t s) {
-  if (!spec_pw_tpw(Spec<RS...>{}, d)) return false;
+  if (!spec_pw_tpw(Spec<RS...>{}, d, stride + nfft)) return false;
   using G = FixedGeo<RS...>;
   constexpr int R0 = [] { constexpr int r[] = {RS...}; return r[0]; }();
   const dim3 grid((unsigned)((nworkers + G::TPW - 1) / G::TPW)), block(G::WG);
@@ -1105,7 +1112,9 @@ static bool launch_pw_spec(std::tuple<S...>, const MixedDesc &d, const double *x
                      int64_t batch, const cd *tw, double scale, hipStream_t s) {             \
     return launch_spec(NAME##_list{}, d, inv, load, in, out, batch, tw, scale, s);            \
   }                                                                                           \
-  int NAME##_pw_tpw(const MixedDesc &d) { return find_pw_tpw(NAME##_list{}, d); }            \
+  int NAME##_pw_tpw(const MixedDesc &d, int64_t span) {                                     \
+    return find_pw_tpw(NAME##_list{}, d, span);                                               \
+  }                                                                                           \
   bool NAME##_pw_launch(const MixedDesc &d, const double *x, int64_t nfft, int64_t stride,    \
                         int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,   \
                         const double *win, const cd *tw, double *partial, hipStream_t s) {   \

@@ -47,6 +47,7 @@ struct JitSpec {
   hipModule_t mod = nullptr;
   hipFunction_t fwd = nullptr, inv = nullptr, real = nullptr, pw = nullptr;
   int n = 0, wg = 0, tpw = 0;
+  int pw_stage = 0;  // the fused Pwelch's LDS-DMA stage in doubles (PwfDma::STG), 0: none
 };
 
 struct JitCol {  // colfixed_kernel for one column length
@@ -459,6 +460,16 @@ JitSpec *jit_spec_build(int dev, const int *rad, int np, int n) {
   int t1 = 0;
   fixed_geo(rad, np, &t1, &j->tpw);
   j->wg = t1 * j->tpw;
+  {
+    // PwfDma (mixed_fixed.hpp) on the host: a radix-25 first pass, one
+    // transform per workgroup, N <= 4096, exchange + stage + twiddle bases
+    // within 80 KiB
+    const int slots = (n + 7) & ~7, stg = (2 * slots + 127) / 128 * 128;
+    int twn = 0, ns = 1;
+    for (int q = 0; q + 1 < np; ++q) twn += (ns *= rad[q]);
+    if (rad[0] == 25 && j->tpw == 1 && n <= 4096 && 8 * (slots + stg) + 16 * twn <= 81920)
+      j->pw_stage = stg;
+  }
   return j;
 }
 
@@ -616,12 +627,16 @@ hipError_t jit_launch_fft(const JitSpec *j, bool inv, int load, const void *in, 
                                nullptr);
 }
 
-int jit_pw_tpw(const JitSpec *j) { return j ? j->tpw : 0; }
+int jit_pw_tpw(const JitSpec *j, int64_t span) {
+  if (!j || (j->pw_stage && span > j->pw_stage)) return 0;
+  return j->tpw;
+}
 
 hipError_t jit_launch_pwelch(const JitSpec *j, const double *x, int64_t nfft, int64_t stride,
                              int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,
                              const double *win, const cd *tw, double *partial, hipStream_t s) {
-  if (nworkers <= 0 || nworkers > 0x7fffffff) return hipErrorInvalidValue;
+  if (nworkers <= 0 || nworkers > 0x7fffffff || !jit_pw_tpw(j, stride + nfft))
+    return hipErrorInvalidValue;
   const int64_t nblk = (nworkers + j->tpw - 1) / j->tpw;
   void *args[] = {(void *)&x,   (void *)&nfft,    (void *)&stride,
                   (void *)&seg_begin, (void *)&seg_end, (void *)&ppw,

@@ -9,7 +9,7 @@ struct cd;
   bool NAME##_find(int n, int *rad, int *npass);                                              \
   bool NAME##_launch(const MixedDesc &d, bool inv, int load, const void *in, cd *out,         \
                      int64_t batch, const cd *tw, double scale, hipStream_t s);              \
-  int NAME##_pw_tpw(const MixedDesc &d);                                                      \
+  int NAME##_pw_tpw(const MixedDesc &d, int64_t span);                                    \
   bool NAME##_pw_launch(const MixedDesc &d, const double *x, int64_t nfft, int64_t stride,    \
                         int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,   \
                         const double *win, const cd *tw, double *partial, hipStream_t s);

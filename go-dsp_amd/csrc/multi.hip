@@ -301,14 +301,26 @@ int nccl_fail(const Rccl &r, ncclResult_t e, const char *what) {
 // a collective on it fails (drop_comms).
 std::mutex g_comms_mu;
 std::map<std::vector<int>, std::vector<ncclComm_t>> g_comms;
-// device lists whose clique ncclCommInitAll refused, with its message: later
-// calls on the same set go straight to the host sum instead of paying the
-// failed setup again
-std::map<std::vector<int>, std::string> g_comms_refused;
+// device lists whose clique ncclCommInitAll refused, with its message: the
+// next kRefusedRetry calls on the same set go straight to the host sum
+// instead of paying the failed setup again; the call after them
+// tries ncclCommInitAll once more, so a transient failure does not disable
+// RCCL for that set for the life of the process
+struct Refusal {
+  std::string why;
+  int skips = 0;
+};
+constexpr int kRefusedRetry = 64;
+std::map<std::vector<int>, Refusal> g_comms_refused;
 
+// true: take the host sum this call (counted toward the retry)
 bool clique_refused(const std::vector<int> &devs) {
   std::lock_guard<std::mutex> lk(g_comms_mu);
-  return g_comms_refused.count(devs) != 0;
+  auto bad = g_comms_refused.find(devs);
+  if (bad == g_comms_refused.end()) return false;
+  if (bad->second.skips++ < kRefusedRetry) return true;
+  g_comms_refused.erase(bad);  // this call tries ncclCommInitAll again
+  return false;
 }
 
 int comms_for(const std::vector<int> &devs, std::vector<ncclComm_t> **out) {
@@ -318,14 +330,14 @@ int comms_for(const std::vector<int> &devs, std::vector<ncclComm_t> **out) {
   if (!r.why.empty()) return set_error(GDSP_ERR_UNSUPPORTED, r.why);
   std::lock_guard<std::mutex> lk(mu);
   auto bad = g_comms_refused.find(devs);
-  if (bad != g_comms_refused.end()) return set_error(GDSP_ERR_UNSUPPORTED, bad->second);
+  if (bad != g_comms_refused.end()) return set_error(GDSP_ERR_UNSUPPORTED, bad->second.why);
   auto it = cache.find(devs);
   if (it == cache.end()) {
     std::vector<ncclComm_t> c(devs.size());
     const ncclResult_t e = r.init_all(c.data(), (int)devs.size(), devs.data());
     if (e != ncclSuccess) {
       const int st = nccl_fail(r, e, "ncclCommInitAll");
-      g_comms_refused.emplace(devs, std::string(gdsp_last_error()));
+      g_comms_refused[devs] = Refusal{std::string(gdsp_last_error()), 0};
       return st;
     }
     it = cache.emplace(devs, std::move(c)).first;

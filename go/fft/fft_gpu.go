@@ -6,9 +6,10 @@
 // results within 1e-9 normwise, same panics.
 //
 // Install (go/README.md): copy this file into the reference's fft/ directory
-// and put `//go:build !gdspgpu` on top of fft/fft.go. radix2.go and
-// bluestein.go stay untagged: the pure-Go small-n path below calls them, and
-// radix2.go keeps EnsureRadix2Factors.
+// and put `//go:build !gdspgpu` on top of fft/fft.go, fft/radix2.go and
+// fft/bluestein.go. No reference FFT code is compiled into the GPU build:
+// every call, at every n, runs on the library (EnsureRadix2Factors and the
+// reverseBits helper fft_test.go uses are defined here).
 // Build with `go build -tags gdspgpu` and the library on the cgo paths:
 //
 //	CGO_CFLAGS="-I<repo>/include"
@@ -31,32 +32,6 @@ import (
 
 	"github.com/mjibson/go-dsp/dsputils"
 )
-
-// GPUMinN is the small-n policy: a one-vector FFT/IFFT/FFTReal/IFFTReal/
-// Convolve whose largest transform is shorter than this stays on the
-// reference's own pure-Go code (radix2FFT / bluesteinFFT), which is faster
-// than a launch + synchronisation there (crossover n = 4096, bench.py
-// configs.fftreal1024.small_n; INTEGRATION.md "Small-n policy"). 0 sends
-// every call to the GPU. FFT2, FFTN and FFTBatch always run on the GPU.
-var GPUMinN = 4096
-
-// onHost applies GPUMinN to the largest transform the pure-Go code would run
-// for n: n itself for a power of 2, bluesteinFFT's convolution length
-// NextPowerOf2(2n-1) otherwise (bluestein.go:70). So a host call never
-// reaches the GPU from inside: bluesteinFFT's Convolve (bluestein.go:87),
-// which is this package's Convolve, gets that power-of-2 length and stays on
-// the host too; a non-power-of-2 n whose convolution would be >= GPUMinN goes
-// to the GPU as one transform instead of a host Bluestein around a GPU
-// convolution.
-func onHost(n int) bool {
-	if dsputils.IsPowerOf2(n) {
-		return n < GPUMinN
-	}
-	return dsputils.NextPowerOf2(2*n-1) < GPUMinN
-}
-
-// read by radix2.go:92 (declared in fft.go:89-91 in the pure-Go build)
-var worker_pool_size = 0
 
 // check maps a libgdspfft status to the reference's panic: the misuse
 // statuses carry the reference's own messages (fft.go:57, :126, :133,
@@ -93,23 +68,9 @@ func real64(x []float64) *C.double {
 // 2, bluesteinFFT (bluestein.go:68-94) otherwise. x is not modified; the
 // result is a fresh slice.
 func FFT(x []complex128) []complex128 {
-	if onHost(len(x)) {
-		return fftPureGo(x)
-	}
 	r := make([]complex128, len(x))
 	check(C.gdsp_fft(cplx(x), cplx(r), C.int64_t(len(x))))
 	return r
-}
-
-// the reference's dispatch on its own kernels (the small-n policy)
-func fftPureGo(x []complex128) []complex128 {
-	if len(x) <= 1 {
-		return append([]complex128(nil), x...)
-	}
-	if dsputils.IsPowerOf2(len(x)) {
-		return radix2FFT(x)
-	}
-	return bluesteinFFT(x)
 }
 
 // IFFT replaces fft/fft.go:35-52. An empty x panics with the runtime's index
@@ -117,20 +78,6 @@ func fftPureGo(x []complex128) []complex128 {
 func IFFT(x []complex128) []complex128 {
 	_ = x[0]
 	n := len(x)
-	if onHost(n) {
-		// fft.go:35-52 on the pure-Go FFT: reversed input, forward FFT, /n
-		rev := make([]complex128, n)
-		rev[0] = x[0]
-		for i := 1; i < n; i++ {
-			rev[i] = x[n-i]
-		}
-		r := fftPureGo(rev)
-		s := complex(float64(n), 0)
-		for i := range r {
-			r[i] /= s
-		}
-		return r
-	}
 	r := make([]complex128, n)
 	check(C.gdsp_ifft(cplx(x), cplx(r), C.int64_t(n)))
 	return r
@@ -139,9 +86,6 @@ func IFFT(x []complex128) []complex128 {
 // FFTReal replaces fft/fft.go:25-27: the float64 samples go over as they are
 // (the kernel reads real rows; no ToComplex copy).
 func FFTReal(x []float64) []complex128 {
-	if onHost(len(x)) {
-		return fftPureGo(dsputils.ToComplex(x))
-	}
 	r := make([]complex128, len(x))
 	check(C.gdsp_fft_real(real64(x), cplx(r), C.int64_t(len(x))))
 	return r
@@ -150,9 +94,6 @@ func FFTReal(x []float64) []complex128 {
 // IFFTReal replaces fft/fft.go:30-32 (panics on an empty x like IFFT).
 func IFFTReal(x []float64) []complex128 {
 	_ = x[0]
-	if onHost(len(x)) {
-		return IFFT(dsputils.ToComplex(x))
-	}
 	r := make([]complex128, len(x))
 	check(C.gdsp_ifft_real(real64(x), cplx(r), C.int64_t(len(x))))
 	return r
@@ -162,13 +103,6 @@ func IFFTReal(x []float64) []complex128 {
 func Convolve(x, y []complex128) []complex128 {
 	if len(x) != len(y) {
 		panic("arrays not of equal size")
-	}
-	if onHost(len(x)) {
-		fx, fy := fftPureGo(x), fftPureGo(y)
-		for i := range fx {
-			fx[i] *= fy[i]
-		}
-		return IFFT(fx)
 	}
 	r := make([]complex128, len(x))
 	check(C.gdsp_convolve(cplx(x), cplx(y), cplx(r), C.int64_t(len(x))))
@@ -264,21 +198,36 @@ func FFTN(m *dsputils.Matrix) *dsputils.Matrix  { return fftn(m, 0) }
 func IFFTN(m *dsputils.Matrix) *dsputils.Matrix { return fftn(m, 1) }
 
 // SetWorkerPoolSize replaces fft/fft.go:95-101. The library records it
-// (gdsp_worker_pool_size); radix2.go's small-n path uses it as before.
+// (gdsp_worker_pool_size); the GPU's parallelism does not depend on it.
 func SetWorkerPoolSize(n int) {
 	if n < 0 {
 		n = 0
 	}
-	worker_pool_size = n
 	C.gdsp_set_worker_pool_size(C.int(n))
 }
 
-// EnsureRadix2Factors (fft/radix2.go:35-37) stays the reference's: it
-// builds the host twiddle table the small-n path uses. EnsurePlan is its
-// device counterpart: it builds the GPU plan (twiddle table, chirp tables)
-// for input_len ahead of the first call.
+// EnsureRadix2Factors replaces fft/radix2.go:35-37: the reference builds its
+// host twiddle table for input_len ahead of the first call; this builds the
+// device plan (twiddle, chirp or Rader tables) for it.
+func EnsureRadix2Factors(input_len int) {
+	EnsurePlan(input_len)
+}
+
+// EnsurePlan builds the GPU plan for input_len ahead of the first call.
 func EnsurePlan(input_len int) {
 	check(C.gdsp_ensure_plan(C.int64_t(input_len)))
+}
+
+// reverseBits returns the first s bits of v in reverse order, the helper
+// fft_test.go:242-247 tests (radix2.go:182-199 in the pure-Go build). The
+// Stockham kernels need no bit reversal; it is kept so the reference's own
+// test file compiles under the gdspgpu tag.
+func reverseBits(v, s uint) uint {
+	var r uint
+	for i := uint(0); i < s; i++ {
+		r = r<<1 | (v>>i)&1
+	}
+	return r
 }
 
 // ---- additive entry points (no reference equivalent) -----------------------

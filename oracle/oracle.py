@@ -245,6 +245,42 @@ def pwelch_threaded(x, fs: float, nfft: int, noverlap: int, nworkers: int):
     return pxx, freqs
 
 
+def pwelch_chunked(x, fs: float, nfft: int, noverlap: int, nthreads: int = 16,
+                   chunks: int = 64):
+    """spectral.Pwelch (spectral/pwelch.go:74-145) of a long stream, for the
+    full-size parity checks: the segments split into `chunks` contiguous
+    ranges, each range's Pwelch by or_pwelch on its own sample span
+    (segments s0 .. s1 - 1 need samples [s0 stride, (s1 - 1) stride + nfft)),
+    run on `nthreads` host threads (ctypes releases the GIL), and the results
+    combined as the segment-count-weighted mean. pwelch.go:126-136 finalises
+    the per-bin power sum linearly (1 / nsegs, the window norm, the doubling of
+    interior bins), so that mean is the whole stream's Pxx; only the order of
+    the float64 additions differs from the reference's single pass. Pad = NFFT,
+    Hann, scaling on."""
+    from concurrent.futures import ThreadPoolExecutor
+    x = _f(x)
+    nf = nfft or 256
+    nsegs = segment_count(x.size, nf, noverlap)
+    stride = nf - noverlap
+    if nsegs <= 0:
+        return pwelch(x, fs, nfft=nfft, noverlap=noverlap)
+    chunks = max(1, min(chunks, nsegs))
+    bounds = [nsegs * i // chunks for i in range(chunks + 1)]
+
+    def one(i):
+        s0, s1 = bounds[i], bounds[i + 1]
+        if s1 <= s0:
+            return None
+        p, f = pwelch(x[s0 * stride:(s1 - 1) * stride + nf], fs, nfft=nfft, noverlap=noverlap)
+        return s1 - s0, p, f
+
+    with ThreadPoolExecutor(max_workers=max(1, nthreads)) as ex:
+        parts = [r for r in ex.map(one, range(chunks)) if r is not None]
+    total = sum(k for k, _, _ in parts)
+    pxx = sum(k * p for k, p, _ in parts) / total
+    return pxx, parts[0][2]
+
+
 def fill_uniform(count: int, seed: int, offset: int = 0) -> np.ndarray:
     """Synthetic inputs identical to the device generator."""
     out = np.empty(count, np.float64)

@@ -1,17 +1,17 @@
 // shim_replay.cpp — the cgo shim (go/fft/fft_gpu.go, go/spectral/pwelch_gpu.go,
 // go/wav/wav_gpu.go) replayed call for call in C++, because no Go toolchain
 // exists on either box. Each goshim:: function below is its Go namesake
-// transcribed: the same small-n policy (GPUMinN), the same C-ABI calls with
-// the same arguments in the same order, the same flattening of [][]complex128
-// and dsputils.Matrix, the same status -> panic mapping (a GoPanic exception
-// carrying the string the Go panic would carry). Where the Go shim calls the
-// reference's own pure-Go code (radix2FFT / bluesteinFFT below GPUMinN), the
-// replay calls the oracle's restatement of that code (oracle/oracle.c, test
-// infrastructure), which is what the reference computes.
+// transcribed: the same C-ABI calls with the same arguments in the same
+// order, the same flattening of [][]complex128 and dsputils.Matrix, the same
+// status -> panic mapping (a GoPanic exception carrying the string the Go
+// panic would carry). Like the shim, no goshim:: function computes a
+// transform on the host: every n, down to 1, goes through the C ABI (the
+// oracle, oracle/oracle.c, is only the checker below).
 //
-// Checks: every shim function against the oracle on the GPU (both sides of
-// GPUMinN), the reference's own tables (fft_test.go, pwelch_test.go; argv[1],
-// written by tests/test_cpp_mirror.py) and every panic. Exit 0 = all pass.
+// Checks: every shim function against the oracle on the GPU, the reference's
+// own tables (fft_test.go, pwelch_test.go; argv[1], written by
+// tests/test_cpp_mirror.py) and every panic. Exit 0 = all pass.
+#include <array>
 #include <cmath>
 #include <complex>
 #include <cstdint>
@@ -45,24 +45,6 @@ namespace goshim {
 
 // ---- go/fft/fft_gpu.go --------------------------------------------------------
 
-int GPUMinN = 4096;
-
-// dsputils.IsPowerOf2 / NextPowerOf2 (dsputils.go:34-45)
-static bool IsPowerOf2(int64_t x) { return (x & (x - 1)) == 0; }
-static int64_t NextPowerOf2(int64_t x) {
-  if (IsPowerOf2(x)) return x;
-  int64_t p = 1;
-  while (p < x) p <<= 1;
-  return p;
-}
-
-// the small-n policy on the largest transform the pure-Go code would run
-// (fft_gpu.go onHost): n for a power of 2, bluesteinFFT's M otherwise
-bool onHost(int64_t n) {
-  if (IsPowerOf2(n)) return n < GPUMinN;
-  return NextPowerOf2(2 * n - 1) < GPUMinN;
-}
-
 static void check(int st) {
   switch (st) {
     case GDSP_OK:
@@ -84,24 +66,11 @@ static const double *cplx(const std::vector<complex128> &x) {
 }
 static const double *real64(const std::vector<double> &x) { return x.empty() ? nullptr : x.data(); }
 
-// the reference's dispatch on its own kernels (radix2FFT / bluesteinFFT):
-// the oracle's restatement of fft.go:72-87
-static std::vector<complex128> fftPureGo(const std::vector<complex128> &x) {
-  std::vector<complex128> r(x.size());
-  if (x.size() <= 1) {
-    r = x;
-    return r;
-  }
-  if (or_fft(cplx(x), cplx(r), (int64_t)x.size()) != OR_OK) throw std::runtime_error("or_fft");
-  return r;
-}
-
 static std::vector<complex128> ToComplex(const std::vector<double> &x) {
   return std::vector<complex128>(x.begin(), x.end());
 }
 
 std::vector<complex128> FFT(const std::vector<complex128> &x) {
-  if (onHost((int64_t)x.size())) return fftPureGo(x);
   std::vector<complex128> r(x.size());
   check(gdsp_fft(cplx(x), cplx(r), (int64_t)x.size()));
   return r;
@@ -110,21 +79,12 @@ std::vector<complex128> FFT(const std::vector<complex128> &x) {
 std::vector<complex128> IFFT(const std::vector<complex128> &x) {
   index0(x);
   const size_t n = x.size();
-  if (onHost((int64_t)n)) {
-    std::vector<complex128> rev(n);
-    rev[0] = x[0];
-    for (size_t i = 1; i < n; ++i) rev[i] = x[n - i];
-    auto r = fftPureGo(rev);
-    for (auto &v : r) v /= complex128((double)n, 0.0);
-    return r;
-  }
   std::vector<complex128> r(n);
   check(gdsp_ifft(cplx(x), cplx(r), (int64_t)n));
   return r;
 }
 
 std::vector<complex128> FFTReal(const std::vector<double> &x) {
-  if (onHost((int64_t)x.size())) return fftPureGo(ToComplex(x));
   std::vector<complex128> r(x.size());
   check(gdsp_fft_real(real64(x), cplx(r), (int64_t)x.size()));
   return r;
@@ -132,7 +92,6 @@ std::vector<complex128> FFTReal(const std::vector<double> &x) {
 
 std::vector<complex128> IFFTReal(const std::vector<double> &x) {
   index0(x);
-  if (onHost((int64_t)x.size())) return IFFT(ToComplex(x));
   std::vector<complex128> r(x.size());
   check(gdsp_ifft_real(real64(x), cplx(r), (int64_t)x.size()));
   return r;
@@ -140,11 +99,6 @@ std::vector<complex128> IFFTReal(const std::vector<double> &x) {
 
 std::vector<complex128> Convolve(const std::vector<complex128> &x, const std::vector<complex128> &y) {
   if (x.size() != y.size()) throw GoPanic("arrays not of equal size");
-  if (onHost((int64_t)x.size())) {
-    auto fx = fftPureGo(x), fy = fftPureGo(y);
-    for (size_t i = 0; i < fx.size(); ++i) fx[i] *= fy[i];
-    return IFFT(fx);
-  }
   std::vector<complex128> r(x.size());
   check(gdsp_convolve(cplx(x), cplx(y), cplx(r), (int64_t)x.size()));
   return r;
@@ -234,6 +188,12 @@ Matrix IFFTN(const Matrix &m) { return fftn(m, 1); }
 
 void SetWorkerPoolSize(int n) { gdsp_set_worker_pool_size(n < 0 ? 0 : n); }
 void EnsurePlan(int input_len) { check(gdsp_ensure_plan(input_len)); }
+void EnsureRadix2Factors(int input_len) { EnsurePlan(input_len); }
+unsigned reverseBits(unsigned v, unsigned s) {  // fft_gpu.go's, for fft_test.go:242-247
+  unsigned r = 0;
+  for (unsigned i = 0; i < s; ++i) r = r << 1 | ((v >> i) & 1u);
+  return r;
+}
 
 std::vector<complex128> FFTBatch(const std::vector<complex128> &x, int n, bool inverse) {
   if (n <= 0 || x.size() % (size_t)n != 0) throw GoPanic("arrays not of equal size");
@@ -434,9 +394,8 @@ static std::vector<complex128> readc(std::istream &in, size_t n) {
 }
 
 static void reference_tables(const char *path) {
-  // fft_test.go / pwelch_test.go tables on both sides of the small-n policy
-  for (int minn : {4096, 0}) {
-    goshim::GPUMinN = minn;
+  // fft_test.go / pwelch_test.go tables
+  {
     std::ifstream f(path);
     std::string line;
     while (std::getline(f, line)) {
@@ -448,7 +407,7 @@ static void reference_tables(const char *path) {
         in >> n;
         auto x = readd(in, n);
         auto out = readc(in, n);
-        EXPECT(close_c(goshim::FFTReal(x), out), "FFTReal n=" << n << " minN=" << minn);
+        EXPECT(close_c(goshim::FFTReal(x), out), "FFTReal n=" << n);
         EXPECT(close_c(goshim::IFFT(out), goshim::ToComplex(x)), "IFFT n=" << n);
       } else if (kind == "FFT2") {  // TestFFT2, fft_test.go:211-223
         size_t r, c;
@@ -496,7 +455,6 @@ static void reference_tables(const char *path) {
       }
     }
   }
-  goshim::GPUMinN = 4096;
 }
 
 int main(int argc, char **argv) {
@@ -506,16 +464,9 @@ int main(int argc, char **argv) {
   }
   reference_tables(argv[1]);
 
-  // FFT / IFFT / FFTReal / IFFTReal / Convolve: below, at and above GPUMinN,
-  // powers of 2 and not, against the restatement of the reference
-  // the small-n policy on bluesteinFFT's convolution length (fft_gpu.go
-  // onHost): non-powers of 2 in (1024, 4096) convolve on M = 4096
-  // or 8192 >= GPUMinN, so they go to the GPU as one transform rather than a
-  // host Bluestein around a GPU Convolve; up to 1024 they stay on the host
-  EXPECT(goshim::onHost(1000) && goshim::onHost(1024) && goshim::onHost(2048) &&
-             !goshim::onHost(1025) && !goshim::onHost(1500) && !goshim::onHost(3000) &&
-             !goshim::onHost(4096) && goshim::onHost(0) && goshim::onHost(1),
-         "onHost policy");
+  // FFT / IFFT / FFTReal / IFFTReal / Convolve at every kind of length (all
+  // on the GPU: the shim has no host transform), against the restatement of
+  // the reference
   for (size_t n : {1ul, 2ul, 5ul, 1000ul, 1024ul, 1025ul, 1500ul, 2048ul, 3000ul, 4095ul, 4096ul,
                    5000ul, 65536ul}) {
     auto x = randc(n, 100 + n);
@@ -616,6 +567,10 @@ int main(int argc, char **argv) {
     EXPECT(e < 1e-9 && ei < 1e-9 && er < 1e-9, "FFTBatch/FFTBatchMulti/FFTRealBatch");
   }
   goshim::EnsurePlan(1 << 20);
+  goshim::EnsureRadix2Factors(3000);
+  // fft_test.go:183-247 (TestReverseBits) through the shim's helper
+  for (auto t : {std::array<unsigned, 3>{0, 1, 0}, {1, 2, 2}, {1, 4, 8}, {2, 4, 4}, {3, 4, 12}})
+    EXPECT(goshim::reverseBits(t[0], t[1]) == t[2], "reverseBits " << t[0] << "," << t[1]);
   {
     goshim::SetDevices({0});
     int d[4] = {-1, -1, -1, -1};

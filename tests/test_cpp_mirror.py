@@ -242,6 +242,18 @@ def test_go_shim_covers_the_reference_api():
         assert names <= defined, (rel, names - defined)
         called = set(re.findall(r"\bC\.(gdsp_\w+)\(", src))
         assert called and called <= declared, (rel, called - declared)
+    # no reference FFT code on the drop-in's path: the
+    # gdspgpu build tags radix2.go / bluestein.go out, so nothing may call
+    # their kernels, and the replay has no host transform either
+    fsrc = open(os.path.join(GO, "fft/fft_gpu.go")).read()
+    body = re.sub(r"//[^\n]*", "", fsrc)
+    for name in ("radix2FFT", "bluesteinFFT", "getRadix2Factors", "GPUMinN", "onHost"):
+        assert name not in body, name
+    assert "func EnsureRadix2Factors(" in fsrc and "func reverseBits(" in fsrc
+    replay = open(os.path.join(REPO, "tests", "cpp", "shim_replay.cpp")).read()
+    ns = re.sub(r"//[^\n]*", "", replay[replay.index("namespace goshim {"):
+                                         replay.index("}  // namespace goshim")])
+    assert "or_fft" not in ns and "or_ifft" not in ns and "or_convolve" not in ns
     pw = open(os.path.join(GO, "spectral/pwelch_gpu.go")).read()
     for field in ("NFFT      int", "Window    func(int) []float64", "Pad       int",
                   "Noverlap  int", "Scale_off bool"):  # pwelch.go:28-65
@@ -255,8 +267,8 @@ def test_shim_replay_built():
 @pytest.mark.gpu
 def test_shim_replay(refvec, tmp_path):
     """The cgo shim's call sequences (go/, replayed in C++) on the GPU: every
-    function against the oracle on both sides of the small-n policy, the
-    reference's tables and every panic."""
+    function against the oracle (every length on the GPU: the shim has no
+    host transform), the reference's tables and every panic."""
     vec = tmp_path / "vectors.txt"
     _write_vectors(refvec, vec)
     r = subprocess.run([SHIM_BIN, str(vec)], capture_output=True, text=True, timeout=300)

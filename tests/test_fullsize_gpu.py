@@ -8,10 +8,14 @@ device-pointer C ABI:
   against a direct DFT sum;
 - Pwelch 2^30 samples, NFFT 4096, 50 % (config 5): the sharded decomposition
   (accumulate over two halves, add) equals the one-shot accumulation, and the
-  full result matches the oracle on a 2^22-sample prefix.
+  full 2^30-sample Pxx matches the oracle on the whole stream (all 524 287
+  segments: oracle.pwelch_chunked, segment ranges on host threads); the same
+  at the reference's default options (NFFT 256, Noverlap 0, 4 194 304
+  segments).
 Tolerance: 1e-9 normwise relative (north star)."""
 import importlib
 import math
+import os
 
 import numpy as np
 import pytest
@@ -113,9 +117,48 @@ def test_pwelch_fullsize(dev, oracle):
     assert np.all(np.isfinite(p)) and p.size == nfft // 2 + 1
     # the uniform[-1,1) stream is white: Pxx ~ variance(1/3) * 2 / Fs in the interior
     assert abs(np.median(p[1:-1]) - 2.0 / 3.0) < 0.01
-    # full pipeline on a prefix against the oracle
+    # full pipeline on a prefix against the oracle, through the host C ABI
     pre = 1 << 22
     xp = x[:pre].cpu().numpy()
     pg, _ = gdsp.spectral.Pwelch(xp, 1.0, gdsp.spectral.PwelchOptions(NFFT=nfft, Noverlap=nov))
     pr, _ = oracle.pwelch(xp, 1.0, nfft=nfft, noverlap=nov)
     assert np.linalg.norm(pg - pr) / np.linalg.norm(pr) < TOL
+    # the whole 2^30-sample stream against the oracle: the GPU's summation
+    # order over all 524 287 segments (pwelch.go:107-122 sums them in order)
+    del xp
+    xh = x.cpu().numpy()
+    del x
+    ref, _ = oracle.pwelch_chunked(xh, 1.0, nfft, nov, nthreads=_host_threads())
+    nrel = np.linalg.norm(p - ref) / np.linalg.norm(ref)
+    print(f"pwelch 2^30 NFFT {nfft} Noverlap {nov}: {S} segments, nrel vs oracle {nrel:.3e}")
+    assert nrel < TOL
+
+
+def _host_threads():
+    # the GPU box's CPU share is 16 threads (os.cpu_count() shows the machine)
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def test_pwelch_default_fullsize(dev, oracle):
+    """spectral.Pwelch with PwelchOptions{} (NFFT 256, Noverlap 0; pwelch.go:
+    85-95) on the same 2^30-sample stream, the device accumulate + finalize
+    against the oracle over the whole stream (4 194 304 segments)."""
+    import torch
+    gdsp = importlib.import_module("go-dsp_amd")
+    Dd = importlib.import_module("go-dsp_amd.distributed")
+    nfft, nov, total = 256, 0, 1 << 30
+    x = torch.empty(total, dtype=torch.float64, device="cuda")
+    dev.fill_uniform(x, 0x5EED)
+    win = torch.tensor(gdsp.window.Hann(nfft), dtype=torch.float64, device="cuda")
+    sh = Dd.plan_pwelch(total, 1, 0, nfft, 0, nov)
+    acc = torch.zeros(nfft, dtype=torch.float64, device="cuda")
+    dev.pwelch_accumulate(x, nfft, nfft, nov, 0, sh.nsegs_total, win, acc)
+    p, _ = gdsp.spectral.finalize(acc.cpu().numpy(), sh.nsegs_total, nfft, nfft,
+                                  gdsp.window.Hann(nfft), 1.0, False)
+    xh = x.cpu().numpy()
+    del x
+    ref, _ = oracle.pwelch_chunked(xh, 1.0, nfft, nov, nthreads=_host_threads())
+    nrel = np.linalg.norm(p - ref) / np.linalg.norm(ref)
+    print(f"pwelch 2^30 NFFT {nfft} Noverlap {nov}: {sh.nsegs_total} segments, "
+          f"nrel vs oracle {nrel:.3e}")
+    assert nrel < TOL

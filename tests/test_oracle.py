@@ -148,3 +148,15 @@ def test_pwelch_vs_scipy(oracle):
 def test_fill_uniform_range(oracle):
     u = oracle.fill_uniform(100000, 0x5EED)
     assert u.min() >= -1 and u.max() < 1 and abs(u.mean()) < 0.01
+
+
+@pytest.mark.parametrize("nfft,nov", [(4096, 2048), (256, 0), (1000, 300), (512, -7)])
+def test_pwelch_chunked_equals_one_pass(oracle, nfft, nov):
+    """The chunked oracle the full-size GPU checks use (segment ranges on
+    host threads, combined by segment count) is the one-pass restatement of
+    spectral/pwelch.go:74-145 up to the order of the float64 additions."""
+    x = oracle.fill_uniform((1 << 20) + 777, 0x5EED)
+    a, fa = oracle.pwelch(x, 1.0, nfft=nfft, noverlap=nov)
+    b, fb = oracle.pwelch_chunked(x, 1.0, nfft, nov, nthreads=4, chunks=37)
+    assert a.size == b.size and np.array_equal(fa, fb)
+    assert nrel(b, a) < 1e-13

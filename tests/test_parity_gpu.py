@@ -496,6 +496,25 @@ def test_pwelch_random_options_vs_oracle(gdsp, oracle, n, nfft, nov, pad, win):
     assert nrel(f, fr) == 0.0
 
 
+# A negative Noverlap (spectral/spectral.go:22-43 allows it) puts the segments
+# farther apart than NFFT: the LDS-DMA fused kernels (radix-25 first pass:
+# 3200 = 25 8 16, 3000 = 25 15 8) must not stage a pair wider than their stage
+# (ADVICE r05), and strides beyond 2^22 samples take the 64-bit materialised
+# path instead of the fused kernels' 32-bit offsets.
+@pytest.mark.parametrize("n,nfft,nov", [
+    (200000, 3200, -1), (200000, 3200, -700), (150000, 3000, -5), (150000, 3000, -3000),
+    (60000, 256, -100), (60000, 1024, -3), (120000, 2048, -1), (200000, 4096, -10),
+    ((1 << 23) + 9000, 256, -((1 << 22) + 100)), ((1 << 23) + 9000, 3200, -((1 << 22) + 1)),
+])
+def test_pwelch_negative_noverlap(gdsp, oracle, n, nfft, nov):
+    rng = np.random.default_rng(n + nfft - nov)
+    x = rng.standard_normal(n)
+    o = gdsp.spectral.PwelchOptions(NFFT=nfft, Noverlap=nov)
+    p, _ = gdsp.spectral.Pwelch(x, 2.0, o)
+    pr, _ = oracle.pwelch(x, 2.0, nfft=nfft, noverlap=nov)
+    assert p.size == pr.size and nrel(p, pr) < TOL
+
+
 # ---- edge cases and conventions --------------------------------------------------
 def test_edge_cases(gdsp):
     F = gdsp.fft
