@@ -97,6 +97,11 @@ __device__ __forceinline__ void r3_dma(const double *x, int64_t seg_begin, int64
 }
 }  // namespace
 
+// FOLD (register count only: tools/pwelch_fold_probe.hip,
+// profiles/r06/pw4096_fold_resusage.txt): 8 folded |Z_k|^2 + |Z_F-k|^2 sums
+// (+ thread 0's bin 2048) instead of 16, through the half buffer per pair, as
+// pwelch_row_kernel's FOLD.
+template <bool FOLD = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void pwelch_row3_kernel(
     const double *__restrict__ x, int64_t seg_begin, int64_t seg_end, int64_t pairs_per_worker,
     const double *__restrict__ win, const cd *__restrict__ tw, double *__restrict__ partial) {
@@ -121,9 +126,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
     for (int k = 0; k < kR3H; ++k) carry[k] = b[k * kR3T];
   }
   r3_dma(x, seg_begin, p0, p0 < nfull, stage, t);
-  double acc[kR3E];
+  constexpr int NACC = FOLD ? kR3H + 1 : kR3E;
+  double acc[NACC];
 #pragma unroll
-  for (int k = 0; k < kR3E; ++k) acc[k] = 0.0;
+  for (int k = 0; k < NACC; ++k) acc[k] = 0.0;
   for (int64_t p = p0; p < pend; ++p) {
     const int tt = opaque_int(t);
     const double *wp = opaque_ptr(win);
@@ -156,18 +162,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
     pass_compute<kR3N, kR3E, kR3T, 16, 16, 0, NoEpi, false, 1, RT, true>(v, tt, rl);
     r3_exchange<16>(v, tt, buf);
     pass_compute<kR3N, kR3E, kR3T, 16, 256, 0, NoEpi, false, 2, RT, true>(v, tt, rl);
+    if constexpr (FOLD) {
+      double pw[kR3E];
 #pragma unroll
-    for (int k = 0; k < kR3E; ++k) acc[k] = fma(v[k].y, v[k].y, fma(v[k].x, v[k].x, acc[k]));
+      for (int k = 0; k < kR3E; ++k) pw[k] = fma(v[k].y, v[k].y, v[k].x * v[k].x);
+      bare_sync();  // the last exchange's reads are done
+#pragma unroll
+      for (int k = kR3H; k < kR3E; ++k) buf[tt * kR3H + (k - kR3H)] = pw[k];
+      bare_sync();
+      if (tt == 0) {
+        acc[0] += pw[0];
+#pragma unroll
+        for (int m = 1; m < kR3H; ++m) acc[m] += pw[m] + buf[kR3H - m];
+        acc[kR3H] += buf[0];
+      } else {
+        const int tp = kR3T - tt;
+#pragma unroll
+        for (int m = 0; m < kR3H; ++m) acc[m] += pw[m] + buf[tp * kR3H + (kR3H - 1 - m)];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kR3E; ++k) acc[k] = fma(v[k].y, v[k].y, fma(v[k].x, v[k].x, acc[k]));
+    }
   }
   double *dst = partial + blockIdx.x * (int64_t)kR3N;
 #pragma unroll
-  for (int k = 0; k < kR3E; ++k) dst[t + k * kR3T] = acc[k];
+  for (int k = 0; k < kR3E; ++k) {
+    if constexpr (FOLD)
+      dst[t + k * kR3T] = k < kR3H ? acc[k] : (t == 0 && k == kR3H ? acc[kR3H] : 0.0);
+    else
+      dst[t + k * kR3T] = acc[k];
+  }
 }
 
 hipError_t launch_pwelch4096_row3(const double *x, int64_t seg_begin, int64_t seg_end, int64_t ppw,
                                   int64_t nworkers, const double *win, const cd *tw,
                                   double *partial, hipStream_t s) {
-  hipLaunchKernelGGL(pwelch_row3_kernel, dim3((unsigned)nworkers), dim3(256), 0, s, x, seg_begin,
+  hipLaunchKernelGGL(pwelch_row3_kernel<false>, dim3((unsigned)nworkers), dim3(256), 0, s, x, seg_begin,
                      seg_end, ppw, win, tw, partial);
   return hipGetLastError();
 }

@@ -295,7 +295,8 @@ int zero_copy_get(ZeroCopy **out) {
 }  // namespace
 
 enum PlanKind { KIND_TRIVIAL = 0, KIND_LDS = 1, KIND_GLOBAL = 2, KIND_BLUESTEIN = 3,
-                KIND_BLUESTEIN_COMPOSED = 4, KIND_MIXED = 5, KIND_MIXED4 = 6, KIND_RADER = 7 };
+                KIND_BLUESTEIN_COMPOSED = 4, KIND_MIXED = 5, KIND_MIXED4 = 6, KIND_RADER = 7,
+                KIND_RADER_PFA = 8 };
 
 struct gdsp_plan {
   int device = 0;
@@ -349,6 +350,9 @@ struct gdsp_plan {
   // bases, bhat = FFT_m(b)/m, gpow[q] = g^q mod n, ginv[r] = g^-r mod n
   gdsp::JitRader *rader = nullptr;
   int *gpow = nullptr, *ginv = nullptr;
+  // prime-factor Rader (KIND_RADER_PFA, n = n1 * n2, n2 a prime with a Rader
+  // plan p2 whose tables the kernel reads, gcd(n1, n2) = 1): rader is
+  // rader_pfa_kernel for the cofactor n1, m = n2 - 1
 };
 
 namespace {
@@ -857,6 +861,44 @@ int rader_try(int dev, int64_t n, gdsp_plan *p, bool *built) {
   return GDSP_OK;
 }
 
+// A composite n <= 8192 whose largest prime factor P > 31 has a Rader plan
+// and whose cofactor M = n / P (gcd(M, P) = 1) has an in-register DFT:
+// rader_pfa_kernel (mixed_fixed.hpp), Good-Thomas over M x P with the M
+// DFT_P as Rader convolutions of length P - 1, one kernel, on the prime P's
+// plan tables; otherwise (*built = false, p untouched) the chirp-z below.
+int pfa_rader_try(int dev, int64_t n, gdsp_plan *p, bool *built) {
+  *built = false;
+  if ((plan_flags() & GDSP_ALGO_NO_RADER) || !gdsp::jit_enabled() || n > gdsp::kMixedSpecMax ||
+      is_prime64(n))
+    return GDSP_OK;
+  int64_t P = 1, m = n;
+  for (int64_t d = 2; d * d <= m; ++d)
+    while (m % d == 0) {
+      P = d;
+      m /= d;
+    }
+  if (m > 1) P = m;  // the largest prime factor
+  const int64_t M = n / P;
+  if (P <= 31 || M % P == 0 || !gdsp::pfa_cofactor_supported((int)M)) return GDSP_OK;
+  gdsp_plan *pp = nullptr;
+  STCHK(get_plan_locked(dev, P, &pp));
+  if (pp->kind != KIND_RADER) return GDSP_OK;
+  int rad[16];
+  const int np = pp->md.npass;
+  if (np < 1 || np > 16) return GDSP_OK;
+  for (int q = 0; q < np; ++q) rad[q] = (int)((pp->md.codes >> (5 * q)) & 31);
+  gdsp::JitRader *j = gdsp::jit_rader_pfa_build(dev, (int)M, rad, np);
+  if (!j) return GDSP_OK;
+  p->kind = KIND_RADER_PFA;
+  p->rader = j;
+  p->p2 = pp;
+  p->n1 = M;
+  p->n2 = P;
+  p->m = P - 1;
+  *built = true;
+  return GDSP_OK;
+}
+
 int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   p->device = dev;
   p->n = n;
@@ -928,6 +970,8 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
   if (!chirpz) {
     bool built = false;
     STCHK(rader_try(dev, n, p, &built));
+    if (built) return GDSP_OK;
+    STCHK(pfa_rader_try(dev, n, p, &built));
     if (built) return GDSP_OK;
   }
   // Bluestein factors, bluestein.go:32-61: w_k = (cos, sin)(Pi/n * k*k),
@@ -1466,6 +1510,12 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
       HIPCHK(gdsp::jit_launch_rader(p->rader, inv, load, in, out, batch, p->tw, p->bhat, p->gpow,
                                     p->ginv, scale, s));
       return GDSP_OK;
+    case KIND_RADER_PFA: {
+      const gdsp_plan *q = p->p2;  // the prime factor's Rader tables
+      HIPCHK(gdsp::jit_launch_rader(p->rader, inv, load, in, out, batch, q->tw, q->bhat, q->gpow,
+                                    q->ginv, scale, s));
+      return GDSP_OK;
+    }
     case KIND_LDS:
       HIPCHK(gdsp::launch_fft_lds(p->log2n, inv, load, lds_split_default(), in, out, batch, p->tw,
                                   scale, s));

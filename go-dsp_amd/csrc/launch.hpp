@@ -99,6 +99,12 @@ JitRader *jit_rader_build(int dev, const int *rad, int np);  // nullptr: not bui
 hipError_t jit_launch_rader(const JitRader *j, bool inv, int load, const void *in, cd *out,
                             int64_t batch, const cd *tw, const cd *bhat, const int *gpow,
                             const int *ginv, double scale, hipStream_t s);
+// rader_pfa_kernel (mixed_fixed.hpp): n = m * P (gcd 1), P = prod(rad) + 1
+// prime, by the prime-factor map and m Rader sub-transforms in one kernel;
+// launched by jit_launch_rader with the prime P's tables. nullptr: m has no
+// in-register DFT, the geometry does not fit, or the kernel did not build.
+bool pfa_cofactor_supported(int m);
+JitRader *jit_rader_pfa_build(int dev, int m, const int *rad, int np);
 hipError_t jit_launch_pwelch(const JitSpec *j, const double *x, int64_t nfft, int64_t stride,
                              int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,
                              const double *win, const cd *tw, double *partial, hipStream_t s);

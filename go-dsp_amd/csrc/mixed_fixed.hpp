@@ -1051,6 +1051,287 @@ __global__ __launch_bounds__((RaderGeo<R0, RS...>::WG)) void rader_fixed_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// A composite n = M * P with a prime factor P > 31 whose P - 1 has a radix
+// list, and gcd(M, P) = 1 (the reference sends it to Bluestein like every
+// non-power-of-2 length, fft/fft.go:82-86 -> fft/bluestein.go:68-94: three
+// FFTs of NextPowerOf2(2n - 1) points). Good-Thomas (prime-factor) index maps
+// make the DFT an M x P two-dimensional one without twiddles:
+//   X[(k1 E1 + k2 E2) mod n] = sum_i2 W_P^(i2 k2) sum_i1 W_M^(i1 k1)
+//                              x[(i1 P + i2 M) mod n],
+// E1 = P (P^-1 mod M) (= 1 mod M, 0 mod P), E2 = M (M^-1 mod P). The DFT_M
+// along i1 runs in registers (one column per thread); the M DFT_P along i2
+// run as Rader's cyclic convolutions of length N = P - 1 on the inlined
+// mixed-radix chain, side by side in one workgroup (rader_fixed_kernel for M
+// sub-transforms). One HBM read and one write per sample, as any one-kernel
+// transform:
+//  1. the workgroup's TPW rows (contiguous) into LDS, coalesced, natural order;
+//  2. column q of row s (q < N: i2 = gpow[q]; q = N: i2 = 0) gathers its M
+//     samples x[(i1 P + i2 M) mod n], DFT_M; output k1 goes to slot q of
+//     sub-transform k1 — Rader's a[q] = y[gpow[q]] in natural order — or, for
+//     q = N, to the sub-transform's y0;
+//  3. each sub-transform: FFT_N, x bhat (+ y0 at k = 0), conj, FFT_N, conj
+//     (rader_fixed_kernel steps 2-4, the same tables as the prime P's plan);
+//  4. output r of sub-transform k1 is X_P[k2 = ginv[r]]: scattered to LDS slot
+//     (k1 E1 + k2 E2) mod n (k2 = 0: y0 + A[0]), then a coalesced store.
+// The LDS a row uses for its samples, its M sub-transforms' exchanges and
+// its output staging is one region, separated by barriers.
+constexpr int pfa_gcd(int a, int b) { return b ? pfa_gcd(b, a % b) : a; }
+constexpr int pfa_inv(int a, int m) {  // a^-1 mod m (gcd(a, m) = 1)
+  for (int x = 1; x < m; ++x)
+    if ((a % m) * x % m == 1) return x;
+  return 0;
+}
+// sizes dft_any has an in-register DFT for
+constexpr bool dft_native(int r) {
+  switch (r) {
+    case 2: case 3: case 4: case 5: case 6: case 7: case 8: case 9: case 10: case 11: case 12:
+    case 13: case 15: case 16: case 17: case 19: case 20: case 23: case 25: case 29: case 31:
+    case 32:
+      return true;
+    default:
+      return false;
+  }
+}
+// R1 of a coprime split M = R1 R2 with both native (0: none)
+constexpr int pfa_split(int m) {
+  for (int r1 = 2; r1 < m; ++r1)
+    if (m % r1 == 0 && pfa_gcd(r1, m / r1) == 1 && dft_native(r1) && dft_native(m / r1)) return r1;
+  return 0;
+}
+// Prime-factor DFT of R1 R2 points (coprime): input (R2 n1 + R1 n2) mod R,
+// output (k1 R2 (R2^-1 mod R1) + k2 R1 (R1^-1 mod R2)) mod R, no twiddles
+template <int R1, int R2>
+__device__ __forceinline__ void dft_pfa2(cd (&v)[R1 * R2]) {
+  constexpr int R = R1 * R2;
+  constexpr int F1 = R2 * pfa_inv(R2 % R1, R1) % R, F2 = R1 * pfa_inv(R1 % R2, R2) % R;
+  cd t[R2][R1];
+#pragma unroll
+  for (int n2 = 0; n2 < R2; ++n2) {
+#pragma unroll
+    for (int n1 = 0; n1 < R1; ++n1) t[n2][n1] = v[(R2 * n1 + R1 * n2) % R];
+    dft_any<R1>(t[n2]);
+  }
+#pragma unroll
+  for (int k1 = 0; k1 < R1; ++k1) {
+    cd u[R2];
+#pragma unroll
+    for (int n2 = 0; n2 < R2; ++n2) u[n2] = t[n2][k1];
+    dft_any<R2>(u);
+#pragma unroll
+    for (int k2 = 0; k2 < R2; ++k2) v[(k1 * F1 + k2 * F2) % R] = u[k2];
+  }
+}
+template <int M>
+__device__ __forceinline__ void dft_m(cd (&v)[M]) {
+  if constexpr (dft_native(M)) {
+    dft_any<M>(v);
+  } else {
+    constexpr int R1 = pfa_split(M);
+    static_assert(R1 > 0, "no in-register DFT for this cofactor");
+    dft_pfa2<R1, M / R1>(v);
+  }
+}
+
+template <int M, int R0, int... RS>
+struct PfaGeo {
+  using G = FixedGeo<R0, RS...>;
+  static constexpr int N = G::N, P = N + 1, T1 = G::T1, NN = M * P;
+  static constexpr int SUBS = G::SLOTS;                      // a sub-transform's slots
+  static constexpr int RSL = M * SUBS > NN ? M * SUBS : NN;  // complex slots per row
+  static constexpr int RT = M * T1;                          // threads per row
+  static constexpr int tpw() {
+    int t = 256 / RT > 1 ? 256 / RT : 1;
+    while (t > 1 && t * RSL * 16 > 65536) --t;
+    return t;
+  }
+  static constexpr int TPW = tpw();
+  static constexpr int WG = TPW * RT;
+  static constexpr int NCOL = TPW * P, CA = (NCOL + WG - 1) / WG;  // stage-A columns
+  static constexpr int CH = TPW * NN, NC = (CH + WG - 1) / WG;     // row elements per thread
+  static constexpr int E1 = P * pfa_inv(P % M, M) % NN, E2 = M * pfa_inv(M % P, P) % NN;
+};
+
+template <bool INV, int LOAD, bool SWZ, int M, int R0, int... RS>
+__global__ __launch_bounds__((PfaGeo<M, R0, RS...>::WG)) void rader_pfa_kernel(
+    const void *__restrict__ in, cd *__restrict__ out, int64_t batch, const cd *__restrict__ tw,
+    const cd *__restrict__ bhat, const int *__restrict__ gpow, const int *__restrict__ ginv,
+    double scale) {
+  using PG = PfaGeo<M, R0, RS...>;
+  constexpr int N = PG::N, P = PG::P, T1 = PG::T1, NN = PG::NN, WG = PG::WG;
+  constexpr int RSL = PG::RSL, SUBS = PG::SUBS, CH = PG::CH, NC = PG::NC;
+  static_assert(N <= 4096, "the sub-transforms exchange as complex128 (N <= 4096)");
+  using First = FPass<R0, N, 1, T1>;
+  using FL = FixedLast<R0, RS...>;
+  using Last = typename FL::Pass;
+  constexpr int RL = FL::R, NSL = N / RL;
+  __shared__ double lds[2 * PG::TPW * RSL + 2 * PG::TPW * M];
+  cd *const xs = reinterpret_cast<cd *>(lds);                       // rows (RSL slots each)
+  cd *const dcs = reinterpret_cast<cd *>(lds + 2 * PG::TPW * RSL);  // y0 of each sub-transform
+  const int tid = (int)threadIdx.x;
+  const int rs = PG::TPW == 1 ? 0 : tid / PG::RT;  // row slot of this thread's sub-transform
+  const int tr = tid - rs * PG::RT;
+  const int k1 = tr / T1, tl = tr - k1 * T1;
+  const int64_t c0 = xcd_remap(blockIdx.x, gridDim.x) * (int64_t)CH, cend = batch * NN;
+  auto slot = [&](int e) -> cd * {  // workgroup chunk element e -> its row's LDS slot
+    const int s = e / NN;
+    return xs + s * RSL + (e - s * NN);
+  };
+  // 1. the rows, natural order
+  {
+    cd xc[NC];
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const int e = tid + q * WG;
+      xc[q] = {0.0, 0.0};
+      if (((q + 1) * WG <= CH || e < CH) && c0 + e < cend) {
+        if constexpr (LOAD == LOAD_REAL) {
+          xc[q] = {ld_nt(reinterpret_cast<const double *>(in) + c0 + e), 0.0};
+        } else {
+          xc[q] = ld_nt(reinterpret_cast<const cd *>(in) + c0 + e);
+          if constexpr (INV) xc[q].y = -xc[q].y;
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const int e = tid + q * WG;
+      if ((q + 1) * WG <= CH || e < CH) *slot(e) = xc[q];
+    }
+  }
+  __syncthreads();
+  // 2. DFT_M down each column, into the sub-transforms' Rader order
+  {
+    cd ya[PG::CA][M];
+    int qa[PG::CA];
+#pragma unroll
+    for (int a = 0; a < PG::CA; ++a) {
+      const int c = tid + a * WG;
+      qa[a] = -1;
+      if ((a + 1) * WG <= PG::NCOL || c < PG::NCOL) {
+        const int s = c / P, q = c - s * P;
+        const int i2 = q < N ? gpow[q] : 0;
+        const cd *row = xs + s * RSL;
+        int idx = M * i2;  // (i1 P + i2 M) mod n for i1 = 0, 1, ...
+#pragma unroll
+        for (int i1 = 0; i1 < M; ++i1) {
+          ya[a][i1] = row[idx];
+          idx += P;
+          if (idx >= NN) idx -= NN;
+        }
+        dft_m<M>(ya[a]);
+        qa[a] = c;
+      }
+    }
+    __syncthreads();  // every gather of the rows is done
+#pragma unroll
+    for (int a = 0; a < PG::CA; ++a) {
+      if (qa[a] >= 0) {
+        const int s = qa[a] / P, q = qa[a] - s * P;
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+          if (q < N) xs[s * RSL + k * SUBS + q] = ya[a][k];
+          else dcs[s * M + k] = ya[a][k];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // 3. sub-transform k1 of row rs: Rader's convolution (rader_fixed_kernel)
+  cd *const lc = xs + rs * RSL + k1 * SUBS;
+  const cd y0 = dcs[rs * M + k1];
+  First p0;
+#pragma unroll
+  for (int jj = 0; jj < First::J; ++jj) {
+    const int j = tl + jj * T1;
+    if (First::act(j, true)) {
+#pragma unroll
+      for (int r = 0; r < R0; ++r) p0.v[jj][r] = lc[j + r * First::NB];
+    }
+  }
+  p0.compute(tl, true, tw);
+  Last keep;
+  if constexpr (sizeof...(RS) == 0) {
+    keep = p0;
+  } else {
+    __syncthreads();  // every first-pass load is done before the first exchange writes
+    auto sink = [&](const Last &c) { keep = c; };
+    fixed_chain_to<false, SWZ, N, T1, R0, 0, First, decltype(sink), RS...>(p0, tl, true, lc, tw,
+                                                                           sink);
+  }
+  cd a0 = {0.0, 0.0};
+#pragma unroll
+  for (int jj = 0; jj < Last::J; ++jj) {
+    const int j = tl + jj * T1;
+    if (Last::act(j, true)) {
+      const int kb = j % NSL, o = (j - kb) * RL + kb;
+#pragma unroll
+      for (int r = 0; r < RL; ++r) {
+        const int k = o + r * NSL;
+        const cd A = keep.v[jj][r];
+        cd c = cmul(A, bhat[k]);
+        if (k == 0) {
+          a0 = A;
+          c = c + y0;
+        }
+        keep.v[jj][r] = conjg(c);
+      }
+    }
+  }
+  const int t2 = opaque_int(tl);
+  const cd *tw2 = opaque_ptr(tw);
+  First p1;
+  __syncthreads();  // the last exchange's reads (or the first-pass loads) are done
+  keep.template store_lds<2, SWZ>(t2, true, lc);
+  __syncthreads();
+  p1.template load_lds<2, SWZ>(t2, true, lc);
+  p1.compute(t2, true, tw2);
+  Last fin;
+  if constexpr (sizeof...(RS) == 0) {
+    fin = p1;
+  } else {
+    __syncthreads();
+    auto sink = [&](const Last &c) { fin = c; };
+    fixed_chain_to<false, SWZ, N, T1, R0, 0, First, decltype(sink), RS...>(p1, t2, true, lc, tw2,
+                                                                           sink);
+  }
+  // 4. X[(k1 E1 + k2 E2) mod n], k2 = ginv[r]; k2 = 0: y0 + A[0]
+  int oi[Last::J][RL];
+#pragma unroll
+  for (int jj = 0; jj < Last::J; ++jj) {
+    const int j = t2 + jj * T1;
+    const int kb = j % NSL, o = (j - kb) * RL + kb;
+#pragma unroll
+    for (int r = 0; r < RL; ++r) oi[jj][r] = Last::act(j, true) ? ginv[o + r * NSL] : 0;
+  }
+  cd *const ro = xs + rs * RSL;
+  const int kb1 = k1 * PG::E1 % NN;
+  __syncthreads();  // every sub-transform's LDS reads are done (the regions overlap)
+#pragma unroll
+  for (int jj = 0; jj < Last::J; ++jj) {
+    const int j = t2 + jj * T1;
+    if (Last::act(j, true)) {
+#pragma unroll
+      for (int r = 0; r < RL; ++r) {
+        int idx = kb1 + oi[jj][r] * PG::E2 % NN;
+        if (idx >= NN) idx -= NN;
+        ro[idx] = conjg(fin.v[jj][r]);
+      }
+    }
+  }
+  if (t2 == 0) ro[kb1] = y0 + a0;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
+    const int e = tid + q * WG;
+    if (((q + 1) * WG <= CH || e < CH) && c0 + e < cend) {
+      cd y = *slot(e);
+      if constexpr (INV) y = {y.x * scale, -y.y * scale};
+      st_nt(out + c0 + e, y);
+    }
+  }
+}
+
 #ifndef __HIPCC_RTC__
 // Workers per workgroup of the fused Pwelch on d's list, 0 where d is not
 // this list or where a pair's samples (span = stride + nfft doubles) exceed

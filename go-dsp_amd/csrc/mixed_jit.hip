@@ -582,6 +582,67 @@ JitRader *jit_rader_build(int dev, const int *rad, int np) {
   return j;
 }
 
+namespace {
+// dft_native / pfa_split (mixed_fixed.hpp) on the host
+bool host_dft_native(int r) {
+  static const int nat[] = {2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 15, 16, 17, 19, 20, 23, 25, 29, 31, 32};
+  return std::find(std::begin(nat), std::end(nat), r) != std::end(nat);
+}
+int host_gcd(int a, int b) { return b ? host_gcd(b, a % b) : a; }
+}  // namespace
+
+bool pfa_cofactor_supported(int m) {
+  if (m < 2) return false;
+  if (host_dft_native(m)) return true;
+  for (int r1 = 2; r1 < m; ++r1)
+    if (m % r1 == 0 && host_gcd(r1, m / r1) == 1 && host_dft_native(r1) && host_dft_native(m / r1))
+      return true;
+  return false;
+}
+
+JitRader *jit_rader_pfa_build(int dev, int m, const int *rad, int np) {
+  if (!jit_enabled() || np < 1 || !pfa_cofactor_supported(m)) return nullptr;
+  int n = 1;
+  for (int q = 0; q < np; ++q) n *= rad[q];
+  if (n > 4096) return nullptr;
+  int t1 = 0, tpw = 0;
+  fixed_geo(rad, np, &t1, &tpw);
+  // PfaGeo (mixed_fixed.hpp) on the host: M sub-transforms of T1 threads per
+  // row, rows per workgroup within 256 threads and 64 KiB of row slots
+  const int p = n + 1, nn = m * p, subs = (n + 7) & ~7;
+  const int rsl = std::max(m * subs, nn), rt = m * t1;
+  tpw = 256 / rt > 1 ? 256 / rt : 1;
+  while (tpw > 1 && tpw * rsl * 16 > 65536) --tpw;
+  const int wg = tpw * rt;
+  const int ncol = tpw * p, ca = (ncol + wg - 1) / wg;
+  const long lds = 16L * tpw * (rsl + m);
+  // one workgroup of at most 1024 threads within the CU's LDS, and the
+  // stage-A columns' M-point values of a thread within 32 complex128 registers
+  if (wg > 1024 || lds > 163840 || ca * m > 32) return nullptr;
+  const std::string list = radix_list(rad, np), sw = rad[0] % 2 == 0 ? "true" : "false";
+  const std::string ms = ", " + std::to_string(m);
+  const std::vector<std::string> names = {
+      "&gdsp::rader_pfa_kernel<false, 0, " + sw + ms + list + ">",
+      "&gdsp::rader_pfa_kernel<true, 0, " + sw + ms + list + ">",
+      "&gdsp::rader_pfa_kernel<false, 1, " + sw + ms + list + ">"};
+  hipModule_t mod = nullptr;
+  std::vector<hipFunction_t> fs;
+  if (!compile_module(dev, names, "prime-factor Rader kernel for n = " + std::to_string(nn) +
+                                      " = " + std::to_string(m) + " x " + std::to_string(p) +
+                                      " (N = " + list.substr(2) + ")",
+                      &mod, fs))
+    return nullptr;
+  JitRader *j = new JitRader;
+  j->mod = mod;
+  j->fwd = fs[0];
+  j->inv = fs[1];
+  j->real = fs[2];
+  j->p = nn;
+  j->tpw = tpw;
+  j->wg = wg;
+  return j;
+}
+
 hipError_t jit_launch_rader(const JitRader *j, bool inv, int load, const void *in, cd *out,
                             int64_t batch, const cd *tw, const cd *bhat, const int *gpow,
                             const int *ginv, double scale, hipStream_t s) {

@@ -50,7 +50,17 @@ namespace gdsp {
 // registers, 5.95 ms without the next pair's samples in flight (touching its
 // lines one pair ahead instead), 10.4 with them; without them at two waves,
 // 3.02 against 2.73-2.77 ms.
-template <int LOG2F, int LOG2E = 4, bool REGTW = true, int LAYOUT = 2>
+//
+// FOLD (measured by register count only, tools/
+// pwelch_fold_probe.hip, profiles/r06/pw4096_fold_resusage.txt): finalise
+// uses only acc[k] + acc[F - k], and the partner of the thread's bin
+// k = t + T m is bin F - k = (T - t) + T (E - 1 - m) of thread T - t, so after
+// each pair's last pass a thread hands its upper-half |Z|^2 to its partner
+// through LDS and keeps E / 2 folded sums (+ one for the self-mirrored bin
+// F / 2 of thread 0), 14 fewer VGPRs, at 8 LDS writes, 8 reads and a barrier
+// per pair. Not instantiated in the library: it does not reach three waves
+// per SIMD.
+template <int LOG2F, int LOG2E = 4, bool REGTW = true, int LAYOUT = 2, bool FOLD = false>
 __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_row_kernel(
     const double *__restrict__ x, int64_t seg_begin, int64_t seg_end, int64_t pairs_per_worker,
     const double *__restrict__ win, const cd *__restrict__ tw, double *__restrict__ partial) {
@@ -101,9 +111,10 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_row_kernel(
     }
   };
   issue(p0);
-  double acc[E];
+  constexpr int NACC = FOLD ? H + 1 : E;  // FOLD: E / 2 folded sums + thread 0's bin F / 2
+  double acc[NACC];
 #pragma unroll
-  for (int k = 0; k < E; ++k) acc[k] = 0.0;
+  for (int k = 0; k < NACC; ++k) acc[k] = 0.0;
   auto pair = [&](int64_t p, bool first, bool partner) {
     const int tt = opaque_int(t);
     cd v[E];
@@ -129,15 +140,41 @@ __global__ __launch_bounds__((Geo<LOG2F, LOG2E>::WG)) void pwelch_row_kernel(
                                                                           first);
     else
       fft_regs<LOG2F, true, 1, LOG2E, 0, 0, const cd *, LAYOUT>(v, tt, tw, lx, lx, first);
+    if constexpr (FOLD) {
+      double pw[E];
 #pragma unroll
-    for (int k = 0; k < E; ++k) acc[k] = fma(v[k].y, v[k].y, fma(v[k].x, v[k].x, acc[k]));
+      for (int k = 0; k < E; ++k) pw[k] = fma(v[k].y, v[k].y, v[k].x * v[k].x);
+      __syncthreads();  // the last exchange's reads are done
+#pragma unroll
+      for (int k = H; k < E; ++k) lx[tt * H + (k - H)] = pw[k];
+      __syncthreads();
+      if (tt == 0) {  // bins T m, mirrors T (E - m): 0 and F / 2 are their own
+        acc[0] += pw[0];
+#pragma unroll
+        for (int m = 1; m < H; ++m) acc[m] += pw[m] + lx[H - m];
+        acc[H] += lx[0];
+      } else {
+        const int tp = T - tt;
+#pragma unroll
+        for (int m = 0; m < H; ++m) acc[m] += pw[m] + lx[tp * H + (H - 1 - m)];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < E; ++k) acc[k] = fma(v[k].y, v[k].y, fma(v[k].x, v[k].x, acc[k]));
+    }
   };
   int64_t p = p0;
   for (; p < fend; ++p) pair(p, p == p0, true);
   if (p < pend) pair(p, p == p0, false);  // the odd count's last segment, zero partner
   double *dst = partial + blockIdx.x * (int64_t)G::N;
+  if constexpr (FOLD) {
 #pragma unroll
-  for (int k = 0; k < E; ++k) dst[t + k * T] = acc[k];
+    for (int k = 0; k < E; ++k)
+      dst[t + k * T] = k < H ? acc[k] : (t == 0 && k == H ? acc[H] : 0.0);
+  } else {
+#pragma unroll
+    for (int k = 0; k < E; ++k) dst[t + k * T] = acc[k];
+  }
 }
 
 

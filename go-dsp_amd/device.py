@@ -31,7 +31,8 @@ class Plan:
     (gdsp_plan_create). kind: 0 trivial, 1 LDS Stockham, 2 multi-pass
     Stockham, 3 fused Bluestein, 4 composed Bluestein, 5 mixed radix,
     6 mixed four-step, 7 Rader (a prime n <= 8193 whose n - 1 has a radix
-    list; m = n - 1, the cyclic convolution's length).
+    list; m = n - 1, the cyclic convolution's length), 8 prime-factor Rader
+    (composite n = n1 * n2 <= 8192, n2 the prime; m = n2 - 1).
     chirpz=True forces the reference's Bluestein algorithm
     (gdsp_plan_create_chirpz) for a non-trivial length."""
 

@@ -83,8 +83,9 @@ enum {
   GDSP_ALGO_CHIRPZ_POW2 = 4,
   /* the composed chirp-z without its fused transposes */
   GDSP_ALGO_CHIRPZ_UNFUSED = 8,
-  /* primes n <= 8193 whose n - 1 has a radix list on the chirp-z kernels
-   * instead of Rader's algorithm (plan kind 7) */
+  /* primes n <= 8193 whose n - 1 has a radix list, and the composites of
+   * plan kind 8, on the chirp-z kernels instead of Rader's algorithm (plan
+   * kinds 7 and 8) */
   GDSP_ALGO_NO_RADER = 16
 };
 /* Unknown bits → GDSP_ERR_INVALID (the selection is left unchanged). */
@@ -261,13 +262,18 @@ int gdsp_plan_create_chirpz(int64_t n, gdsp_plan **plan);
  * 7 Rader (a prime 17 <= n <= 8193 whose n - 1 has a list of radices <= 25
  * within 640 threads per transform: the DFT as
  * a cyclic convolution of length n - 1, two FFTs of n - 1 points in one
- * runtime-compiled kernel; GDSP_ALGO_NO_RADER keeps such primes on kind 3). */
+ * runtime-compiled kernel; GDSP_ALGO_NO_RADER keeps such primes on kind 3),
+ * 8 prime-factor Rader (a composite n <= 8192 = n1 * n2, n2 > 31 its largest
+ * prime factor with a kind-7 plan, gcd(n1, n2) = 1, n1 with an in-register
+ * DFT: the Good-Thomas map, DFT_n1 per column and n1 Rader transforms of n2
+ * points, one runtime-compiled kernel; GDSP_ALGO_NO_RADER keeps kind 3). */
 int gdsp_plan_kind(const gdsp_plan *plan);
 /* Geometry of a plan (any pointer may be NULL): its length n; the chirp-z
  * convolution length m (kinds 3 and 4; the reference's NextPowerOf2(2n-1),
  * bluestein.go:70, or a smooth m >= 2n-1 that the composed chirp-z may
- * choose; kind 7: Rader's cyclic convolution length n - 1); the four-step
- * split n = n1*n2 (kinds 2 and 6); and whether a
+ * choose; kind 7: Rader's cyclic convolution length n - 1; kind 8: n2 - 1);
+ * the four-step split n = n1*n2 (kinds 2 and 6) or the prime-factor split
+ * (kind 8: cofactor n1, prime n2); and whether a
  * runtime-compiled specialisation backs it (1) or not (0). 0 where n/a. */
 int gdsp_plan_info(const gdsp_plan *plan, int64_t *n, int64_t *m, int64_t *n1, int64_t *n2,
                    int *runtime_compiled);

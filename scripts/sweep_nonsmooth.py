@@ -72,12 +72,12 @@ def main():
         del z
         rec = {"n": n, "batch": batch, "plan_kind": p.kind, "m": p.m, "n1": p.n1, "n2": p.n2,
                "ms": round(ms, 4), "gsamples_s": round(batch * n / ms / 1e6, 2),
-               "frac": round(32 * batch * n / ms / 1e9 / 8000.0, 4),
+               "frac": round(32 * batch * n / ms / 1e6 / 8000.0, 4),
                "nrel_vs_oracle": nrel, "roundtrip_nrel": rt}
         if not a.no_chirpz:
             cz = timed(n, x, y, True, a.reps)
             rec.update({"chirpz_ms": round(cz, 4),
-                        "chirpz_frac": round(32 * batch * n / cz / 1e9 / 8000.0, 4),
+                        "chirpz_frac": round(32 * batch * n / cz / 1e6 / 8000.0, 4),
                         "speedup_vs_chirpz": round(cz / ms, 3)})
         print(json.dumps(rec), flush=True)
         del x, y

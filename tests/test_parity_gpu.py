@@ -551,7 +551,8 @@ def test_plan_kinds(gdsp):
     assert D.plan(4096).kind == 1
     assert D.plan(1 << 16).kind == 2
     assert D.plan(3000).kind == 5  # 2^3 3 5^3: mixed radix
-    assert D.plan(4097).kind == 3  # 17 * 241: fused Bluestein
+    assert D.plan(4097).kind == 8  # 17 * 241: prime-factor Rader (240 = 16 * 15)
+    assert D.plan(2062).kind == 3  # 2 * 1031, 1030 = 2 * 5 * 103: fused Bluestein
     assert D.plan(10000).kind == 6  # 16 x 625: mixed four-step (power-of-2 columns)
     assert D.plan(44100).kind == 6  # 25 x 1764: mixed four-step (single-radix columns)
     assert D.plan(5000).kind == 5  # a compiled specialisation above 4096 (25*25*8)
@@ -1318,6 +1319,112 @@ def test_rader_large_batch_properties(gdsp):
     n, batch = 3001, 65536
     assert D.plan(n).kind == 7
     g = torch.Generator(device="cuda").manual_seed(9)
+    x = torch.complex(torch.rand(batch, n, dtype=torch.float64, device="cuda", generator=g) - 0.5,
+                      torch.rand(batch, n, dtype=torch.float64, device="cuda", generator=g) - 0.5)
+    y = D.fft_batch(x)
+    z = D.fft_batch(y, inverse=True)
+    err = ((z - x).abs().amax(dim=1) / x.abs().amax(dim=1)).max().item()
+    assert err < 1e-12, err
+    y2 = D.fft_batch(2.0 * x[:64] - 1j * x[64:128])
+    lin = ((y2 - (2.0 * y[:64] - 1j * y[64:128])).abs().max() / y[:128].abs().max()).item()
+    assert lin < 1e-13, lin
+    rows = [0, 1, 777, 4096, 30000, 65534, 65535, 12345]
+    xs = x[rows].cpu().numpy()
+    assert row_nrel(y[rows].cpu().numpy(), np.fft.fft(xs, axis=1)) < 1e-13
+
+
+# ---- prime-factor Rader (rader_pfa_kernel, plan kind 8) ---------------------------
+# composites n = M * P <= 8192, P > 31 the largest prime factor with a Rader
+# plan, gcd(M, P) = 1: the reference's Bluestein (fft/bluestein.go:68-94) on
+# NextPowerOf2(2n - 1) replaced by the Good-Thomas map and M Rader transforms
+PFA_CASES = [74, 111, 185, 259, 333, 407, 481, 518, 666, 777, 888, 925, 1147, 1184, 82, 129,
+             265, 427, 803, 1067, 1111, 1507, 2222, 2410, 3027, 4097, 5045, 6010, 7206, 8072,
+             8116]
+
+
+def _pfa_split(n):
+    f, m, d = [], n, 2
+    while d * d <= m:
+        while m % d == 0:
+            f.append(d)
+            m //= d
+        d += 1
+    if m > 1:
+        f.append(m)
+    P = max(f)
+    return n // P, P
+
+
+@pytest.mark.parametrize("n", PFA_CASES)
+def test_rader_pfa_vs_oracle(gdsp, oracle, n):
+    """Forward, inverse, real input, in place, batches 1 and 7, against the
+    oracle (the reference's Bluestein restated) and numpy's float64 DFT; the
+    forced chirp-z plan (GDSP_ALGO_NO_RADER) on the same rows."""
+    import torch
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    F = __import__("importlib").import_module("go-dsp_amd.fft")
+    M, P = _pfa_split(n)
+    p = D.plan(n)
+    assert (p.kind, p.n1, p.n2, p.m, p.runtime_compiled) == (8, M, P, P - 1, True), \
+        (n, p.kind, p.n1, p.n2, p.m)
+    rng = np.random.default_rng(8000 + n)
+    for batch in (1, 7):
+        x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
+        ref = oracle.fft_rows(x)
+        y = gdsp.fft.FFTBatch(x)
+        assert row_nrel(y, ref) < TOL
+        assert row_nrel(y, np.fft.fft(x, axis=1)) < 1e-13
+        assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL
+        xr = rng.uniform(-1, 1, (batch, n))
+        assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
+        xt = torch.from_numpy(x).cuda()
+        D.fft_batch(xt, xt)
+        torch.cuda.synchronize()
+        assert row_nrel(xt.cpu().numpy(), ref) < TOL
+    x = rng.uniform(-1, 1, (3, n)) + 1j * rng.uniform(-1, 1, (3, n))
+    assert nrel(gdsp.fft.FFT(x[0]), oracle.fft(x[0])) < TOL
+    assert nrel(gdsp.fft.IFFT(x[1]), oracle.ifft(x[1])) < TOL
+    F.SetAlgorithm(F.ALGO_NO_RADER)
+    try:
+        assert D.plan(n).kind in (3, 4)
+        yc = gdsp.fft.FFTBatch(x)
+    finally:
+        F.SetAlgorithm(0)
+    assert row_nrel(yc, oracle.fft_rows(x)) < TOL
+
+
+def test_rader_pfa_every_cofactor(gdsp, oracle):
+    """Every cofactor M = 2 ... 32 beside P = 37 (36 = the Rader list): the
+    native in-register DFTs and the coprime splits (14 = 2 x 7, 18 = 2 x 9,
+    21, 22, 24, 26, 28, 30); 27 = 3^3 has neither (chirp-z)."""
+    import torch
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    for M in range(2, 33):
+        n = 37 * M
+        if M == 27:
+            assert D.plan(n).kind == 3, n
+            continue
+        assert D.plan(n).kind == 8, (n, D.plan(n).kind)
+        g = torch.Generator(device="cuda").manual_seed(M)
+        x = torch.complex(torch.rand(301, n, dtype=torch.float64, device="cuda", generator=g) - 0.5,
+                          torch.rand(301, n, dtype=torch.float64, device="cuda", generator=g) - 0.5)
+        y = D.fft_batch(x)
+        rows = [0, 150, 300]
+        xs = x[rows].cpu().numpy()
+        assert row_nrel(y[rows].cpu().numpy(), oracle.fft_rows(xs)) < TOL, n
+        assert row_nrel(y[rows].cpu().numpy(), np.fft.fft(xs, axis=1)) < 1e-13, n
+        z = D.fft_batch(y, inverse=True)
+        assert float(((z - x).abs().amax(dim=1) / x.abs().amax(dim=1)).max()) < 1e-12, n
+
+
+def test_rader_pfa_large_batch_properties(gdsp):
+    """65 536 rows of 3027 = 3 x 1009 (the bench's shape): round trip and
+    linearity on every row, eight rows against numpy."""
+    import torch
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    n, batch = 3027, 65536
+    assert D.plan(n).kind == 8
+    g = torch.Generator(device="cuda").manual_seed(11)
     x = torch.complex(torch.rand(batch, n, dtype=torch.float64, device="cuda", generator=g) - 0.5,
                       torch.rand(batch, n, dtype=torch.float64, device="cuda", generator=g) - 0.5)
     y = D.fft_batch(x)
