@@ -67,6 +67,7 @@ SIGNATURES = {
     "gdsp_plan_destroy": (_I, [_P]),
     "gdsp_plan_kind": (_I, [_P]),
     "gdsp_plan_parts": (_I, [_P]),
+    "gdsp_plan_radices": (_I, [_P, ctypes.POINTER(_I), _I]),
     "gdsp_plan_info": (_I, [_P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64),
                             ctypes.POINTER(_I64), ctypes.POINTER(_I)]),
     "gdsp_fft_batch_device": (_I, [_P, _P, _P, _I64, _I, _P]),

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <functional>
 #include <map>
 #include <tuple>
 #include <mutex>
@@ -92,7 +93,7 @@ bool lds_split_default() { return true; }
 std::atomic<unsigned> g_algo{GDSP_ALGO_DEFAULT};
 constexpr unsigned kAlgoAll = GDSP_ALGO_GENERIC_MIXED | GDSP_ALGO_NO_CHIRPZ_PARTS |
                               GDSP_ALGO_CHIRPZ_POW2 | GDSP_ALGO_CHIRPZ_UNFUSED |
-                              GDSP_ALGO_NO_RADER;
+                              GDSP_ALGO_NO_RADER | GDSP_ALGO_NO_RACE;
 
 // Scratch device memory: a grow-only buffer per (device, stream, use-site
 // slot), allocated with hipMalloc. Reuse is ordered by the stream itself: a
@@ -350,6 +351,12 @@ struct gdsp_plan {
   // bases, bhat = FFT_m(b)/m, gpow[q] = g^q mod n, ginv[r] = g^-r mod n
   gdsp::JitRader *rader = nullptr;
   int *gpow = nullptr, *ginv = nullptr;
+  // fused chirp-z on a smooth convolution length (KIND_BLUESTEIN, m = L):
+  // bluestein_fixed_kernel for n, tw_blu its per-pass twiddle bases
+  gdsp::JitBlu *blufix = nullptr;
+  cd *tw_blu = nullptr, *bhat_blu = nullptr;
+  int64_t m_blu = 0;
+  gdsp::MixedDesc md_blu{};
   // prime-factor Rader (KIND_RADER_PFA, n = n1 * n2, n2 a prime with a Rader
   // plan p2 whose tables the kernel reads, gcd(n1, n2) = 1): rader is
   // rader_pfa_kernel for the cofactor n1, m = n2 - 1
@@ -861,11 +868,79 @@ int rader_try(int dev, int64_t n, gdsp_plan *p, bool *built) {
   return GDSP_OK;
 }
 
+// Plan-time race of two ways to run a batched transform of n, where the cost
+// model cannot rank them (the prime-factor Rader kernel against the chirp-z
+// plan it would replace; the smooth-L chirp-z against the power-of-2 one):
+// ~2^23 samples of synthetic rows, each candidate launched three times,
+// alternating, on the building thread's stream; *a_wins = a's fastest launch
+// < margin x b's. Plans are built once per (device, n, flags), so this costs
+// a few milliseconds once. Where the scratch cannot be had, a wins (the
+// model's candidate); GDSP_ALGO_NO_RACE skips the race the same way.
+using Runner = std::function<int(const cd *in, cd *out, int64_t batch, hipStream_t s)>;
+int race(int dev, int64_t n, const Runner &a, const Runner &b, double margin, bool *a_wins) {
+  *a_wins = true;
+  if (plan_flags() & GDSP_ALGO_NO_RACE) return GDSP_OK;
+  hipStream_t s = thread_stream(dev);
+  const int64_t batch = std::max<int64_t>(1, ((int64_t)1 << 23) / n);
+  const size_t bytes = (size_t)batch * (size_t)n * sizeof(cd);
+  cd *in = nullptr, *out = nullptr;
+  if (hipMalloc((void **)&in, bytes) != hipSuccess) return GDSP_OK;
+  if (hipMalloc((void **)&out, bytes) != hipSuccess) {
+    (void)hipFree(in);
+    return GDSP_OK;
+  }
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  float best[2] = {1e30f, 1e30f};
+  int st = GDSP_OK;
+  hipError_t he = hipEventCreate(&e0);
+  if (he == hipSuccess) he = hipEventCreate(&e1);
+  if (he == hipSuccess)
+    he = gdsp::launch_fill_uniform(reinterpret_cast<double *>(in), 2 * batch * n, 0x5EED, 0, s);
+  if (he != hipSuccess) st = fail(GDSP_ERR_HIP, hipGetErrorString(he));
+  const Runner *run[2] = {&a, &b};
+  for (int c = 0; c < 2 && st == GDSP_OK; ++c) st = (*run[c])(in, out, batch, s);  // warm-up
+  for (int it = 0; it < 3 && st == GDSP_OK; ++it)
+    for (int c = 0; c < 2 && st == GDSP_OK; ++c) {
+      he = hipEventRecord(e0, s);
+      if (he == hipSuccess) st = (*run[c])(in, out, batch, s);
+      if (st == GDSP_OK && he == hipSuccess) he = hipEventRecord(e1, s);
+      if (st == GDSP_OK && he == hipSuccess) he = hipEventSynchronize(e1);
+      float ms = 0.0f;
+      if (st == GDSP_OK && he == hipSuccess) he = hipEventElapsedTime(&ms, e0, e1);
+      if (he != hipSuccess && st == GDSP_OK) st = fail(GDSP_ERR_HIP, hipGetErrorString(he));
+      if (st == GDSP_OK) best[c] = std::min(best[c], ms);
+    }
+  (void)hipStreamSynchronize(s);
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  (void)hipFree(in);
+  (void)hipFree(out);
+  if (st == GDSP_OK) *a_wins = best[0] < margin * best[1];
+  return st;
+}
+
+// The device tables a plan owns (not its cached sub-plans), for a plan built
+// only to be raced and dropped.
+void free_plan_tables(gdsp_plan *p) {
+  for (cd *t : {p->tw, p->tw_gen == p->tw ? nullptr : p->tw_gen, p->tw_pw, p->chirp, p->bhat,
+                p->tw6k, p->tw_blu, p->bhat_blu})
+    if (t) (void)hipFree(t);
+  if (p->gpow) (void)hipFree(p->gpow);
+  if (p->ginv) (void)hipFree(p->ginv);
+}
+
+int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false, bool nopfa = false);
+
 // A composite n <= 8192 whose largest prime factor P > 31 has a Rader plan
 // and whose cofactor M = n / P (gcd(M, P) = 1) has an in-register DFT:
 // rader_pfa_kernel (mixed_fixed.hpp), Good-Thomas over M x P with the M
 // DFT_P as Rader convolutions of length P - 1, one kernel, on the prime P's
-// plan tables; otherwise (*built = false, p untouched) the chirp-z below.
+// plan tables — where it beats the plan n gets without it (the race; the
+// prime-factor kernel loses where the Rader list has a radix-17/19/23 pass
+// or the cofactor is large: 38 of 150 sampled lengths at 0.59-0.99 x the
+// chirp-z time, profiles/r06/pfa_calib.jsonl, and no cost model separated
+// them). *built: p is complete (kind 8, or the alternative plan where that
+// won); false (p untouched): not applicable, build_plan goes on as before.
 int pfa_rader_try(int dev, int64_t n, gdsp_plan *p, bool *built) {
   *built = false;
   if ((plan_flags() & GDSP_ALGO_NO_RADER) || !gdsp::jit_enabled() || n > gdsp::kMixedSpecMax ||
@@ -889,6 +964,34 @@ int pfa_rader_try(int dev, int64_t n, gdsp_plan *p, bool *built) {
   for (int q = 0; q < np; ++q) rad[q] = (int)((pp->md.codes >> (5 * q)) & 31);
   gdsp::JitRader *j = gdsp::jit_rader_pfa_build(dev, (int)M, rad, np);
   if (!j) return GDSP_OK;
+  if (!(plan_flags() & GDSP_ALGO_NO_RACE)) {
+    const double scale = 1.0 / (double)n;
+    Runner pfa = [&](const cd *in, cd *out, int64_t batch, hipStream_t s) -> int {
+      HIPCHK(gdsp::jit_launch_rader(j, false, gdsp::LOAD_COMPLEX, in, out, batch, pp->tw,
+                                    pp->bhat, pp->gpow, pp->ginv, scale, s));
+      return GDSP_OK;
+    };
+    gdsp_plan *alt = new gdsp_plan();
+    int st = build_plan(dev, n, alt, false, /*nopfa=*/true);
+    bool pfa_wins = true;
+    if (st == GDSP_OK) {
+      Runner other = [&](const cd *in, cd *out, int64_t batch, hipStream_t s) -> int {
+        return exec_plan(alt, in, out, batch, false, gdsp::LOAD_COMPLEX, s);
+      };
+      // the prime-factor kernel only where it is 3 % faster: near a tie the
+      // alternative (the reference's algorithm) stays
+      st = race(dev, n, pfa, other, 0.97, &pfa_wins);
+    }
+    if (st == GDSP_OK && !pfa_wins) {
+      *p = *alt;  // the alternative plan, tables and all
+      delete alt;
+      *built = true;
+      return GDSP_OK;
+    }
+    free_plan_tables(alt);
+    delete alt;
+    STCHK(st);
+  }
   p->kind = KIND_RADER_PFA;
   p->rader = j;
   p->p2 = pp;
@@ -899,7 +1002,84 @@ int pfa_rader_try(int dev, int64_t n, gdsp_plan *p, bool *built) {
   return GDSP_OK;
 }
 
-int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
+// The fused chirp-z on a smooth convolution length L >= 2n - 1
+// (bluestein_fixed_kernel), tried on a complete fused chirp-z plan p on M
+// (a power of 2, or the M = 6144 / 3072 kernel): L where the lane-cost
+// model puts it below 0.85 of M's kernel (blufix_length: n just above a
+// power of 2 — 4097 <= n <= 6144 on L <= 12288 instead of 16384, ...),
+// built with its own tables (b on L, bhat = FFT_L(b) / L by the engine), and
+// kept where it wins the race against p as it is (3 % margin). The same
+// linear convolution, hence the same DFT. GDSP_ALGO_CHIRPZ_POW2 keeps the
+// power of 2; the forced chirp-z plan keeps its M.
+int blufix_try(int dev, int64_t n, gdsp_plan *p, const std::vector<cd> &w) {
+  if (p->kind != KIND_BLUESTEIN || p->parts != 1 || (plan_flags() & GDSP_ALGO_CHIRPZ_POW2) ||
+      !gdsp::jit_enabled())
+    return GDSP_OK;
+  std::vector<int> now;
+  if (p->c6k) {
+    now = {16, (int)(p->m / 256), 16};
+  } else {
+    int a = p->log2m;
+    for (; a >= 4; a -= 4) now.push_back(16);
+    if (a) now.push_back(1 << a);
+  }
+  int rad[4], np = 0;
+  const int L = gdsp::blufix_length(n, p->m, now.data(), (int)now.size(), rad, &np);
+  if (!L) return GDSP_OK;
+  gdsp::JitBlu *j = gdsp::jit_blu_build(dev, n, rad, np);
+  if (!j) return GDSP_OK;
+  gdsp_plan *lp = nullptr;  // FFT_L for bhat
+  STCHK(get_plan_locked(dev, L, &lp));
+  gdsp::MixedDesc d{};
+  cd *tw = nullptr, *bh = nullptr, *db = nullptr;
+  STCHK(make_mixed_desc(dev, L, std::vector<int>(rad, rad + np), d, &tw));
+  std::vector<cd> b((size_t)L, cd{0.0, 0.0});
+  for (int64_t i = 0; i < n; ++i) {  // bluestein.go:78-85 on L
+    b[(size_t)i] = w[(size_t)i];
+    if (i != 0) b[(size_t)(L - i)] = w[(size_t)i];
+  }
+  hipStream_t s = thread_stream(dev);
+  int st = GDSP_OK;
+  if (hipMalloc((void **)&bh, (size_t)L * sizeof(cd)) != hipSuccess ||
+      hipMalloc((void **)&db, (size_t)L * sizeof(cd)) != hipSuccess)
+    st = fail(GDSP_ERR_HIP, "hipMalloc (chirp-z tables)");
+  if (st == GDSP_OK) st = copy_h2d(db, b.data(), (size_t)L * sizeof(cd), s);
+  if (st == GDSP_OK) st = exec_plan(lp, db, bh, 1, false, gdsp::LOAD_COMPLEX, s);
+  if (st == GDSP_OK) {
+    hipError_t e = gdsp::launch_scale(bh, L, 1.0 / (double)L, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) st = fail(GDSP_ERR_HIP, hipGetErrorString(e));
+  }
+  if (db) (void)hipFree(db);
+  bool wins = true;
+  if (st == GDSP_OK) {
+    const double scale = 1.0 / (double)n;
+    Runner smooth = [&](const cd *in, cd *out, int64_t batch, hipStream_t q) -> int {
+      HIPCHK(gdsp::jit_launch_blu(j, false, gdsp::LOAD_COMPLEX, in, out, batch, tw, p->chirp, bh,
+                                  scale, q));
+      return GDSP_OK;
+    };
+    Runner now_plan = [&](const cd *in, cd *out, int64_t batch, hipStream_t q) -> int {
+      return exec_plan(p, in, out, batch, false, gdsp::LOAD_COMPLEX, q);
+    };
+    st = race(dev, n, smooth, now_plan, 0.97, &wins);
+  }
+  if (st != GDSP_OK || !wins) {
+    (void)hipFree(tw);
+    if (bh) (void)hipFree(bh);
+    return st;
+  }
+  p->blufix = j;
+  p->tw_blu = tw;
+  p->bhat_blu = bh;
+  p->m_blu = L;
+  p->md_blu = d;
+  return GDSP_OK;
+}
+
+// nopfa: without the prime-factor Rader plan (the alternative it is raced
+// against, pfa_rader_try)
+int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz, bool nopfa) {
   p->device = dev;
   p->n = n;
   if (n <= 1) {
@@ -971,8 +1151,10 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
     bool built = false;
     STCHK(rader_try(dev, n, p, &built));
     if (built) return GDSP_OK;
-    STCHK(pfa_rader_try(dev, n, p, &built));
-    if (built) return GDSP_OK;
+    if (!nopfa) {
+      STCHK(pfa_rader_try(dev, n, p, &built));
+      if (built) return GDSP_OK;
+    }
   }
   // Bluestein factors, bluestein.go:32-61: w_k = (cos, sin)(Pi/n * k*k),
   // k = 0 exactly 1 (angle not reduced, as the reference computes it).
@@ -1082,7 +1264,9 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false) {
     if (e != hipSuccess) st = fail(GDSP_ERR_HIP, hipGetErrorString(e));
   }
   (void)hipFree(db);
-  return st;
+  STCHK(st);
+  if (!chirpz) STCHK(blufix_try(dev, n, p, w));
+  return GDSP_OK;
 }
 
 int get_plan_locked(int dev, int64_t n, gdsp_plan **out, bool chirpz = false) {
@@ -1526,6 +1710,11 @@ int exec_plan_depth(const gdsp_plan *p, const void *in, cd *out, int64_t batch, 
       return exec_global(p, in, out, batch, inv, load, s);
     case KIND_BLUESTEIN:
     case KIND_BLUESTEIN_COMPOSED: {
+      if (p->kind == KIND_BLUESTEIN && p->blufix) {
+        HIPCHK(gdsp::jit_launch_blu(p->blufix, inv, load, in, out, batch, p->tw_blu, p->chirp,
+                                    p->bhat_blu, scale, s));
+        return GDSP_OK;
+      }
       if (p->kind == KIND_BLUESTEIN && p->c6k) {
         // real input read by the kernel itself (no complex copy first)
         HIPCHK(gdsp::launch_chirpz6k(p->m, inv, load, in, out, p->n, batch, p->tw6k, p->chirp,
@@ -2022,14 +2211,26 @@ int gdsp_plan_destroy(gdsp_plan *) { return GDSP_OK; }
 int gdsp_plan_kind(const gdsp_plan *plan) { return plan ? plan->kind : -1; }
 int gdsp_plan_parts(const gdsp_plan *plan) { return plan ? plan->parts : 0; }
 
+int gdsp_plan_radices(const gdsp_plan *plan, int *rad, int cap) {
+  if (!plan || cap < 0 || (cap > 0 && !rad)) return fail(GDSP_ERR_INVALID, "bad argument");
+  const gdsp::MixedDesc *d = nullptr;
+  if (plan->kind == KIND_MIXED || plan->kind == KIND_RADER) d = &plan->md;
+  else if (plan->blufix) d = &plan->md_blu;
+  else if (plan->kind == KIND_RADER_PFA && plan->p2) d = &plan->p2->md;
+  if (!d) return 0;
+  for (int q = 0; q < d->npass && q < cap; ++q) rad[q] = (int)((d->codes >> (5 * q)) & 31);
+  return d->npass;
+}
+
 int gdsp_plan_info(const gdsp_plan *plan, int64_t *n, int64_t *m, int64_t *n1, int64_t *n2,
                    int *runtime_compiled) {
   if (!plan) return fail(GDSP_ERR_INVALID, "NULL plan");
   if (n) *n = plan->n;
-  if (m) *m = plan->m;
+  if (m) *m = plan->blufix ? plan->m_blu : plan->m;
   if (n1) *n1 = plan->n1;
   if (n2) *n2 = plan->n2;
-  if (runtime_compiled) *runtime_compiled = (plan->jit || plan->mixcol || plan->rader) ? 1 : 0;
+  if (runtime_compiled)
+    *runtime_compiled = (plan->jit || plan->mixcol || plan->rader || plan->blufix) ? 1 : 0;
   return GDSP_OK;
 }
 

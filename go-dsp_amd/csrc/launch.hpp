@@ -104,6 +104,16 @@ hipError_t jit_launch_rader(const JitRader *j, bool inv, int load, const void *i
 // launched by jit_launch_rader with the prime P's tables. nullptr: m has no
 // in-register DFT, the geometry does not fit, or the kernel did not build.
 bool pfa_cofactor_supported(int m);
+// bluestein_fixed_kernel (mixed_fixed.hpp): the fused chirp-z on a smooth
+// convolution length L = prod(rad) >= 2n - 1. blufix_length: L (and its list)
+// where the lane-cost model puts it below 0.85 of the current fused kernel
+// on m_now with list rad_now, else 0.
+int blufix_length(int64_t n, int64_t m_now, const int *rad_now, int np_now, int *rad, int *np);
+struct JitBlu;
+JitBlu *jit_blu_build(int dev, int64_t n, const int *rad, int np);  // nullptr: not built
+hipError_t jit_launch_blu(const JitBlu *j, bool inv, int load, const void *in, cd *out,
+                          int64_t batch, const cd *tw, const cd *chirp, const cd *bhat,
+                          double scale, hipStream_t s);
 JitRader *jit_rader_pfa_build(int dev, int m, const int *rad, int np);
 hipError_t jit_launch_pwelch(const JitSpec *j, const double *x, int64_t nfft, int64_t stride,
                              int64_t seg_begin, int64_t seg_end, int64_t ppw, int64_t nworkers,

@@ -1332,6 +1332,135 @@ __global__ __launch_bounds__((PfaGeo<M, R0, RS...>::WG)) void rader_pfa_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Chirp-z (Bluestein, fft/bluestein.go:68-94) with the convolution on a
+// smooth length L = prod(R0, RS...) >= 2n - 1 instead of NextPowerOf2(2n - 1)
+// (bluestein.go:70): the same linear convolution, hence the same DFT, on up
+// to half the points where n sits just above a power of 2 (n = 4099: L =
+// 8232 against 16384). The inlined mixed-radix chain (fixed_chain_to) twice,
+// one transform per workgroup slot:
+//  1. the first pass loads a[i] = x[i] conj(w_i) (i < n; zero for n <= i < L)
+//     straight from HBM (element j + r L / R0 of the slot's row: each wave-
+//     instruction a contiguous run) — chirp = conj(w), a table every slot
+//     re-reads from L2;
+//  2. FFT_L, then C = conj(A bhat) in the last pass's registers (bhat =
+//     FFT_L(b) / L, built at plan creation with the engine itself);
+//  3. an LDS exchange into natural order, FFT_L again;
+//  4. X[k] = conj(C'[k]) chirp[k] for k < n from the last pass's registers
+//     (the outputs k >= n are not stored). INV: conj in, conj and 1/n out.
+// SPLIT (L > 4096): the exchanges as real then imaginary halves.
+template <bool INV, int LOAD, bool SPLIT, bool SWZ, int NLEN, int R0, int... RS>
+__global__ __launch_bounds__((FixedGeo<R0, RS...>::WG)) void bluestein_fixed_kernel(
+    const void *__restrict__ in, cd *__restrict__ out, int64_t batch, const cd *__restrict__ tw,
+    const cd *__restrict__ chirp, const cd *__restrict__ bhat, double scale) {
+  using G = FixedGeo<R0, RS...>;
+  constexpr int L = G::N, T1 = G::T1;
+  static_assert(2 * NLEN - 1 <= L, "the convolution must hold 2n - 1 points");
+  using First = FPass<R0, L, 1, T1>;
+  using FL = FixedLast<R0, RS...>;
+  using Last = typename FL::Pass;
+  constexpr int RL = FL::R, NSL = L / RL;
+  __shared__ double lds[G::TPW * (SPLIT ? G::SLOTS : 2 * G::SLOTS)];
+  const int sub = G::TPW == 1 ? 0 : (int)threadIdx.x / T1;
+  const int tl = (int)threadIdx.x - sub * T1;
+  const int64_t row = xcd_remap(blockIdx.x, gridDim.x) * G::TPW + sub;
+  const bool valid = row < batch;
+  const int64_t lrow = valid ? row : batch - 1;  // a slot past the batch reads a valid row
+  double *ld = lds + sub * (SPLIT ? G::SLOTS : 2 * G::SLOTS);
+  // 1. a = x conj(w), zero-padded to L, into the first pass
+  First p0;
+#pragma unroll
+  for (int jj = 0; jj < First::J; ++jj) {
+    const int j = tl + jj * T1;
+    if (First::act(j, true)) {
+#pragma unroll
+      for (int r = 0; r < R0; ++r) {
+        const int i = j + r * First::NB;
+        cd a = {0.0, 0.0};
+        if (r * First::NB < NLEN && i < NLEN) {
+          cd x;
+          if constexpr (LOAD == LOAD_REAL) {
+            x = {ld_nt(reinterpret_cast<const double *>(in) + lrow * NLEN + i), 0.0};
+          } else {
+            x = ld_nt(reinterpret_cast<const cd *>(in) + lrow * NLEN + i);
+            if constexpr (INV) x.y = -x.y;
+          }
+          a = cmul(x, chirp[i]);
+        }
+        p0.v[jj][r] = a;
+      }
+    }
+  }
+  p0.compute(tl, true, tw);
+  Last keep;
+  if constexpr (sizeof...(RS) == 0) {
+    keep = p0;
+  } else {
+    auto sink = [&](const Last &c) { keep = c; };
+    fixed_chain_to<SPLIT, SWZ, L, T1, R0, 0, First, decltype(sink), RS...>(p0, tl, true, ld, tw,
+                                                                          sink);
+  }
+  // 2. C = conj(A bhat)
+#pragma unroll
+  for (int jj = 0; jj < Last::J; ++jj) {
+    const int j = tl + jj * T1;
+    if (Last::act(j, true)) {
+      const int kb = j % NSL, o = (j - kb) * RL + kb;
+#pragma unroll
+      for (int r = 0; r < RL; ++r) keep.v[jj][r] = conjg(cmul(keep.v[jj][r], bhat[o + r * NSL]));
+    }
+  }
+  // 3. natural order, FFT_L
+  const int t2 = opaque_int(tl);
+  const cd *tw2 = opaque_ptr(tw);
+  First p1;
+  __syncthreads();  // the last exchange's reads are done
+  if constexpr (SPLIT) {
+    keep.template store_lds<0, SWZ>(t2, true, ld);
+    __syncthreads();
+    p1.template load_lds<0, SWZ>(t2, true, ld);
+    __syncthreads();
+    keep.template store_lds<1, SWZ>(t2, true, ld);
+    __syncthreads();
+    p1.template load_lds<1, SWZ>(t2, true, ld);
+  } else {
+    keep.template store_lds<2, SWZ>(t2, true, ld);
+    __syncthreads();
+    p1.template load_lds<2, SWZ>(t2, true, ld);
+  }
+  p1.compute(t2, true, tw2);
+  Last fin;
+  if constexpr (sizeof...(RS) == 0) {
+    fin = p1;
+  } else {
+    __syncthreads();
+    auto sink = [&](const Last &c) { fin = c; };
+    fixed_chain_to<SPLIT, SWZ, L, T1, R0, 0, First, decltype(sink), RS...>(p1, t2, true, ld, tw2,
+                                                                          sink);
+  }
+  // 4. X[k] = conj(fin[k]) chirp[k], k < n
+  if (valid) {
+    const cd *ch = opaque_ptr(chirp);
+    cd *dst = out + row * NLEN;
+#pragma unroll
+    for (int jj = 0; jj < Last::J; ++jj) {
+      const int j = t2 + jj * T1;
+      if (Last::act(j, true)) {
+        const int kb = j % NSL, o = (j - kb) * RL + kb;
+#pragma unroll
+        for (int r = 0; r < RL; ++r) {
+          const int k = o + r * NSL;
+          if (r * NSL < NLEN && k < NLEN) {
+            cd y = cmul(conjg(fin.v[jj][r]), ch[k]);
+            if constexpr (INV) y = {y.x * scale, -y.y * scale};
+            st_nt(dst + k, y);
+          }
+        }
+      }
+    }
+  }
+}
+
 #ifndef __HIPCC_RTC__
 // Workers per workgroup of the fused Pwelch on d's list, 0 where d is not
 // this list or where a pair's samples (span = stride + nfft doubles) exceed

@@ -325,6 +325,61 @@ bool jit_radices(int n, int *rad, int *npass) {
   return true;
 }
 
+// The convolution length of the smooth-L chirp-z (bluestein_fixed_kernel) for
+// n, if one beats the current fused chirp-z's M by the lane-cost model:
+// among L in [2n - 1, M), with a list of 2-4 passes of radices <= 16 (the
+// cheap DFTs; 25 / 20 / odd primes above 13 cost 14-34 FP64 operations per
+// point) within 1024 threads per transform, the L of the lowest L x
+// lane_cost; taken only where that is below 0.85 of the current kernel's
+// (M x lane_cost of its list: radix-16 passes for a power of 2, 16 x RB x 16
+// for the M = 6144 / 3072 kernel).
+int blufix_length(int64_t n, int64_t m_now, const int *rad_now, int np_now, int *rad, int *np) {
+  if (n < 2 || 2 * n - 1 > 16384 || m_now <= 2 * n - 1) return 0;
+  int t_now = 0, tpw_now = 0;
+  fixed_geo(rad_now, np_now, &t_now, &tpw_now);
+  double best = 0.85 * (double)m_now * lane_cost(rad_now, np_now, t_now);
+  int bl = 0;
+  static const int small[] = {16, 15, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2};
+  for (int64_t L = 2 * n - 1; L < m_now && L <= 16384; ++L) {
+    int64_t f = L;
+    for (int q : {2, 3, 5, 7, 11, 13})
+      while (f % q == 0) f /= q;
+    if (f != 1 || (L & (L - 1)) == 0) continue;
+    // every list of 2-4 radices <= 16 for L: the lowest L x lane_cost
+    int cur[4];
+    auto rec = [&](auto &&self, int64_t left, int depth) -> void {
+      if (left == 1) {
+        if (depth < 2) return;
+        int t1 = 0, tpw = 0;
+        fixed_geo(cur, depth, &t1, &tpw);
+        if (t1 > 1024) return;
+        const double c = (double)L * lane_cost(cur, depth, t1);
+        if (c < best) {
+          best = c;
+          bl = (int)L;
+          for (int q = 0; q < depth; ++q) rad[q] = cur[q];
+          *np = depth;
+        }
+        return;
+      }
+      if (depth == 4) return;
+      for (int r : small)
+        if (left % r == 0) {
+          cur[depth] = r;
+          self(self, left / r, depth + 1);
+        }
+    };
+    rec(rec, L, 0);
+  }
+  return bl;
+}
+
+struct JitBlu {  // bluestein_fixed_kernel for one n on one L
+  hipModule_t mod = nullptr;
+  hipFunction_t fwd = nullptr, inv = nullptr, real = nullptr;
+  int n = 0, wg = 0, tpw = 0;
+};
+
 namespace {
 
 // Compile `names` (kernel template instances of mixed_fixed.hpp) for device
@@ -641,6 +696,50 @@ JitRader *jit_rader_pfa_build(int dev, int m, const int *rad, int np) {
   j->tpw = tpw;
   j->wg = wg;
   return j;
+}
+
+JitBlu *jit_blu_build(int dev, int64_t n, const int *rad, int np) {
+  if (!jit_enabled() || np < 1) return nullptr;
+  int L = 1;
+  for (int q = 0; q < np; ++q) L *= rad[q];
+  int t1 = 0, tpw = 0;
+  fixed_geo(rad, np, &t1, &tpw);
+  const bool split = L > 4096;  // as FixedGeo's exchange in spec_launch
+  if (t1 > 1024 || 2 * n - 1 > L) return nullptr;
+  const std::string list = radix_list(rad, np), sw = rad[0] % 2 == 0 ? "true" : "false";
+  const std::string sp = split ? "true" : "false", ns = ", " + std::to_string(n);
+  const std::vector<std::string> names = {
+      "&gdsp::bluestein_fixed_kernel<false, 0, " + sp + ", " + sw + ns + list + ">",
+      "&gdsp::bluestein_fixed_kernel<true, 0, " + sp + ", " + sw + ns + list + ">",
+      "&gdsp::bluestein_fixed_kernel<false, 1, " + sp + ", " + sw + ns + list + ">"};
+  hipModule_t mod = nullptr;
+  std::vector<hipFunction_t> fs;
+  if (!compile_module(dev, names, "chirp-z kernel for n = " + std::to_string(n) + " on L = " +
+                                      std::to_string(L) + " (" + list.substr(2) + ")",
+                      &mod, fs))
+    return nullptr;
+  JitBlu *j = new JitBlu;
+  j->mod = mod;
+  j->fwd = fs[0];
+  j->inv = fs[1];
+  j->real = fs[2];
+  j->n = (int)n;
+  j->tpw = tpw;
+  j->wg = t1 * tpw;
+  return j;
+}
+
+hipError_t jit_launch_blu(const JitBlu *j, bool inv, int load, const void *in, cd *out,
+                          int64_t batch, const cd *tw, const cd *chirp, const cd *bhat,
+                          double scale, hipStream_t s) {
+  if (load == LOAD_REAL && inv) return hipErrorInvalidValue;
+  const int64_t nblk = (batch + j->tpw - 1) / j->tpw;
+  if (batch < 1 || nblk > 0x7fffffff) return hipErrorInvalidValue;
+  hipFunction_t f = inv ? j->inv : (load == LOAD_REAL ? j->real : j->fwd);
+  void *args[] = {(void *)&in,    (void *)&out,  (void *)&batch, (void *)&tw,
+                  (void *)&chirp, (void *)&bhat, (void *)&scale};
+  return hipModuleLaunchKernel(f, (unsigned)nblk, 1, 1, (unsigned)j->wg, 1, 1, 0, s, args,
+                               nullptr);
 }
 
 hipError_t jit_launch_rader(const JitRader *j, bool inv, int load, const void *in, cd *out,

@@ -54,6 +54,11 @@ class Plan:
         self.runtime_compiled = bool(rc.value)
         # output parts of the chirp-z kernel (> 1: n in (8192, 14563] on M = 16384)
         self.parts = int(lib().gdsp_plan_parts(self.handle))
+        # the mixed-radix passes (kind 5: the transform; 7 / 8: the Rader
+        # convolution's), () for the other kinds
+        r = (ctypes.c_int * 16)()
+        k = int(lib().gdsp_plan_radices(self.handle, r, 16))
+        self.radices = tuple(r[:min(k, 16)])
 
 
 _plans: dict = {}

@@ -206,6 +206,7 @@ ALGO_NO_CHIRPZ_PARTS = 2
 ALGO_CHIRPZ_POW2 = 4
 ALGO_CHIRPZ_UNFUSED = 8
 ALGO_NO_RADER = 16
+ALGO_NO_RACE = 32
 
 
 def SetAlgorithm(flags: int = ALGO_DEFAULT) -> None:

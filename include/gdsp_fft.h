@@ -86,7 +86,13 @@ enum {
   /* primes n <= 8193 whose n - 1 has a radix list, and the composites of
    * plan kind 8, on the chirp-z kernels instead of Rader's algorithm (plan
    * kinds 7 and 8) */
-  GDSP_ALGO_NO_RADER = 16
+  GDSP_ALGO_NO_RADER = 16,
+  /* no plan-time measurement: where the default races two kernels on
+   * synthetic rows when a plan is built (plan kind 8 against the chirp-z
+   * plan it would replace; the fused chirp-z on a smooth convolution length
+   * against the one on a power of 2) and keeps the faster, take the
+   * cost model's candidate instead */
+  GDSP_ALGO_NO_RACE = 32
 };
 /* Unknown bits → GDSP_ERR_INVALID (the selection is left unchanged). */
 int gdsp_set_algorithm(unsigned flags);
@@ -277,6 +283,11 @@ int gdsp_plan_kind(const gdsp_plan *plan);
  * runtime-compiled specialisation backs it (1) or not (0). 0 where n/a. */
 int gdsp_plan_info(const gdsp_plan *plan, int64_t *n, int64_t *m, int64_t *n1, int64_t *n2,
                    int *runtime_compiled);
+/* The radix list of a plan's mixed-radix passes: kind 5 its transform's,
+ * kind 7 the cyclic convolution's (n - 1), kind 8 the prime factor's
+ * convolution (n2 - 1). Writes min(count, cap) radices and returns the
+ * count; 0 for the other kinds. */
+int gdsp_plan_radices(const gdsp_plan *plan, int *rad, int cap);
 /* Output parts of a kind-3 plan: 1 for the one-convolution chirp-z of
  * bluestein.go:68-94; P > 1 when n in (8192, 14563] (NextPowerOf2(2n-1) =
  * 32768, beyond one kernel) runs as P fused convolutions of M = 16384, each

@@ -551,7 +551,7 @@ def test_plan_kinds(gdsp):
     assert D.plan(4096).kind == 1
     assert D.plan(1 << 16).kind == 2
     assert D.plan(3000).kind == 5  # 2^3 3 5^3: mixed radix
-    assert D.plan(4097).kind == 8  # 17 * 241: prime-factor Rader (240 = 16 * 15)
+    assert D.plan(4097).kind in (3, 8)  # 17 * 241: prime-factor Rader where it wins the race
     assert D.plan(2062).kind == 3  # 2 * 1031, 1030 = 2 * 5 * 103: fused Bluestein
     assert D.plan(10000).kind == 6  # 16 x 625: mixed four-step (power-of-2 columns)
     assert D.plan(44100).kind == 6  # 25 x 1764: mixed four-step (single-radix columns)
@@ -1364,6 +1364,21 @@ def test_rader_pfa_vs_oracle(gdsp, oracle, n):
     D = __import__("importlib").import_module("go-dsp_amd.device")
     F = __import__("importlib").import_module("go-dsp_amd.fft")
     M, P = _pfa_split(n)
+    # the default plan races kind 8 against the chirp-z plan and keeps the
+    # faster: either way the oracle's results
+    assert D.plan(n).kind in (3, 8)
+    x = np.random.default_rng(n).uniform(-1, 1, (3, n)).astype(np.complex128)
+    assert row_nrel(gdsp.fft.FFTBatch(x), oracle.fft_rows(x)) < TOL
+    # the prime-factor kernel itself, without the race
+    F.SetAlgorithm(F.ALGO_NO_RACE)
+    try:
+        _pfa_checks(gdsp, oracle, D, F, n, M, P)
+    finally:
+        F.SetAlgorithm(0)
+
+
+def _pfa_checks(gdsp, oracle, D, F, n, M, P):
+    import torch
     p = D.plan(n)
     assert (p.kind, p.n1, p.n2, p.m, p.runtime_compiled) == (8, M, P, P - 1, True), \
         (n, p.kind, p.n1, p.n2, p.m)
@@ -1384,12 +1399,12 @@ def test_rader_pfa_vs_oracle(gdsp, oracle, n):
     x = rng.uniform(-1, 1, (3, n)) + 1j * rng.uniform(-1, 1, (3, n))
     assert nrel(gdsp.fft.FFT(x[0]), oracle.fft(x[0])) < TOL
     assert nrel(gdsp.fft.IFFT(x[1]), oracle.ifft(x[1])) < TOL
-    F.SetAlgorithm(F.ALGO_NO_RADER)
+    F.SetAlgorithm(F.ALGO_NO_RADER | F.ALGO_NO_RACE)
     try:
         assert D.plan(n).kind in (3, 4)
         yc = gdsp.fft.FFTBatch(x)
     finally:
-        F.SetAlgorithm(0)
+        F.SetAlgorithm(F.ALGO_NO_RACE)
     assert row_nrel(yc, oracle.fft_rows(x)) < TOL
 
 
@@ -1397,6 +1412,15 @@ def test_rader_pfa_every_cofactor(gdsp, oracle):
     """Every cofactor M = 2 ... 32 beside P = 37 (36 = the Rader list): the
     native in-register DFTs and the coprime splits (14 = 2 x 7, 18 = 2 x 9,
     21, 22, 24, 26, 28, 30); 27 = 3^3 has neither (chirp-z)."""
+    F = __import__("importlib").import_module("go-dsp_amd.fft")
+    F.SetAlgorithm(F.ALGO_NO_RACE)
+    try:
+        _pfa_cofactors(oracle)
+    finally:
+        F.SetAlgorithm(0)
+
+
+def _pfa_cofactors(oracle):
     import torch
     D = __import__("importlib").import_module("go-dsp_amd.device")
     for M in range(2, 33):
@@ -1422,7 +1446,17 @@ def test_rader_pfa_large_batch_properties(gdsp):
     linearity on every row, eight rows against numpy."""
     import torch
     D = __import__("importlib").import_module("go-dsp_amd.device")
+    F = __import__("importlib").import_module("go-dsp_amd.fft")
     n, batch = 3027, 65536
+    F.SetAlgorithm(F.ALGO_NO_RACE)
+    try:
+        _pfa_large_batch(D, n, batch)
+    finally:
+        F.SetAlgorithm(0)
+
+
+def _pfa_large_batch(D, n, batch):
+    import torch
     assert D.plan(n).kind == 8
     g = torch.Generator(device="cuda").manual_seed(11)
     x = torch.complex(torch.rand(batch, n, dtype=torch.float64, device="cuda", generator=g) - 0.5,
@@ -1437,3 +1471,56 @@ def test_rader_pfa_large_batch_properties(gdsp):
     rows = [0, 1, 777, 4096, 30000, 65534, 65535, 12345]
     xs = x[rows].cpu().numpy()
     assert row_nrel(y[rows].cpu().numpy(), np.fft.fft(xs, axis=1)) < 1e-13
+
+
+# ---- chirp-z on a smooth convolution length (bluestein_fixed_kernel) ---------------
+# the fused chirp-z (plan kind 3) with L >= 2n - 1 smooth instead of
+# bluestein.go:70's NextPowerOf2(2n - 1) where the lane-cost model expects it
+# cheaper: the same linear convolution, hence the same DFT
+BLUFIX_CASES = [1031, 2062, 4099, 4402, 4981, 5402, 6011, 6143]
+
+
+@pytest.mark.parametrize("n", BLUFIX_CASES)
+def test_chirpz_smooth_l_vs_oracle(gdsp, oracle, n):
+    D = __import__("importlib").import_module("go-dsp_amd.device")
+    F = __import__("importlib").import_module("go-dsp_amd.fft")
+    assert D.plan(n).kind == 3  # (smooth L or not: the race decides)
+    x = np.random.default_rng(n).uniform(-1, 1, (3, n)).astype(np.complex128)
+    assert row_nrel(gdsp.fft.FFTBatch(x), oracle.fft_rows(x)) < TOL
+    F.SetAlgorithm(F.ALGO_NO_RACE)  # the model's candidate, L smooth
+    try:
+        _blufix_checks(gdsp, oracle, D, F, n)
+    finally:
+        F.SetAlgorithm(0)
+
+
+def _blufix_checks(gdsp, oracle, D, F, n):
+    import torch
+    p = D.plan(n)
+    L = p.m
+    assert p.kind == 3 and p.runtime_compiled and L >= 2 * n - 1 and L & (L - 1), (n, p.kind, L)
+    assert int(np.prod(p.radices)) == L and max(p.radices) <= 16, p.radices
+    rng = np.random.default_rng(9000 + n)
+    for batch in (1, 7):
+        x = rng.uniform(-1, 1, (batch, n)) + 1j * rng.uniform(-1, 1, (batch, n))
+        ref = oracle.fft_rows(x)
+        y = gdsp.fft.FFTBatch(x)
+        assert row_nrel(y, ref) < TOL
+        assert row_nrel(y, np.fft.fft(x, axis=1)) < 1e-13
+        assert row_nrel(gdsp.fft.FFTBatch(x, inverse=True), oracle.ifft_rows(x)) < TOL
+        xr = rng.uniform(-1, 1, (batch, n))
+        assert row_nrel(gdsp.fft.FFTRealBatch(xr), oracle.fft_rows(xr.astype(np.complex128))) < TOL
+        xt = torch.from_numpy(x).cuda()
+        D.fft_batch(xt, xt)
+        torch.cuda.synchronize()
+        assert row_nrel(xt.cpu().numpy(), ref) < TOL
+    x = rng.uniform(-1, 1, (3, n)) + 1j * rng.uniform(-1, 1, (3, n))
+    assert nrel(gdsp.fft.FFT(x[0]), oracle.fft(x[0])) < TOL
+    F.SetAlgorithm(F.ALGO_CHIRPZ_POW2 | F.ALGO_NO_RACE)
+    try:
+        q = D.plan(n)
+        assert q.kind == 3 and q.m & (q.m - 1) == 0, (q.kind, q.m)
+        yc = gdsp.fft.FFTBatch(x)
+    finally:
+        F.SetAlgorithm(F.ALGO_NO_RACE)
+    assert row_nrel(yc, oracle.fft_rows(x)) < TOL
