@@ -123,15 +123,15 @@ __host__ __device__ constexpr int blu_epi_mode(int log2m, int log2e) {
 // The input then fills more than half of M, so only the output side is pruned.
 // Rows ahead a chirp-z block touches for its successor on the XCD (0: off).
 // chirpz3000 2.95-3.05 -> 2.80-2.89 ms at 8-32, 2.84-2.85 at 48, 2.94-3.03 at
-// 64-128 (scripts/dev/blu_pf_ab.sh); blocks of several transforms (M <= 2048)
+// 64-128 (scripts/archive/dev/blu_pf_ab.sh); blocks of several transforms (M <= 2048)
 // touch the same slot's row kBluPf blocks on: primes 13..1021 10-22 %
-// faster (scripts/dev/blu_pfall_ab.sh)
+// faster (scripts/archive/dev/blu_pfall_ab.sh)
 constexpr int kBluPf = 16;
 // Twiddle powers of the radix-8 passes by the three-term recurrence
 // (pass_compute CHEB; one transform per workgroup): chirpz3000 2.65-2.67
 // against 2.71-2.74 ms, parity 1.58e-15 against 1.56e-15 vs the oracle. The
 // radix-32 passes keep complex products: the recurrence there bought 0.3 %
-// for 5.5e-15 (scripts/gpu_r03_cheb.sh)
+// for 5.5e-15 (scripts/archive/gpu_r03_cheb.sh)
 constexpr int kBluChebR = 8;
 constexpr int kBluPf14 = 4;     // M = 16384, one block per CU: 2-4 % faster than 8 or 16
 constexpr int kBluPfParts = 2;  // PARTS: the row's part-0 block touches 2 rows on
@@ -1126,10 +1126,10 @@ static hipError_t launch_blu_t(const cd *in, cd *out, int64_t n, int64_t batch, 
   // 4099..8191 (M = 16384) 2-5 %; round 3, with
   // the 16-point kernel held to 128 VGPRs (amdgpu_waves_per_eu: at 130 it ran
   // one 512-thread block per CU, 4.37 ms) and n-aware pruning (KN = 6):
-  // 3.27-3.34 against 2.80 ms (scripts/gpu_r03_e16.sh). The 32 points
+  // 3.27-3.34 against 2.80 ms (scripts/archive/gpu_r03_e16.sh). The 32 points
   // alone hold 128 VGPRs, so a third wave per SIMD is out of reach: with the
   // exchange through half-size buffers (34 KiB of LDS) and 168 VGPRs the
-  // kernel spills 206 registers, 6.20 against 2.62 ms (scripts/gpu_r03_occ.sh)
+  // kernel spills 206 registers, 6.20 against 2.62 ms (scripts/archive/gpu_r03_occ.sh)
   if constexpr (LOG2M == 13 || LOG2M == 14) {
     using G5 = Geo<LOG2M, 5>;
     const int64_t nb5 = (batch + G5::TPW - 1) / G5::TPW;
@@ -1286,7 +1286,7 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
     }
     // (F = 8192 held to four waves per SIMD with the window read from L1/L2,
     // two workgroups per CU at 128 VGPRs and 62 spilled: 1.64-1.65 against
-    // 1.16-1.17 ms per 2^28 samples; scripts/gpu_r05_h13.sh)
+    // 1.16-1.17 ms per 2^28 samples; scripts/archive/gpu_r05_h13.sh)
     case 13: return launch_pwh_t<13>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
     // F = 16384: the exchange buffer alone takes 136 KiB, so the window is
     // re-read from L1/L2 instead of living in LDS
@@ -1295,7 +1295,7 @@ hipError_t launch_pwelch_half(int log2f, const double *x, int64_t seg_begin, int
       // 2^28 samples for 16 (1024 threads); both spill (re-measured at the end
       // of round 5 on the linear exchange slots: 256 VGPRs, 123 spilled, two
       // waves per SIMD, 1.91 ms, against 128 VGPRs, 67 spilled, four waves,
-      // 2.00-2.01 ms; scripts/gpu_r05_h16.sh)
+      // 2.00-2.01 ms; scripts/archive/gpu_r05_h16.sh)
       return launch_pwh_t<14, 1, 1, 5>(x, seg_begin, seg_end, ppw, nworkers, win, tw, partial, s);
     }
     default: return hipErrorInvalidValue;

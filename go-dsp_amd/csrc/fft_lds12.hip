@@ -3,7 +3,7 @@
 // it alone is compiled with the wave-priority pass (Makefile: each wave runs
 // at raised priority until its row loads are issued): 1.3598 / 1.3414 against
 // 1.3703 / 1.3515 ms per 65536 transforms; the same pass made the n = 3000
-// mixed kernel 4 % and FFT2 1-2 % slower (scripts/gpu_r03_flags.sh).
+// mixed kernel 4 % and FFT2 1-2 % slower (scripts/archive/gpu_r03_flags.sh).
 #include "lds_kernel.hpp"
 
 namespace gdsp {

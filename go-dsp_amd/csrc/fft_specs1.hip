@@ -2,13 +2,13 @@
 // Each Spec is a radix list (first pass .. last pass); the batched transform
 // and fused Pwelch kernels for it are instantiated here (mixed_fixed.hpp).
 // Radix lists: as few passes as the radices <= 25 allow, full waves where
-// possible, a power-of-2 radix last. Late in round 5 (scripts/gpu_r05_specd.sh,
+// possible, a power-of-2 radix last. Late in round 5 (scripts/archive/gpu_r05_specd.sh,
 // profiles/r05/radix_lists_ab.txt) lists that keep more of a transform's
 // threads busy in every pass replaced 100 (25 4), 300 (25 12), 360 (12 3 10),
 // 400 (25 16), 600 (25 6 4), 640 (16 10 4) and 1470 (7 5 6 7): fused Pwelch
 // per 2^28 samples -10 to -64 % (600: 2.98 -> 1.06 ms), batched FFT 0 to
 // -11 %; Rader's 101 / 601 -17 / -9 %, 641 +8 %.
-// Last (scripts/gpu_r05_t12.sh, f2.sh), the three-pass lists the fused
+// Last (scripts/archive/gpu_r05_t12.sh, f2.sh), the three-pass lists the fused
 // Pwelch took for 250 and 500 (1.62 -> 0.87 and 1.57 -> 0.86 ms per 2^28
 // samples) as FFT lists too: 250 10 5 5 0.752 against 0.777-0.781 ms per
 // 2^27 samples (Rader's 251 1.16 against 1.26), 500 10 5 10 0.760-0.762

@@ -2,7 +2,7 @@
 // Each Spec is a radix list (first pass .. last pass); the batched transform
 // and fused Pwelch kernels for it are instantiated here (mixed_fixed.hpp).
 // Radix lists: as few passes as the radices <= 25 allow, full waves where
-// possible, a power-of-2 radix last. Late in round 5 (scripts/gpu_r05_specd.sh,
+// possible, a power-of-2 radix last. Late in round 5 (scripts/archive/gpu_r05_specd.sh,
 // profiles/r05/radix_lists_ab.txt) lists that keep more of a transform's
 // threads busy in every pass replaced 720 (20 9 4), 750 (25 5 6), 1080
 // (15 9 8), 1152 (16 9 8), 1280 (16 10 8), 2160 (15 9 16), 1125 (25 5 9) and

@@ -2,15 +2,15 @@
 // Each Spec is a radix list (first pass .. last pass); the batched transform
 // and fused Pwelch kernels for it are instantiated here (mixed_fixed.hpp).
 // Radix lists: as few passes as the radices <= 25 allow, full waves where
-// possible, a power-of-2 radix last. Round 5 (scripts/gpu_r05_spec6.sh, two
+// possible, a power-of-2 radix last. Round 5 (scripts/archive/gpu_r05_spec6.sh, two
 // alternating rounds, profiles/r05/radix_lists_ab.txt): lists whose passes
 // keep more of the transform's threads busy (tools/spec_candidates.py) took
 // 2880 from 20 9 16, 3200 from 20 10 16, 3840 from 20 12 16, 4500 from
 // 25 9 20 and 6000 from 25 12 20: batched FFT -7 to -22 %, fused Pwelch
-// (half overlap) -20 to -38 % (6000 equal); then (scripts/gpu_r05_specd.sh)
+// (half overlap) -20 to -38 % (6000 equal); then (scripts/archive/gpu_r05_specd.sh)
 // 8000 from 25 20 16 (-8 % / -20 %) and 5880 from 20 6 7 7 (-4 % / -12 %,
 // Rader's 5881 -4 %). 2560, 4000 and the others keep their lists. Last
-// (scripts/gpu_r05_f1.sh), the four-pass lists the fused Pwelch got for
+// (scripts/archive/gpu_r05_f1.sh), the four-pass lists the fused Pwelch got for
 // itself (fft_specs0.hip, specspw) as FFT lists too: 5000 10 10 10 5 0.774
 // against 0.942-0.945 ms per 2^27 samples, 7500 20 5 5 15 0.813-0.821
 // against 0.876-0.879, 3750 15 5 5 10 0.938-0.946 against 0.986-0.992; 768,

@@ -747,7 +747,7 @@ bool rader_radices(int64_t N, std::vector<int> &rad) {
   // profiles/r05/rader_radix_ab.txt; the fused Pwelch's own four-pass lists
   // are slower here too: 3001 on 15 5 5 8 1.41-1.42 against 1.30-1.31 ms per
   // 2^27 samples, 4001 on 10 10 10 4 1.63 against 1.40-1.41,
-  // scripts/gpu_r05_raderpw.sh)
+  // scripts/archive/gpu_r05_raderpw.sh)
   if (is_pow2(N)) {
     int a = ilog2(N);
     while (a >= 4) {
@@ -1400,7 +1400,7 @@ int exec_fourstep(const gdsp_plan *p, const void *in, cd *out, int64_t batch, bo
   // Few transforms: rows of 8192 leave the row pass at <= 256 workgroups, and
   // rows of 4096 (twice the rows, the column DFT twice as long) measured
   // 5-20 % faster per call at batch * 2^(ln-13) <= 256 (2^17..2^21 at batch 1:
-  // 2^20 0.0275 -> 0.026 ms, 2^18 0.022 -> 0.0177; scripts/dev/fs_split_ab.py,
+  // 2^20 0.0275 -> 0.026 ms, 2^18 0.022 -> 0.0177; scripts/archive/dev/fs_split_ab.py,
   // profiles/r02/fs_split.jsonl); larger batches keep 8192.
   if (lc == 13 && lr + 1 <= gdsp::kColMaxLog2 && (batch << lr) <= 256) {
     lc = 12;

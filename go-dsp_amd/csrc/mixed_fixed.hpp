@@ -426,7 +426,7 @@ struct FixedTwN {
 // 1.33; 2205 / 1102: 1.24 -> 1.55), as did staging each pair through the
 // exchange buffer without the DMA (10 10 10, 12 16 8, 15 8 4: 7-20 %).
 // Lists whose fused Pwelch is faster held to more waves per SIMD than the
-// compiler's natural count, measured per list (scripts/gpu_r05_w4.sh, w5.sh,
+// compiler's natural count, measured per list (scripts/archive/gpu_r05_w4.sh, w5.sh,
 // profiles/r05/pwelch_wpe_ab.txt); it pays where it adds a resident workgroup
 // per CU for few spills:
 //  - 6000 15 5 5 16 (the fused Pwelch's own list; seven-wave workgroups) at
@@ -439,7 +439,7 @@ struct FixedTwN {
 // two or more workgroups per CU already); the other lists above 4096 spill
 // 140-510 VGPRs held to two workgroups per CU; and of seven more lists with
 // 4-42 spills at the cap that adds a workgroup per CU (160, 150, 1000, 882,
-// 4410, 2880, 2560; scripts/gpu_r05_w6.sh) six lost 2-58 % and 150 gained
+// 4410, 2880, 2560; scripts/archive/gpu_r05_w6.sh) six lost 2-58 % and 150 gained
 // 2 %. 0: no override.
 template <int... RS>
 struct PwWpe {

@@ -44,7 +44,7 @@ namespace gdsp {
 // stage as FMAs (w_j z_j +- w_(j+8) z_(j+8): 16 fewer FP64 instructions per
 // thread and pair), 2.92 against 2.74 ms — the weights stay live in 32 more
 // registers through the first DFT.
-// And for a third wave per SIMD (scripts/gpu_r03_occ.sh): the exchange through
+// And for a third wave per SIMD (scripts/archive/gpu_r03_occ.sh): the exchange through
 // a buffer of half a transform (each component in two rounds, 17 KiB: three
 // workgroups per CU by LDS) with the VGPRs capped at 168 spills 106-186
 // registers, 5.95 ms without the next pair's samples in flight (touching its

@@ -4,7 +4,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/r06d
 export GDSP_JIT_CACHE=$GRAFT_REPO_ROOT/gpurun_out/jitcache
-timeout -k 10 700 python -u -m pytest tests/test_parity_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread -k "rader_pfa or plan_kinds or smooth_l or chirpz or random_lengths or rader" > gpurun_out/r06d/pytest.log 2>&1; rc=$?
+timeout -k 10 700 python -u -m pytest tests/test_parity_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread -k "smooth_l" > gpurun_out/r06d/pytest.log 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -5 gpurun_out/r06d/pytest.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 500 python -u scripts/sweep_nonsmooth.py > gpurun_out/r06d/nonsmooth_sweep.jsonl 2> gpurun_out/r06d/sweep.err; rc=$?
 echo "sweep rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/r06d/sweep.err; exit $rc; }

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Candidate radix lists for the compiled mixed-radix specialisations
 (fft_specs*.hip), ranked by a lane-occupancy cost model, for an A/B on the
-GPU (scripts/gpu_r05_specd.sh).
+GPU (scripts/archive/gpu_r05_specd.sh).
 
 A pass of radix R over n points has n/R butterflies; FixedGeo gives every
 transform T1 = max over passes of ceil((n/R) / jm) threads (jm = 16/R
