@@ -14,8 +14,10 @@ independent). value = 2^28 samples / max-over-ranks wall time; at N > 1 a
 weak-scaling figure (65536 rows per rank) is added as "weak_scaling".
 
 The default run also times the other BASELINE configs and nests them under
-"configs": bluestein3000, chirpz3000 and prime3001 (configs[2]; the prime n = 3001
-through the production dispatch, Rader), fft2_8192 (configs[3];
+"configs": bluestein3000, chirpz3000, prime3001 and pfa3027 (configs[2]; the prime
+n = 3001 and the composite 3027 = 3 x 1009 through the production dispatch: Rader,
+and the prime-factor Rader kernel, each with its chirp-z plan timed beside it),
+fft2_8192 (configs[3];
 rows sharded with two RCCL all-to-alls at N > 1) and pwelch (configs[4]; one
 RCCL all-reduce of the PSD accumulators). --workload X runs one alone.
 bluestein3000 is fft.FFT of N = 3000 through the production dispatch (the
@@ -50,16 +52,16 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec (tools/fp64peak.hip measures 
 # kernels whose FP64 work is taken from the committed SQ counter passes
 # (profiles/r02/sq_counters.json: 64 x (2 FMA + ADD + MUL) F64 instructions)
 SQ_KERNELS = {"radix4096": ["fft_lds_kernel<12"], "bluestein3000": ["fft_mixed_fixed_kernel"],
-              "prime3001": ["rader_fixed_kernel"],
+              "prime3001": ["rader_fixed_kernel"], "pfa3027": ["rader_pfa_kernel"],
               "chirpz3000": ["chirpz6k_kernel"], "pwelch": ["pwelch_row_kernel<12"],
               "pwelch_default": ["pwelch_wave_kernel<8"],
               "fft2_8192": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"],
               "fft2_dist": ["fft_lds_kernel<13", "colfft_tile_kernel<6", "colfft_tile_kernel<7"]}
-SQ_ROUNDS = ("r05", "r04", "r03", "r02")  # SQ counter passes quoted: the newest round that has the kernel
+SQ_ROUNDS = ("r06", "r05", "r04", "r03", "r02")  # SQ counter passes quoted: the newest round that has the kernel
 # rocprofv3 --kernel-trace --stats summaries quoted beside the event timing
 # (profiles/<round>/<workload>_kernel_stats.csv, the closing session's runs of
 # `bench.py --workload <w>`): the newest round that has the workload
-STATS_ROUNDS = ("r05", "r04", "r03", "r02")
+STATS_ROUNDS = ("r06", "r05", "r04", "r03", "r02")
 SEED = 0x5EED
 WARM_S = 0.06  # untimed GPU work before the timed steps (steady clocks; measure())
 # algorithmic bytes of one launch in the N=1 full-size configuration the
@@ -67,6 +69,7 @@ WARM_S = 0.06  # untimed GPU work before the timed steps (steady clocks; measure
 # summaries were measured on
 PROFILED_ALG_BYTES = {"radix4096": 32 * 4096 * 65536, "bluestein3000": 32 * 3000 * 65536,
                       "chirpz3000": 32 * 3000 * 65536, "prime3001": 32 * 3001 * 65536,
+                      "pfa3027": 32 * 3027 * 65536,
                       "fft2_8192": 4 * 16 * 8192 * 8192,
                       "fft2_dist": 4 * 16 * 8192 * 8192, "pwelch": 8 * (1 << 30),
                       "pwelch_default": 8 * (1 << 30),
@@ -93,13 +96,14 @@ def parse():
     return ap.parse_args()
 
 
-WORKLOADS = ["radix4096", "bluestein3000", "chirpz3000", "prime3001", "fft2_8192", "fft2_dist",
+WORKLOADS = ["radix4096", "bluestein3000", "chirpz3000", "prime3001", "pfa3027", "fft2_8192",
+             "fft2_dist",
              "pwelch", "pwelch_default",
              "fftn_512", "wav_decode", "fft_2p20", "fftreal1024"]
 # the BASELINE configs nested in the default line: configs[2] (production
 # dispatch and the reference's chirp-z algorithm), configs[3], configs[4]
-NESTED = ["bluestein3000", "chirpz3000", "prime3001", "fft2_8192", "pwelch", "pwelch_default",
-          "fftreal1024"]
+NESTED = ["bluestein3000", "chirpz3000", "prime3001", "pfa3027", "fft2_8192", "pwelch",
+          "pwelch_default", "fftreal1024"]
 HEADLINE_METRIC = "Gsamples/s + % HBM roofline, batched N=4096 complex128 FFT at 1/2/4/8 GPUs"
 
 
@@ -133,6 +137,11 @@ class Ctx:
         self.D = importlib.import_module("go-dsp_amd.device")
         self.Dd = importlib.import_module("go-dsp_amd.distributed")
         self.stream = torch.cuda.Stream(self.dev)
+        # the sources this run executes (tools/source_stamp.py), printed in the
+        # line and compared with the stamps of the profiles it quotes
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        import source_stamp
+        self.stamp = source_stamp.stamp()
 
     def barrier(self):
         if self.world > 1:
@@ -145,8 +154,8 @@ def setup(w: str, c: Ctx, weak: bool = False) -> dict:
     reference's own benchmark is fixed-work, fft/fft_test.go:262-280);
     weak=True gives every rank the full 65536 rows instead."""
     torch, D, Dd, dev, stream, rank, world = c.torch, c.D, c.Dd, c.dev, c.stream, c.rank, c.world
-    if w in ("radix4096", "bluestein3000", "chirpz3000", "prime3001"):
-        n = {"radix4096": 4096, "prime3001": 3001}.get(w, 3000)
+    if w in ("radix4096", "bluestein3000", "chirpz3000", "prime3001", "pfa3027"):
+        n = {"radix4096": 4096, "prime3001": 3001, "pfa3027": 3027}.get(w, 3000)
         chirpz = w == "chirpz3000"
         total = c.args.batch or 65536
         if weak:
@@ -165,10 +174,14 @@ def setup(w: str, c: Ctx, weak: bool = False) -> dict:
         algo = {1: "Stockham radix-16 (one kernel)", 3: "Bluestein chirp-z (fused, M=8192)",
                 5: "mixed-radix Stockham 25*15*8 (one compiled kernel)",
                 7: f"Rader (cyclic convolution of length {n - 1} = 25*15*8, two FFTs in one "
-                   "runtime-compiled kernel; the reference: Bluestein, M=8192)"}.get(kind, str(kind))
+                   "runtime-compiled kernel; the reference: Bluestein, M=8192)",
+                8: f"prime-factor Rader ({n} = {p.n1} x {p.n2}: DFT_{p.n1} per column, {p.n1} "
+                   f"Rader transforms of {p.n2} on a {p.n2 - 1}-point convolution "
+                   f"({'*'.join(map(str, p.radices))}), one runtime-compiled kernel; the "
+                   "reference: Bluestein, M=8192)"}.get(kind, str(kind))
         kernel = {1: "fft_lds_kernel<12>", 3: "bluestein_kernel<13>",
                   5: "fft_mixed_fixed_kernel<25,15,8>",
-                  7: "rader_fixed_kernel"}.get(kind, str(kind))
+                  7: "rader_fixed_kernel", 8: "rader_pfa_kernel"}.get(kind, str(kind))
         if kind == 3 and p.m == 6144:
             # 2049 <= n <= 3072: the convolution on M = 6144 (chirpz6k.hip);
             # bluestein.go:70 pads to 8192 (GDSP_ALGO_CHIRPZ_POW2 keeps it)
@@ -367,7 +380,7 @@ def parity(w: str, wl: dict, c: Ctx):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
     import oracle
-    if w in ("radix4096", "bluestein3000", "chirpz3000", "prime3001"):
+    if w in ("radix4096", "bluestein3000", "chirpz3000", "prime3001", "pfa3027"):
         x, y = wl["x"], wl["y"]
         rows = np.linspace(0, y.shape[0] - 1, c.args.check_rows).astype(int)
         xs, ys = x[rows].cpu().numpy(), y[rows].cpu().numpy()
@@ -595,7 +608,7 @@ def run(w: str, c: Ctx, weak: bool = False) -> dict:
     # configuration: scale them to this launch's share of that work (a rank's
     # shard at N>1, or a --batch override)
     share = wl["alg_bytes"] / PROFILED_ALG_BYTES[w]
-    traffic = None
+    traffic = traffic_src = None
     pmc = os.path.join(REPO, "profiles", f"pmc_{w}.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
@@ -605,6 +618,9 @@ def run(w: str, c: Ctx, weak: bool = False) -> dict:
         if isinstance(pk, str) and not wl["kernel"].startswith(pk):
             t = None  # profiled on another kernel than the one timed here
         traffic = None if t is None else int(round(t * share))
+        traffic_src = {"file": f"profiles/pmc_{w}.json", "source": pj.get("source"),
+                       "stamp": pj.get("stamp"),
+                       "same_sources": stamp_matches(pj.get("stamp"), c.stamp)}
     out = {
         "metric": wl["metric"],
         "value": round(value, 3),
@@ -620,7 +636,8 @@ def run(w: str, c: Ctx, weak: bool = False) -> dict:
                      "frac_vs_copy": round(achieved / HBM_COPY_GBS, 4),
                      "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                      "alg_bytes_per_launch": wl["alg_bytes"], "traffic": traffic,
-                     "rocprof": rocprof_info(w, wl["alg_bytes"], share)},
+                     "traffic_source": traffic_src,
+                     "rocprof": rocprof_info(w, wl["alg_bytes"], share, c.stamp)},
         "fp64": fp64_info(w, avg_launch_s, share),
         "cpu_baseline": None,  # filled in by main() after every GPU measurement
         "parity": check,
@@ -644,7 +661,8 @@ def run(w: str, c: Ctx, weak: bool = False) -> dict:
         del w8
         c.torch.cuda.empty_cache()
         return out
-    if w == "prime3001" and not weak and wl["kernel"] == "rader_fixed_kernel":
+    if (w, wl["kernel"]) in (("prime3001", "rader_fixed_kernel"),
+                             ("pfa3027", "rader_pfa_kernel")) and not weak:
         # the same prime on the chirp-z kernel it took before Rader
         # (GDSP_ALGO_NO_RADER: the fused chirp-z on M = 6144), timed the same way
         F = c.gdsp.fft
@@ -884,7 +902,8 @@ def main():
             "ms_per_step": head["ms_per_step"], "higher_is_better": True,
             "warmup_steps_run": head.get("warmup_steps_run"),
             "scaling": head["scaling"], "vs_baseline": None, "dtype": head["dtype"],
-            "data": "synthetic (splitmix64 uniform[-1,1), generated in HBM)"}
+            "data": "synthetic (splitmix64 uniform[-1,1), generated in HBM)",
+            "sources": c.stamp}
     line.update({k: head[k] for k in ("config", "roofline", "fp64", "cpu_baseline", "parity")})
     if "host_api" in head:
         line["host_api"] = head["host_api"]
@@ -945,7 +964,15 @@ def fp64_info(workload: str, launch_s: float, share: float = 1.0):
     return None
 
 
-def rocprof_info(workload: str, alg_bytes: int, share: float = 1.0):
+def stamp_matches(profiled, now):
+    """Whether a committed profile was taken on the sources this run executes
+    (tools/source_stamp.py: the kernel sources' sha256); None if unstamped."""
+    if not profiled or not now:
+        return None
+    return profiled.get("source_sha") == now.get("source_sha")
+
+
+def rocprof_info(workload: str, alg_bytes: int, share: float = 1.0, stamp=None):
     """The dominant kernel's duration from the committed rocprofv3
     --kernel-trace --stats summary of this workload (newest round; FFT2: its
     launches summed), and roofline.frac recomputed from that average: the
@@ -982,7 +1009,9 @@ def rocprof_info(workload: str, alg_bytes: int, share: float = 1.0):
                         "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
                         "over": "the timed launches of the profiled run (its last "
                                 f"{last}; warm-up excluded)",
-                        "source": f"profiles/{rnd}/{w}_kernel_trace.json"}
+                        "source": f"profiles/{rnd}/{w}_kernel_trace.json",
+                        "stamp": tr.get("stamp"),
+                        "same_sources": stamp_matches(tr.get("stamp"), stamp)}
         path = os.path.join(REPO, "profiles", rnd, f"{w}_kernel_stats.csv")
         if not os.path.exists(path):
             continue
@@ -1112,7 +1141,7 @@ def _cpu_baseline(workload: str, seconds: float, cores: int, pool: str, np, orac
     if workload == "fft2_dist":
         workload = "fft2_8192"
     n = {"radix4096": 4096, "bluestein3000": 3000, "chirpz3000": 3000, "prime3001": 3001,
-         "fft2_8192": 8192}[workload]
+         "pfa3027": 3027, "fft2_8192": 8192}[workload]
     rows = 64 if n != 8192 else 16
     x = oracle.fill_uniform(2 * n * rows, SEED).view(np.complex128).reshape(rows, n)
     done = 0

@@ -17,6 +17,7 @@ KERNELS = {"radix4096": "fft_lds_kernel<12", "bluestein3000": "fft_mixed_fixed_k
            "pwelch": "pwelch_row_kernel<12",
            "pwelch_default": "pwelch_wave_kernel<8",
            "prime3001": "rader_fixed_kernel",
+           "pfa3027": "rader_pfa_kernel",
            # one FFT2 step = row pass + the two column-tile launches: summed
            "fft2_8192": ["fft_lds_kernel<13", "colfft_tile_kernel<7", "colfft_tile_kernel<6"],
            # one FFTN step = the row pass + two column-tile axes
@@ -24,6 +25,16 @@ KERNELS = {"radix4096": "fft_lds_kernel<12", "bluestein3000": "fft_mixed_fixed_k
            "wav_decode": "wav_decode_vec_kernel",
            # one 2^20 four-step at batch 1: column tiles (256), rows of 4096, transpose
            "fft_2p20": ["colfft_tile_kernel<8", "fft_lds_kernel<12", "transpose_kernel"]}
+
+
+def session_stamp():
+    """The sources the PMC session ran on (gpurun_out/source_stamp.json,
+    written on the GPU box by the session script: tools/source_stamp.py)."""
+    p = os.path.join(REPO, "gpurun_out", "source_stamp.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f)
 
 
 def values(w, counter, kernel):
@@ -50,6 +61,7 @@ def main(w, tag):
         "hbm_bytes_per_launch": int((2 * f_kib + w_kib) * 1024),
         "correction": "FETCH_SIZE x2 (gfx950 16-B/lane streaming reads), KiB -> bytes",
         "source": f"profiles/{tag}/pmc_{w}_FETCH_SIZE.csv, profiles/{tag}/pmc_{w}_WRITE_SIZE.csv",
+        "stamp": session_stamp(),
     }
     dst = os.path.join(REPO, "profiles", tag)
     os.makedirs(dst, exist_ok=True)

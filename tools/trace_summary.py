@@ -16,6 +16,16 @@ from collections import defaultdict
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def session_stamp():
+    """The sources the profiled session ran on: gpurun_out/source_stamp.json,
+    written on the GPU box by the session script (tools/source_stamp.py)."""
+    p = os.path.join(REPO, "gpurun_out", "source_stamp.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f)
+
+
 def main(tag, steps, workloads):
     for w in workloads:
         path = os.path.join(REPO, "gpurun_out", f"prof_{w}", "run_kernel_trace.csv")
@@ -25,6 +35,7 @@ def main(tag, steps, workloads):
             d[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
         out = {"workload": w, "timed_last": steps,
                "source": f"rocprofv3 --kernel-trace of bench.py --workload {w} --steps {steps}",
+               "stamp": session_stamp(),
                "kernels": {k: v for k, v in d.items() if len(v) >= steps}}
         dst = os.path.join(REPO, "profiles", tag, f"{w}_kernel_trace.json")
         with open(dst, "w") as f:
