@@ -929,7 +929,39 @@ void free_plan_tables(gdsp_plan *p) {
   if (p->ginv) (void)hipFree(p->ginv);
 }
 
-int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false, bool nopfa = false);
+// skip: the kinds a plan built as a race's alternative leaves out
+enum { SKIP_RADER = 1, SKIP_PFA = 2 };
+int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false, int skip = 0);
+
+// Rader's plan for a prime n (kind 7, built by rader_try) against the chirp-z
+// plan n gets without it, timed (race): kept where it is 3 % faster,
+// otherwise p becomes that plan. Round 5 measured Rader 1.1-2.2x faster on a
+// sample of primes (profiles/r05/rader_sweep.jsonl); the race covers the
+// lists it did not sample (a radix-17/19/23 pass in n - 1's list: the
+// round-6 kind-8 calibration lost on those, profiles/r06/pfa_calib.jsonl).
+int rader_race(int dev, int64_t n, gdsp_plan *p) {
+  if (plan_flags() & GDSP_ALGO_NO_RACE) return GDSP_OK;
+  gdsp_plan *alt = new gdsp_plan();
+  int st = build_plan(dev, n, alt, false, SKIP_RADER | SKIP_PFA);
+  bool rader_wins = true;
+  if (st == GDSP_OK) {
+    Runner rader = [&](const cd *in, cd *out, int64_t batch, hipStream_t s) -> int {
+      return exec_plan(p, in, out, batch, false, gdsp::LOAD_COMPLEX, s);
+    };
+    Runner other = [&](const cd *in, cd *out, int64_t batch, hipStream_t s) -> int {
+      return exec_plan(alt, in, out, batch, false, gdsp::LOAD_COMPLEX, s);
+    };
+    st = race(dev, n, rader, other, 0.97, &rader_wins);
+  }
+  if (st == GDSP_OK && !rader_wins) {
+    free_plan_tables(p);
+    *p = *alt;
+  } else {
+    free_plan_tables(alt);
+  }
+  delete alt;
+  return st;
+}
 
 // A composite n <= 8192 whose largest prime factor P > 31 has a Rader plan
 // and whose cofactor M = n / P (gcd(M, P) = 1) has an in-register DFT:
@@ -972,7 +1004,7 @@ int pfa_rader_try(int dev, int64_t n, gdsp_plan *p, bool *built) {
       return GDSP_OK;
     };
     gdsp_plan *alt = new gdsp_plan();
-    int st = build_plan(dev, n, alt, false, /*nopfa=*/true);
+    int st = build_plan(dev, n, alt, false, SKIP_PFA);
     bool pfa_wins = true;
     if (st == GDSP_OK) {
       Runner other = [&](const cd *in, cd *out, int64_t batch, hipStream_t s) -> int {
@@ -1077,9 +1109,9 @@ int blufix_try(int dev, int64_t n, gdsp_plan *p, const std::vector<cd> &w) {
   return GDSP_OK;
 }
 
-// nopfa: without the prime-factor Rader plan (the alternative it is raced
-// against, pfa_rader_try)
-int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz, bool nopfa) {
+// skip (SKIP_RADER, SKIP_PFA): without those kinds, for the alternative a
+// race times them against (rader_race, pfa_rader_try)
+int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz, int skip) {
   p->device = dev;
   p->n = n;
   if (n <= 1) {
@@ -1149,9 +1181,11 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz, bool nopfa) {
   }
   if (!chirpz) {
     bool built = false;
-    STCHK(rader_try(dev, n, p, &built));
-    if (built) return GDSP_OK;
-    if (!nopfa) {
+    if (!(skip & SKIP_RADER)) {
+      STCHK(rader_try(dev, n, p, &built));
+      if (built) return rader_race(dev, n, p);
+    }
+    if (!(skip & SKIP_PFA)) {
       STCHK(pfa_rader_try(dev, n, p, &built));
       if (built) return GDSP_OK;
     }

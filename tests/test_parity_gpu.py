@@ -564,7 +564,7 @@ def test_plan_kinds(gdsp):
     assert (D.plan(64 * 8209).kind, D.plan(64 * 8209).n2) == (6, 8209)
     assert (D.plan(2 * 10007).kind, D.plan(2 * 10007).n2) == (6, 10007)
     assert D.plan(8191 * 64).kind == 6  # power-of-2 columns, chirp-z rows of 8191
-    assert (D.plan(3001).kind, D.plan(3001).m) == (7, 3000)  # prime: Rader on 25 * 15 * 8
+    assert (D.plan(3001).kind, D.plan(3001).m) in ((7, 3000), (3, 6144))  # prime: Rader (raced)
     assert D.plan(3067).kind == 3  # prime, 3066 = 2 * 3 * 7 * 73: no radix list, chirp-z
     assert D.plan(3000, chirpz=True).kind == 3
     assert D.plan(10000, chirpz=True).kind == 4
@@ -1267,9 +1267,19 @@ def test_rader_vs_oracle(gdsp, oracle, n):
     fft/bluestein.go:68-94) and numpy's float64 DFT: forward, inverse, real
     input, batches 1 and 7, in place on the device, and the same rows through
     the chirp-z plan (GDSP_ALGO_NO_RADER)."""
-    import torch
     D = __import__("importlib").import_module("go-dsp_amd.device")
     F = __import__("importlib").import_module("go-dsp_amd.fft")
+    # the default plan races Rader against chirp-z and keeps the faster
+    assert D.plan(n).kind in (3, 7)
+    F.SetAlgorithm(F.ALGO_NO_RACE)  # Rader itself
+    try:
+        _rader_checks(gdsp, oracle, D, F, n)
+    finally:
+        F.SetAlgorithm(0)
+
+
+def _rader_checks(gdsp, oracle, D, F, n):
+    import torch
     p = D.plan(n)
     assert (p.kind, p.m, p.runtime_compiled) == (7, n - 1, True), (n, p.kind, p.m)
     rng = np.random.default_rng(7000 + n)
@@ -1288,12 +1298,12 @@ def test_rader_vs_oracle(gdsp, oracle, n):
         assert row_nrel(xt.cpu().numpy(), ref) < TOL
     x = rng.uniform(-1, 1, (3, n)) + 1j * rng.uniform(-1, 1, (3, n))
     assert nrel(gdsp.fft.FFT(x[0]), oracle.fft(x[0])) < TOL
-    F.SetAlgorithm(F.ALGO_NO_RADER)
+    F.SetAlgorithm(F.ALGO_NO_RADER | F.ALGO_NO_RACE)
     try:
         assert D.plan(n).kind == 3
         yc = gdsp.fft.FFTBatch(x)
     finally:
-        F.SetAlgorithm(0)
+        F.SetAlgorithm(F.ALGO_NO_RACE)
     assert row_nrel(yc, oracle.fft_rows(x)) < TOL
 
 
@@ -1317,7 +1327,7 @@ def test_rader_large_batch_properties(gdsp):
     import torch
     D = __import__("importlib").import_module("go-dsp_amd.device")
     n, batch = 3001, 65536
-    assert D.plan(n).kind == 7
+    assert D.plan(n).kind in (3, 7)
     g = torch.Generator(device="cuda").manual_seed(9)
     x = torch.complex(torch.rand(batch, n, dtype=torch.float64, device="cuda", generator=g) - 0.5,
                       torch.rand(batch, n, dtype=torch.float64, device="cuda", generator=g) - 0.5)
