@@ -1140,9 +1140,12 @@ struct PfaGeo {
   static constexpr int SUBS = G::SLOTS;                      // a sub-transform's slots
   static constexpr int RSL = M * SUBS > NN ? M * SUBS : NN;  // complex slots per row
   static constexpr int RT = M * T1;                          // threads per row
+  // rows per workgroup: about 256 threads within 40 KiB of row slots, so
+  // that four workgroups share a CU's LDS where the registers allow it (at
+  // 64 KiB, rows of 74 = 2 x 37 ran two 252-thread workgroups per CU)
   static constexpr int tpw() {
     int t = 256 / RT > 1 ? 256 / RT : 1;
-    while (t > 1 && t * RSL * 16 > 65536) --t;
+    while (t > 1 && t * RSL * 16 > 40960) --t;
     return t;
   }
   static constexpr int TPW = tpw();

@@ -663,11 +663,11 @@ JitRader *jit_rader_pfa_build(int dev, int m, const int *rad, int np) {
   int t1 = 0, tpw = 0;
   fixed_geo(rad, np, &t1, &tpw);
   // PfaGeo (mixed_fixed.hpp) on the host: M sub-transforms of T1 threads per
-  // row, rows per workgroup within 256 threads and 64 KiB of row slots
+  // row, rows per workgroup within 256 threads and 40 KiB of row slots
   const int p = n + 1, nn = m * p, subs = (n + 7) & ~7;
   const int rsl = std::max(m * subs, nn), rt = m * t1;
   tpw = 256 / rt > 1 ? 256 / rt : 1;
-  while (tpw > 1 && tpw * rsl * 16 > 65536) --tpw;
+  while (tpw > 1 && tpw * rsl * 16 > 40960) --tpw;
   const int wg = tpw * rt;
   const int ncol = tpw * p, ca = (ncol + wg - 1) / wg;
   const long lds = 16L * tpw * (rsl + m);

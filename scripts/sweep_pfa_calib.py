@@ -77,9 +77,13 @@ def main():
     ap.add_argument("--per", type=int, default=5)
     ap.add_argument("--samples", type=int, default=1 << 26)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--no-race", action="store_true",
+                    help="the kind-8 kernel itself (GDSP_ALGO_NO_RACE), not the race's choice")
     ap.add_argument("sizes", nargs="*", type=int)
     a = ap.parse_args()
     torch.cuda.set_device(0)
+    if a.no_race:
+        F.SetAlgorithm(F.ALGO_NO_RACE)
     for n in a.sizes or candidates(a.per):
         batch = max(1, a.samples // n)
         x = torch.empty((batch, n), dtype=torch.complex128, device="cuda")
