@@ -1145,7 +1145,7 @@ struct PfaGeo {
   // 64 KiB, rows of 74 = 2 x 37 ran two 252-thread workgroups per CU)
   static constexpr int tpw() {
     int t = 256 / RT > 1 ? 256 / RT : 1;
-    while (t > 1 && t * RSL * 16 > 40960) --t;
+    while (t > 1 && t * (RSL + M) * 16 > 40960) --t;
     return t;
   }
   static constexpr int TPW = tpw();
@@ -1180,6 +1180,18 @@ __global__ __launch_bounds__((PfaGeo<M, R0, RS...>::WG)) void rader_pfa_kernel(
     const int s = e / NN;
     return xs + s * RSL + (e - s * NN);
   };
+  // the stage-A columns' i2 = gpow[q] (q = P - 1: 0), read before the rows
+  // so that the table's latency hides behind the row loads
+  int i2a[PG::CA];
+#pragma unroll
+  for (int a = 0; a < PG::CA; ++a) {
+    const int c = tid + a * WG;
+    i2a[a] = 0;
+    if ((a + 1) * WG <= PG::NCOL || c < PG::NCOL) {
+      const int q = c - (c / P) * P;
+      if (q < N) i2a[a] = gpow[q];
+    }
+  }
   // 1. the rows, natural order
   {
     cd xc[NC];
@@ -1212,10 +1224,9 @@ __global__ __launch_bounds__((PfaGeo<M, R0, RS...>::WG)) void rader_pfa_kernel(
       const int c = tid + a * WG;
       qa[a] = -1;
       if ((a + 1) * WG <= PG::NCOL || c < PG::NCOL) {
-        const int s = c / P, q = c - s * P;
-        const int i2 = q < N ? gpow[q] : 0;
+        const int s = c / P;
         const cd *row = xs + s * RSL;
-        int idx = M * i2;  // (i1 P + i2 M) mod n for i1 = 0, 1, ...
+        int idx = M * i2a[a];  // (i1 P + i2 M) mod n for i1 = 0, 1, ...
 #pragma unroll
         for (int i1 = 0; i1 < M; ++i1) {
           ya[a][i1] = row[idx];

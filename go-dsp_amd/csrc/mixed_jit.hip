@@ -667,7 +667,7 @@ JitRader *jit_rader_pfa_build(int dev, int m, const int *rad, int np) {
   const int p = n + 1, nn = m * p, subs = (n + 7) & ~7;
   const int rsl = std::max(m * subs, nn), rt = m * t1;
   tpw = 256 / rt > 1 ? 256 / rt : 1;
-  while (tpw > 1 && tpw * rsl * 16 > 40960) --tpw;
+  while (tpw > 1 && tpw * (rsl + m) * 16 > 40960) --tpw;
   const int wg = tpw * rt;
   const int ncol = tpw * p, ca = (ncol + wg - 1) / wg;
   const long lds = 16L * tpw * (rsl + m);
