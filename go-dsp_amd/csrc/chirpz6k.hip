@@ -1,14 +1,17 @@
 // chirpz6k.hip — fused chirp-z (Bluestein, fft/bluestein.go:68-94) on the
-// convolution length M = 16 * RB * 16 = 3 * 2^k: M = 6144 (RB = 24) for
-// 2049 <= n <= 3072 and M = 3072 (RB = 12) for 1025 <= n <= 1536.
+// convolution length M = 16 * RB * 16: for 1025 <= n <= 4096 the smallest
+// such M >= 2n - 1 over the compiled pass-B radices RB (kC6RB below). Round
+// 3 built RB = 24 (M = 6144, 2049 <= n <= 3072) and RB = 12 (3072); round 6
+// every RB 9 ... 32 with an in-register DFT (pass B: dft3x for 24 and 12 as
+// measured, dft_m — native or coprime split — for the others).
 //
 // bluestein.go:70 pads the circular convolution to NextPowerOf2(2n - 1)
-// (8192, 4096) for these n because its FFT is radix 2. Any M >= 2n - 1 gives
-// the same linear convolution, hence the same DFT; 3 * 2^k is a quarter fewer
-// points. At M = 6144 the exchange buffer (48 KiB) and a 16-point-per-thread
-// register set let two 384-thread workgroups share a CU at 128 VGPRs, where
-// the M = 8192 kernel (bluestein_kernel<13>, 32 points per thread, 256 VGPRs)
-// runs two 256-thread ones.
+// because its FFT is radix 2. Any M >= 2n - 1 gives the same linear
+// convolution, hence the same DFT; 256 RB is at most 1/8 above 2n - 1 where
+// the power of 2 is up to twice it. At M = 6144 the exchange buffer (48 KiB)
+// and a 16-point-per-thread register set let two 384-thread workgroups share
+// a CU at 128 VGPRs, where the M = 8192 kernel (bluestein_kernel<13>, 32
+// points per thread, 256 VGPRs) runs two 256-thread ones.
 //
 // One workgroup per transform, T = max(M / 16, 256) threads (thread t):
 //   premultiply  a[t + NA r] = x * conj(w), r < KN (n <= NA KN; rest zero),
@@ -26,324 +29,39 @@
 // parts. Slots: after pass A (stride-16 writes) XOR-swizzled, i ^ ((i >> 4)
 // & 15) — every 16-lane write group and 32-lane read group hits distinct
 // banks; after pass B plain (16 contiguous writes, 32 contiguous reads).
-#include "fft_device.hpp"
-#include "launch.hpp"
-#include "mixed_core.hpp"
+#include "chirpz6k.hpp"
 
 namespace gdsp {
 
-// (kernel and helpers outside an anonymous namespace, so profiler kernel
-// names read gdsp::chirpz6k_kernel<...>)
-constexpr int kC6B = 256;  // pass-B butterflies (both sizes)
-template <int RB>
-struct C6Geo {
-  static constexpr int M = 256 * RB;               // points
-  static constexpr int NA = M / 16;                // pass A / C butterflies
-  static constexpr int T = NA > kC6B ? NA : kC6B;  // threads
-};
+GDSP_C6_LAUNCH(, 12)
+GDSP_C6_LAUNCH(, 24)
+GDSP_C6_LAUNCH(extern, 9)
+GDSP_C6_LAUNCH(extern, 10)
+GDSP_C6_LAUNCH(extern, 13)
+GDSP_C6_LAUNCH(extern, 14)
+GDSP_C6_LAUNCH(extern, 15)
+GDSP_C6_LAUNCH(extern, 16)
+GDSP_C6_LAUNCH(extern, 18)
+GDSP_C6_LAUNCH(extern, 20)
+GDSP_C6_LAUNCH(extern, 21)
+GDSP_C6_LAUNCH(extern, 25)
 
-// x * W_24^q (q a compile-time constant after unrolling)
-#define GDSP_C24 0.96592582628906828675  // cos(pi/12)
-#define GDSP_S24 0.25881904510252076235  // sin(pi/12)
-#define GDSP_C12 0.86602540378443864676  // cos(pi/6)
-__device__ __forceinline__ cd rot24(cd x, int q) {
-  q %= 24;
-  if (q % 3 == 0) return rot16(x, 2 * (q / 3));  // W_24^(3k) = W_16^(2k)
-  double c, s;                                   // W_24^q = c - i s
-  switch (q) {
-    case 1: c = GDSP_C24; s = GDSP_S24; break;
-    case 2: c = GDSP_C12; s = 0.5; break;
-    case 4: c = 0.5; s = GDSP_C12; break;
-    case 5: c = GDSP_S24; s = GDSP_C24; break;
-    case 7: c = -GDSP_S24; s = GDSP_C24; break;
-    case 8: c = -0.5; s = GDSP_C12; break;
-    case 10: c = -GDSP_C12; s = 0.5; break;
-    case 11: c = -GDSP_C24; s = GDSP_S24; break;
-    case 13: c = -GDSP_C24; s = -GDSP_S24; break;
-    case 14: c = -GDSP_C12; s = -0.5; break;
-    case 16: c = -0.5; s = -GDSP_C12; break;
-    case 17: c = -GDSP_S24; s = -GDSP_C24; break;
-    case 19: c = GDSP_S24; s = -GDSP_C24; break;
-    case 20: c = 0.5; s = -GDSP_C12; break;
-    case 22: c = GDSP_C12; s = -0.5; break;
-    default: c = GDSP_C24; s = -GDSP_S24; break;  // 23
-  }
-  return {fma(x.x, c, x.y * s), fma(x.y, c, -(x.x * s))};
-}
+// The pass-B radices, ascending: a length takes the first M = 256 RB >=
+// 2n - 1 (n >= 1025; 0 = none: the power-of-2 chirp-z). Measured against
+// the round-5 choice (M = 3072 / 6144 / the power of 2) on the first and last
+// prime of each RB's range, forced chirp-z plans, 2^27 samples
+// (profiles/r06/chirpz_rb_sweep.jsonl): RB 9, 10, 13-16, 18, 20, 21, 25 are
+// 1.04-1.19x faster; not kept: 11 (0.99x), 22 (0.77x; 0.97x at 128 VGPRs),
+// 26-32 (0.78-0.82x: 144-168 VGPRs hold them to one 7-8-wave workgroup per
+// CU; 26 at 128 VGPRs spills 40 and runs 0.90x), where the M = 8192 kernel
+// stays.
+static const int kC6RB[] = {9, 10, 12, 13, 14, 15, 16, 18, 20, 21, 24, 25};
 
-// DFT_R, R = 3 Q (Q = 8: 24, Q = 4: 12): DFT_Q over n1 (n = 3 n1 + n2),
-// twiddles W_R^(n2 k1) (= W_24^((24 / R) n2 k1)), DFT_3 over n2 (k = k1 + Q k2)
-template <int R>
-__device__ __forceinline__ void dft3x(cd (&a)[R]) {
-  constexpr int Q = R / 3, S = 24 / R;
-  cd y[3][Q];
-#pragma unroll
-  for (int n2 = 0; n2 < 3; ++n2) {
-    cd tmp[Q];
-#pragma unroll
-    for (int n1 = 0; n1 < Q; ++n1) tmp[n1] = a[3 * n1 + n2];
-    Dft<Q>::run(tmp);
-#pragma unroll
-    for (int k1 = 0; k1 < Q; ++k1) y[n2][k1] = tmp[k1];
-  }
-#pragma unroll
-  for (int k1 = 0; k1 < Q; ++k1) {
-    const cd a0 = y[0][k1], a1 = rot24(y[1][k1], S * k1), a2 = rot24(y[2][k1], 2 * S * k1);
-    // DFT_3: X1 = a0 - (a1 + a2)/2 - i sin(2 pi/3) (a1 - a2), X2 its mirror
-    const cd s = a1 + a2, d = a1 - a2;
-    const cd m = {fma(-0.5, s.x, a0.x), fma(-0.5, s.y, a0.y)};
-    a[k1] = a0 + s;
-    a[k1 + Q] = {fma(GDSP_C12, d.y, m.x), fma(-GDSP_C12, d.x, m.y)};
-    a[k1 + 2 * Q] = {fma(-GDSP_C12, d.y, m.x), fma(GDSP_C12, d.x, m.y)};
-  }
-}
-
-// v[r] *= w^r, r = 1..R-1, the powers by the three-term recurrence
-// w^(r+2) = 2 cos(2 theta) w^r - w^(r-2) (two FMAs each, as pass_compute's
-// CHEB) instead of twiddle_chain's products: 1.5 % faster, parity 3.7e-15
-// against 1.6e-15 vs the oracle (profiles/r03/chirpz6k_ab.txt)
-template <int R>
-__device__ __forceinline__ void c6_twiddle(cd (&v)[R], cd w) {
-  {
-    const cd w2 = cmul(w, w);
-    v[1] = cmul(v[1], w);
-    v[2] = cmul(v[2], w2);
-    const double c2 = w2.x + w2.x;
-    cd om = conjg(w), o = w;     // odd powers w^(r-2), w^r
-    cd em = {1.0, 0.0}, e = w2;  // even powers
-#pragma unroll
-    for (int r = 3; r < R; ++r) {
-      if (r & 1) {
-        const cd q = {fma(c2, o.x, -om.x), fma(c2, o.y, -om.y)};
-        om = o;
-        o = q;
-        v[r] = cmul(v[r], o);
-      } else {
-        const cd q = {fma(c2, e.x, -em.x), fma(c2, e.y, -em.y)};
-        em = e;
-        e = q;
-        v[r] = cmul(v[r], e);
-      }
-    }
-  }
-}
-
-// The steps after each FFT's last DFT: FFT 1's bhat step, FFT 2's
-// postmultiply and store (issue: the loads, apply: the arithmetic). Issued
-// before the pass-C twiddles or the last exchange's reads instead, the loads
-// push the kernel past 128 VGPRs into spills: 2.43 against 2.37 ms.
-template <int RB>
-struct C6Bhat {
-  using G = C6Geo<RB>;
-  rsrc_t rb;
-  uint32_t off;
-  cd f[16];
-  __device__ __forceinline__ void issue() {
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-      f[r] = buf_ld(rb, off + (uint32_t)(r * G::NA * 16));
-  }
-  __device__ __forceinline__ void apply(cd (&v)[16]) const {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = conjg(cmul(v[r], f[r]));
-  }
-};
-template <int RB, int KN, bool INV>
-struct C6Out {
-  using G = C6Geo<RB>;
-  rsrc_t rch, rout;
-  uint32_t off;
-  double scale;
-  cd f[KN];
-  __device__ __forceinline__ void issue() {
-#pragma unroll
-    for (int r = 0; r < KN; ++r)
-      f[r] = buf_ld(rch, off + (uint32_t)(r * G::NA * 16));
-  }
-  __device__ __forceinline__ void apply(cd (&v)[16]) const {
-#pragma unroll
-    for (int r = 0; r < KN; ++r) {
-      cd y = cmul(conjg(v[r]), f[r]);
-      if constexpr (INV) y = {y.x * scale, -y.y * scale};
-      buf_st_nt(rout, off + (uint32_t)(r * G::NA * 16), y);
-    }
-  }
-};
-
-// One FFT_M of the thread's registers v[r] = element t + NA r, in place
-// (natural order in and out), then epi. ZIN: inputs r >= ZIN are zero (pass
-// A pruned); first: no exchange precedes this one in the kernel. tw: the pass
-// twiddle bases, W_{16 RB}^k (k < 16, pass B) then W_M^k (k < NA, pass C).
-// Threads t >= NA (M = 6144: none) sit out passes A and C, threads t >= 256
-// (M = 3072: none) pass B; all take part in the barriers.
-template <int RB, int ZIN, class EPI>
-__device__ __forceinline__ void c6_fft(cd (&v)[16], int t, const cd *__restrict__ tw, double *lds,
-                                       bool first, EPI &epi) {
-  using G = C6Geo<RB>;
-  const bool pa = G::NA == G::T || t < G::NA;
-  const bool pb = kC6B == G::T || t < kC6B;
-  // pass A
-  if (pa) {
-    if constexpr (ZIN > 0 && ZIN <= 8) dft_half_in<16, ZIN>(v);
-    else Dft<16>::run(v);
-  }
-  // exchange 1: write 16 t + r, read t + 256 r (t < 256)
-  // (the twiddle bases are read where they are used: read a pass ahead,
-  // 3.2-3.3 against 2.37 ms)
-  const int wa = 16 * t, ma = t & 15;
-  const int ra = t ^ ((t >> 4) & 15);
-  cd u[RB];
-  if (!first) __syncthreads();
-  if (pa) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) lds[wa + (r ^ ma)] = v[r].x;
-  }
-  __syncthreads();
-  if (pb) {
-#pragma unroll
-    for (int r = 0; r < RB; ++r) u[r].x = lds[ra + kC6B * r];
-  }
-  __syncthreads();
-  if (pa) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) lds[wa + (r ^ ma)] = v[r].y;
-  }
-  __syncthreads();
-  // pass B
-  const int wbo = (t >> 4) * (16 * RB) + (t & 15);
-  if (pb) {
-#pragma unroll
-    for (int r = 0; r < RB; ++r) u[r].y = lds[ra + kC6B * r];
-    c6_twiddle<RB>(u, tw[t & 15]);
-    dft3x<RB>(u);
-  }
-  __syncthreads();
-  // exchange 2: write (t / 16) 16 RB + t % 16 + 16 r, read t + NA r
-  if (pb) {
-#pragma unroll
-    for (int r = 0; r < RB; ++r) lds[wbo + 16 * r] = u[r].x;
-  }
-  __syncthreads();
-  if (pa) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[r].x = lds[t + G::NA * r];
-  }
-  __syncthreads();
-  if (pb) {
-#pragma unroll
-    for (int r = 0; r < RB; ++r) lds[wbo + 16 * r] = u[r].y;
-  }
-  __syncthreads();
-  if (pa) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[r].y = lds[t + G::NA * r];
-  }
-  if (pa) {
-    // pass C: twiddle W_M^(t r), DFT_16, the epilogue
-    c6_twiddle<16>(v, tw[16 + t]);
-    Dft<16>::run(v);
-    epi.issue();
-    epi.apply(v);
-  }
-}
-
-// M = 6144: two workgroups of 6 waves share a CU. Held to 128 VGPRs (4 waves
-// per SIMD of room): at 144 (3 per SIMD) the second workgroup's waves did not
-// fit beside the first's 2-2-1-1 placement and the kernel ran 3.13 against
-// 2.43 ms (profiles/r03/chirpz6k_ab.txt). M = 3072 (4-wave workgroups, one
-// wave per SIMD each) takes its natural 144-146 VGPRs, three per SIMD: at 128
-// it spills 54-78.
-// KN: n <= NA KN (inputs and wanted outputs at r < KN)
-// REAL: float64 input rows (fft.FFTReal, fft/fft.go:25-27), read directly
-// (no complex copy of the input first)
-//
-// One transform (row g) of the workgroup: premultiply, FFT 1, bhat, FFT 2,
-// postmultiply and store.
-// Measured and not kept (round 4, profiles/r04/chirpz6k_ablation.txt): with the
-// row's loads replaced by constants the launch takes 16 % less, but hiding
-// them did not pay at the 128 VGPRs two workgroups per CU allow — an L2
-// touch-ahead of a later block's row (1-6 % slower at every distance), a
-// persistent form touching its next row (29 spilled VGPRs, 2.97 ms), the row
-// by LDS-DMA into the idle exchange buffer (equal), two rows per workgroup
-// with the second one's DMA in flight (26 spilled VGPRs, 5 % slower).
-template <int RB, bool INV, int KN, bool REAL>
-__device__ __forceinline__ void c6_transform(const void *__restrict__ in, cd *__restrict__ out,
-                                             int64_t n, int64_t g, int t, const cd *tw,
-                                             const cd *chirp, const cd *bhat, double scale,
-                                             double *lds) {
-  using G = C6Geo<RB>;
-  const uint32_t off = (uint32_t)t * 16u;
-  const int64_t rowb = n * 16;
-  const int64_t inb = REAL ? n * 8 : rowb;
-  cd v[16];
-  if (G::NA == G::T || t < G::NA) {
-    const rsrc_t rin = make_rsrc(static_cast<const char *>(in) + g * inb, inb);
-    const rsrc_t rch = make_rsrc(chirp, rowb);
-    cd xv[KN], cv[KN];
-#pragma unroll
-    for (int r = 0; r < KN; ++r) {
-      if constexpr (REAL)
-        xv[r] = {buf_ld1(rin, (uint32_t)t * 8u + (uint32_t)(r * G::NA * 8)), 0.0};
-      else
-        xv[r] = buf_ld(rin, off + (uint32_t)(r * G::NA * 16));
-      cv[r] = buf_ld(rch, off + (uint32_t)(r * G::NA * 16));
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      if (r < KN) {
-        cd x = xv[r];
-        if constexpr (INV) x.y = -x.y;
-        v[r] = cmul(x, cv[r]);
-      } else {
-        v[r] = {0.0, 0.0};
-      }
-    }
-  }
-  C6Bhat<RB> be{make_rsrc(bhat, (int64_t)G::M * 16), off, {}};
-  c6_fft<RB, KN, C6Bhat<RB>>(v, t, tw, lds, true, be);
-  // the second FFT must not share the first one's addresses (opaque copies:
-  // otherwise the compiler keeps them live across both)
-  const int t2 = opaque_int(t);
-  C6Out<RB, KN, INV> oe{make_rsrc(opaque_ptr(chirp), rowb), make_rsrc(out + g * n, rowb),
-                        (uint32_t)t2 * 16u, scale, {}};
-  c6_fft<RB, 0, C6Out<RB, KN, INV>>(v, t2, opaque_ptr(tw), lds, false, oe);
-}
-
-template <int RB, bool INV, int KN, bool REAL = false>
-__global__ __launch_bounds__(C6Geo<RB>::T) __attribute__((amdgpu_waves_per_eu(RB == 24 ? 4 : 3))) void chirpz6k_kernel(
-    const void *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
-    const cd *__restrict__ tw, const cd *__restrict__ chirp, const cd *__restrict__ bhat,
-    double scale) {
-  using G = C6Geo<RB>;
-  static_assert(KN >= 1 && KN <= 8, "n <= M/2");
-  __shared__ double lds[G::M];
-  const int64_t g = xcd_remap(blockIdx.x, gridDim.x);
-  if (g >= batch) return;  // (grid = batch: never taken)
-  c6_transform<RB, INV, KN, REAL>(in, out, n, g, (int)threadIdx.x, tw, chirp, bhat, scale, lds);
-}
-
-// The convolution length for n (0: neither size applies)
 int chirpz6k_m(int64_t n) {
-  if (n >= 2049 && 2 * n - 1 <= 6144) return 6144;
-  if (n >= 1025 && 2 * n - 1 <= 3072) return 3072;
+  if (n < 1025) return 0;
+  for (int rb : kC6RB)
+    if (256 * (int64_t)rb >= 2 * n - 1) return 256 * rb;
   return 0;
-}
-
-template <int RB>
-static hipError_t launch_c6(bool inv, int load, const void *in, cd *out, int64_t n, int64_t batch,
-                            const cd *tw, const cd *chirp, const cd *bhat, double scale,
-                            hipStream_t s) {
-  const dim3 grid((unsigned)batch), block(C6Geo<RB>::T);
-  if (load == LOAD_REAL)
-    hipLaunchKernelGGL((chirpz6k_kernel<RB, false, 8, true>), grid, block, 0, s, in, out, n, batch,
-                       tw, chirp, bhat, scale);
-  else if (inv)
-    hipLaunchKernelGGL((chirpz6k_kernel<RB, true, 8>), grid, block, 0, s, in, out, n, batch, tw,
-                       chirp, bhat, scale);
-  else
-    hipLaunchKernelGGL((chirpz6k_kernel<RB, false, 8>), grid, block, 0, s, in, out, n, batch, tw,
-                       chirp, bhat, scale);
-  return hipGetLastError();
 }
 
 hipError_t launch_chirpz6k(int64_t m, bool inv, int load, const void *in, cd *out, int64_t n,
@@ -352,8 +70,14 @@ hipError_t launch_chirpz6k(int64_t m, bool inv, int load, const void *in, cd *ou
   if (chirpz6k_m(n) != m || batch < 0 || batch > 0x7fffffff || (inv && load == LOAD_REAL))
     return hipErrorInvalidValue;
   if (batch == 0) return hipSuccess;
-  if (m == 6144) return launch_c6<24>(inv, load, in, out, n, batch, tw, chirp, bhat, scale, s);
-  return launch_c6<12>(inv, load, in, out, n, batch, tw, chirp, bhat, scale, s);
+  switch (m / 256) {
+#define C6_CASE(RB) \
+  case RB: return launch_c6<RB>(inv, load, in, out, n, batch, tw, chirp, bhat, scale, s);
+    C6_CASE(9) C6_CASE(10) C6_CASE(12) C6_CASE(13) C6_CASE(14) C6_CASE(15) C6_CASE(16)
+    C6_CASE(18) C6_CASE(20) C6_CASE(21) C6_CASE(24) C6_CASE(25)
+#undef C6_CASE
+    default: return hipErrorInvalidValue;
+  }
 }
 
 }  // namespace gdsp

@@ -338,9 +338,9 @@ struct gdsp_plan {
   // NextPowerOf2(2n-1) = 32768 exceeds one kernel runs as `parts` fused
   // convolutions of M = 16384, each giving kpart outputs; bhat holds parts * M
   int parts = 1;
-  // fused chirp-z on M = 6144 / 3072 (chirpz6k.hip, 2049 <= n <= 3072 /
-  // 1025 <= n <= 1536, where bluestein.go:70 pads to 8192 / 4096); tw6k: its
-  // pass twiddle bases
+  // fused chirp-z on M = 16 RB 16 (chirpz6k.hip: the smallest such M >= 2n - 1,
+  // 1025 <= n <= 4096, where bluestein.go:70 pads to NextPowerOf2(2n - 1));
+  // tw6k: its pass twiddle bases
   bool c6k = false;
   cd *tw6k = nullptr;
   // composed chirp-z without its fused transposes (GDSP_ALGO_CHIRPZ_UNFUSED)
@@ -1242,10 +1242,10 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz, int skip) {
   }
   bool c6k_ok = !(plan_flags() & GDSP_ALGO_CHIRPZ_POW2);
   if (p->kind == KIND_BLUESTEIN && p->parts == 1 && gdsp::chirpz6k_m(n) && c6k_ok) {
-    // 2049 <= n <= 3072 (1025 <= n <= 1536): bluestein.go:70 pads the
-    // convolution to 8192 (4096); M = 6144 (3072) = 16 * RB * 16 gives the
-    // same linear convolution (and DFT) with a quarter fewer points
-    // (chirpz6k.hip). GDSP_ALGO_CHIRPZ_POW2 keeps the power of 2.
+    // 1025 <= n <= 4096: bluestein.go:70 pads the convolution to
+    // NextPowerOf2(2n - 1); the smallest M = 16 * RB * 16 >= 2n - 1 of the
+    // compiled RB gives the same linear convolution (and DFT) on up to 44 %
+    // fewer points (chirpz6k.hip). GDSP_ALGO_CHIRPZ_POW2 keeps the power of 2.
     p->m = gdsp::chirpz6k_m(n);
     p->log2m = 0;
     p->c6k = true;

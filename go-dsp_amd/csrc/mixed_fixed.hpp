@@ -1076,63 +1076,7 @@ __global__ __launch_bounds__((RaderGeo<R0, RS...>::WG)) void rader_fixed_kernel(
 //     (k1 E1 + k2 E2) mod n (k2 = 0: y0 + A[0]), then a coalesced store.
 // The LDS a row uses for its samples, its M sub-transforms' exchanges and
 // its output staging is one region, separated by barriers.
-constexpr int pfa_gcd(int a, int b) { return b ? pfa_gcd(b, a % b) : a; }
-constexpr int pfa_inv(int a, int m) {  // a^-1 mod m (gcd(a, m) = 1)
-  for (int x = 1; x < m; ++x)
-    if ((a % m) * x % m == 1) return x;
-  return 0;
-}
-// sizes dft_any has an in-register DFT for
-constexpr bool dft_native(int r) {
-  switch (r) {
-    case 2: case 3: case 4: case 5: case 6: case 7: case 8: case 9: case 10: case 11: case 12:
-    case 13: case 15: case 16: case 17: case 19: case 20: case 23: case 25: case 29: case 31:
-    case 32:
-      return true;
-    default:
-      return false;
-  }
-}
-// R1 of a coprime split M = R1 R2 with both native (0: none)
-constexpr int pfa_split(int m) {
-  for (int r1 = 2; r1 < m; ++r1)
-    if (m % r1 == 0 && pfa_gcd(r1, m / r1) == 1 && dft_native(r1) && dft_native(m / r1)) return r1;
-  return 0;
-}
-// Prime-factor DFT of R1 R2 points (coprime): input (R2 n1 + R1 n2) mod R,
-// output (k1 R2 (R2^-1 mod R1) + k2 R1 (R1^-1 mod R2)) mod R, no twiddles
-template <int R1, int R2>
-__device__ __forceinline__ void dft_pfa2(cd (&v)[R1 * R2]) {
-  constexpr int R = R1 * R2;
-  constexpr int F1 = R2 * pfa_inv(R2 % R1, R1) % R, F2 = R1 * pfa_inv(R1 % R2, R2) % R;
-  cd t[R2][R1];
-#pragma unroll
-  for (int n2 = 0; n2 < R2; ++n2) {
-#pragma unroll
-    for (int n1 = 0; n1 < R1; ++n1) t[n2][n1] = v[(R2 * n1 + R1 * n2) % R];
-    dft_any<R1>(t[n2]);
-  }
-#pragma unroll
-  for (int k1 = 0; k1 < R1; ++k1) {
-    cd u[R2];
-#pragma unroll
-    for (int n2 = 0; n2 < R2; ++n2) u[n2] = t[n2][k1];
-    dft_any<R2>(u);
-#pragma unroll
-    for (int k2 = 0; k2 < R2; ++k2) v[(k1 * F1 + k2 * F2) % R] = u[k2];
-  }
-}
-template <int M>
-__device__ __forceinline__ void dft_m(cd (&v)[M]) {
-  if constexpr (dft_native(M)) {
-    dft_any<M>(v);
-  } else {
-    constexpr int R1 = pfa_split(M);
-    static_assert(R1 > 0, "no in-register DFT for this cofactor");
-    dft_pfa2<R1, M / R1>(v);
-  }
-}
-
+// (pfa_gcd, pfa_inv, dft_m: mixed_core.hpp)
 template <int M, int R0, int... RS>
 struct PfaGeo {
   using G = FixedGeo<R0, RS...>;

@@ -622,12 +622,22 @@ def test_chirpz_plan_vs_oracle(gdsp, oracle, n):
     assert row_nrel(yci, oracle.ifft_rows(x)) < TOL
 
 
-# M = 6144 (16 * 24 * 16) where bluestein.go:70 pads to 8192, M = 3072
-# (16 * 12 * 16) where it pads to 4096: the ranges' ends, primes across them,
-# and lengths that are smooth (3072 = 2^10 * 3, 1500, 1536: the mixed-radix
-# kernel by default, chirp-z only when forced)
-C6K = [2049, 2053, 2307, 2729, 3000, 3001, 3067, 3071, 3072,
-       1025, 1031, 1201, 1500, 1531, 1536]
+# The fused chirp-z on M = 16 * RB * 16 (chirpz6k.hpp): the smallest such M
+# >= 2n - 1 over the compiled pass-B radices (chirpz6k.hip kC6RB), 1025 <= n
+# <= 3200, where bluestein.go:70 pads to NextPowerOf2(2n - 1) (and keeps it
+# above 3200). Per RB the first and last
+# prime of its range, the ranges' ends, and lengths that are smooth (3072 =
+# 2^10 * 3, 1500, 1536: the mixed-radix kernel by default, chirp-z only when
+# forced)
+C6_RB = [9, 10, 12, 13, 14, 15, 16, 18, 20, 21, 24, 25]
+C6K = [1025, 1031, 1151, 1153, 1279, 1283, 1399, 1409, 1531, 1543, 1663, 1667, 1789, 1801,
+       1913, 1931, 2039, 2049, 2053, 2297, 2307, 2309, 2557, 2579, 2687, 2689, 2729, 2803, 2819,
+       3000, 3001, 3067, 3071, 3072, 3073, 3079, 3191, 3203, 3323, 3329, 3583, 3593, 3833,
+       3847, 4093, 4096, 1500, 1536, 2062]
+
+
+def c6_m(n):  # (above 256 * 25 / 2: the power of 2)
+    return next((256 * rb for rb in C6_RB if 256 * rb >= 2 * n - 1), 1 << (2 * n - 2).bit_length())
 
 
 @pytest.mark.parametrize("n", C6K)
@@ -636,7 +646,7 @@ def test_chirpz6k_vs_oracle(gdsp, oracle, n):
     D = __import__("importlib").import_module("go-dsp_amd.device")
     F = __import__("importlib").import_module("go-dsp_amd.fft")
     pc = D.plan(n, chirpz=True)
-    m, m_ref = (6144, 8192) if n > 2048 else (3072, 4096)
+    m, m_ref = c6_m(n), 1 << (2 * n - 2).bit_length()
     assert (pc.kind, pc.m) == (3, m), (n, pc.kind, pc.m)
     rng = np.random.default_rng(6144 + n)
     for batch in (1, 5):
@@ -1487,7 +1497,7 @@ def _pfa_large_batch(D, n, batch):
 # the fused chirp-z (plan kind 3) with L >= 2n - 1 smooth instead of
 # bluestein.go:70's NextPowerOf2(2n - 1) where the lane-cost model expects it
 # cheaper: the same linear convolution, hence the same DFT
-BLUFIX_CASES = [1031, 2062, 4099, 4402, 4981, 5402, 6011, 6143]
+BLUFIX_CASES = [4099, 4402, 4981, 5402, 6011, 6143]
 
 
 @pytest.mark.parametrize("n", BLUFIX_CASES)
