@@ -4,7 +4,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/r06s
 export GDSP_JIT_CACHE=$GRAFT_REPO_ROOT/gpurun_out/jitcache
 python3 tools/source_stamp.py > gpurun_out/source_stamp.json
-timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > gpurun_out/r06s/pytest_gpu.log 2>&1; rc=$?
+timeout -k 10 800 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > gpurun_out/r06s/pytest_gpu.log 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -3 gpurun_out/r06s/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r06s/smoke.log 2>&1; rc=$?
 echo "smoke rc=$rc"; tail -2 gpurun_out/r06s/smoke.log; [ $rc -eq 0 ] || exit $rc
