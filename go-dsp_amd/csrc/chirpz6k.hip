@@ -1,9 +1,10 @@
 // chirpz6k.hip — fused chirp-z (Bluestein, fft/bluestein.go:68-94) on the
-// convolution length M = 16 * RB * 16: for 1025 <= n <= 4096 the smallest
-// such M >= 2n - 1 over the compiled pass-B radices RB (kC6RB below). Round
-// 3 built RB = 24 (M = 6144, 2049 <= n <= 3072) and RB = 12 (3072); round 6
-// every RB 9 ... 32 with an in-register DFT (pass B: dft3x for 24 and 12 as
-// measured, dft_m — native or coprime split — for the others).
+// convolution length M = 16 * RB * 16: for 129 <= n <= 3200 the smallest
+// such M >= 2n - 1 over the kept pass-B radices RB (kC6RB below). Round 3
+// built RB = 24 (M = 6144, 2049 <= n <= 3072) and RB = 12 (3072); round 6
+// measured every RB 2 ... 32 with an in-register DFT (pass B: dft3x for 24
+// and 12 as measured, dft_m — native or coprime split — for the others;
+// several transforms per workgroup below RB = 9, c6_fft_multi).
 //
 // bluestein.go:70 pads the circular convolution to NextPowerOf2(2n - 1)
 // because its FFT is radix 2. Any M >= 2n - 1 gives the same linear
@@ -35,6 +36,10 @@ namespace gdsp {
 
 GDSP_C6_LAUNCH(, 12)
 GDSP_C6_LAUNCH(, 24)
+GDSP_C6_LAUNCH(extern, 3)
+GDSP_C6_LAUNCH(extern, 4)
+GDSP_C6_LAUNCH(extern, 5)
+GDSP_C6_LAUNCH(extern, 6)
 GDSP_C6_LAUNCH(extern, 9)
 GDSP_C6_LAUNCH(extern, 10)
 GDSP_C6_LAUNCH(extern, 13)
@@ -47,20 +52,23 @@ GDSP_C6_LAUNCH(extern, 21)
 GDSP_C6_LAUNCH(extern, 25)
 
 // The pass-B radices, ascending: a length takes the first M = 256 RB >=
-// 2n - 1 (n >= 1025; 0 = none: the power-of-2 chirp-z). Measured against
-// the round-5 choice (M = 3072 / 6144 / the power of 2) on the first and last
-// prime of each RB's range, forced chirp-z plans, 2^27 samples
-// (profiles/r06/chirpz_rb_sweep.jsonl): RB 9, 10, 13-16, 18, 20, 21, 25 are
-// 1.04-1.19x faster; not kept: 11 (0.99x), 22 (0.77x; 0.97x at 128 VGPRs),
-// 26-32 (0.78-0.82x: 144-168 VGPRs hold them to one 7-8-wave workgroup per
-// CU; 26 at 128 VGPRs spills 40 and runs 0.90x), where the M = 8192 kernel
-// stays.
-static const int kC6RB[] = {9, 10, 12, 13, 14, 15, 16, 18, 20, 21, 24, 25};
+// 2n - 1 (n >= 129) unless the power of 2 is smaller (0 = none: the
+// power-of-2 chirp-z). Measured against the round-5 choice (M = 3072 / 6144 /
+// the power of 2) on the first and last prime of each RB's range, forced
+// chirp-z plans, 2^27 samples (profiles/r06/chirpz_rb_sweep.jsonl): RB 3-6,
+// 9, 10, 13-16, 18, 20, 21, 25 are 1.04-1.25x faster; not kept: 2 (0.96-0.98x),
+// 7 and 8 (0.94-0.96x; 0.89-0.98x at two waves per SIMD), 11 (0.99x), 22
+// (0.77x; 0.97x at 128 VGPRs), 26-32 (0.78-0.82x: 144-168 VGPRs hold their
+// 7-8-wave workgroups to one per CU; 26 at 128 VGPRs spills 40 and runs
+// 0.90x), where M = 6144 or the power of 2 stays.
+static const int kC6RB[] = {3, 4, 5, 6, 9, 10, 12, 13, 14, 15, 16, 18, 20, 21, 24, 25};
 
 int chirpz6k_m(int64_t n) {
-  if (n < 1025) return 0;
+  if (n < 129) return 0;
+  int64_t p2 = 1;
+  while (p2 < 2 * n - 1) p2 <<= 1;
   for (int rb : kC6RB)
-    if (256 * (int64_t)rb >= 2 * n - 1) return 256 * rb;
+    if (256 * (int64_t)rb >= 2 * n - 1) return 256 * rb <= p2 ? 256 * rb : 0;
   return 0;
 }
 
@@ -73,6 +81,7 @@ hipError_t launch_chirpz6k(int64_t m, bool inv, int load, const void *in, cd *ou
   switch (m / 256) {
 #define C6_CASE(RB) \
   case RB: return launch_c6<RB>(inv, load, in, out, n, batch, tw, chirp, bhat, scale, s);
+    C6_CASE(3) C6_CASE(4) C6_CASE(5) C6_CASE(6)
     C6_CASE(9) C6_CASE(10) C6_CASE(12) C6_CASE(13) C6_CASE(14) C6_CASE(15) C6_CASE(16)
     C6_CASE(18) C6_CASE(20) C6_CASE(21) C6_CASE(24) C6_CASE(25)
 #undef C6_CASE

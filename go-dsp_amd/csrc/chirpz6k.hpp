@@ -19,9 +19,12 @@ constexpr int kC6B = 256;  // pass-B butterflies (every RB)
 constexpr int c6_wpe(int rb) { return (rb >= 18 && rb <= 21) || rb == 24 || rb == 25 ? 4 : 3; }
 template <int RB>
 struct C6Geo {
-  static constexpr int M = 256 * RB;               // points
-  static constexpr int NA = M / 16;                // pass A / C butterflies
-  static constexpr int T = NA > kC6B ? NA : kC6B;  // threads
+  static constexpr int M = 256 * RB;  // points
+  static constexpr int NA = M / 16;   // pass A / C butterflies of one transform
+  // transforms per workgroup: one, or for RB <= 8 (NA <= 128) as many as keep
+  // the 256 threads busy in passes A and C (pass B: 256 butterflies each)
+  static constexpr int TPW = NA >= kC6B ? 1 : kC6B / NA;
+  static constexpr int T = TPW * NA > kC6B ? TPW * NA : kC6B;  // threads
   static constexpr int WPE = c6_wpe(RB);
 };
 
@@ -87,7 +90,9 @@ __device__ __forceinline__ void dft3x(cd (&a)[R]) {
 // against 1.6e-15 vs the oracle (profiles/r03/chirpz6k_ab.txt)
 template <int R>
 __device__ __forceinline__ void c6_twiddle(cd (&v)[R], cd w) {
-  {
+  if constexpr (R == 2) {
+    v[1] = cmul(v[1], w);
+  } else {
     const cd w2 = cmul(w, w);
     v[1] = cmul(v[1], w);
     v[2] = cmul(v[2], w2);
@@ -137,6 +142,7 @@ struct C6Out {
   rsrc_t rch, rout;
   uint32_t off;
   double scale;
+  bool ok;  // the row exists (TPW > 1: the last workgroup's extra slots)
   cd f[KN];
   __device__ __forceinline__ void issue() {
 #pragma unroll
@@ -148,7 +154,7 @@ struct C6Out {
     for (int r = 0; r < KN; ++r) {
       cd y = cmul(conjg(v[r]), f[r]);
       if constexpr (INV) y = {y.x * scale, -y.y * scale};
-      buf_st_nt(rout, off + (uint32_t)(r * G::NA * 16), y);
+      if (G::TPW == 1 || ok) buf_st_nt(rout, off + (uint32_t)(r * G::NA * 16), y);
     }
   }
 };
@@ -231,6 +237,95 @@ __device__ __forceinline__ void c6_fft(cd (&v)[16], int t, const cd *__restrict_
   }
 }
 
+// c6_fft for TPW > 1 transforms per workgroup (RB <= 8): thread t holds
+// element tt + NA r of transform s (t = s NA + tt) in passes A and C, and
+// takes pass-B butterfly t of every transform; transform s exchanges through
+// lds + s M. (A separate function: folding TPW = 1 into it, the same
+// arithmetic, cost the RB = 24 / 25 kernels 14-36 spilled VGPRs.)
+template <int RB, int ZIN, class EPI>
+__device__ __forceinline__ void c6_fft_multi(cd (&v)[16], int t, int s, int tt,
+                                       const cd *__restrict__ tw, double *lds, bool first,
+                                       EPI &epi) {
+  using G = C6Geo<RB>;
+  constexpr int TPW = G::TPW, M = G::M;
+  static_assert(TPW > 1 && G::T == kC6B, "several transforms per 256-thread workgroup");
+  const bool pa = t < TPW * G::NA;
+  double *const la = lds + s * M;
+  // pass A
+  if (pa) {
+    if constexpr (ZIN > 0 && ZIN <= 8) dft_half_in<16, ZIN>(v);
+    else Dft<16>::run(v);
+  }
+  // exchange 1: write 16 tt + r, read t + 256 r (t < 256)
+  // (the twiddle bases are read where they are used: read a pass ahead,
+  // 3.2-3.3 against 2.37 ms)
+  const int wa = 16 * tt, ma = tt & 15;
+  const int ra = t ^ ((t >> 4) & 15);
+  cd u[TPW][RB];
+  if (!first) __syncthreads();
+  if (pa) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) la[wa + (r ^ ma)] = v[r].x;
+  }
+  __syncthreads();
+  {
+#pragma unroll
+    for (int q = 0; q < TPW; ++q)
+#pragma unroll
+      for (int r = 0; r < RB; ++r) u[q][r].x = lds[q * M + ra + kC6B * r];
+  }
+  __syncthreads();
+  if (pa) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) la[wa + (r ^ ma)] = v[r].y;
+  }
+  __syncthreads();
+  // pass B
+  const int wbo = (t >> 4) * (16 * RB) + (t & 15);
+  {
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+#pragma unroll
+      for (int r = 0; r < RB; ++r) u[q][r].y = lds[q * M + ra + kC6B * r];
+      c6_twiddle<RB>(u[q], tw[t & 15]);
+      if constexpr (RB == 24 || RB == 12) dft3x<RB>(u[q]);  // (measured, round 3)
+      else dft_m<RB>(u[q]);
+    }
+  }
+  __syncthreads();
+  // exchange 2: write (t / 16) 16 RB + t % 16 + 16 r, read tt + NA r
+  {
+#pragma unroll
+    for (int q = 0; q < TPW; ++q)
+#pragma unroll
+      for (int r = 0; r < RB; ++r) lds[q * M + wbo + 16 * r] = u[q][r].x;
+  }
+  __syncthreads();
+  if (pa) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r].x = la[tt + G::NA * r];
+  }
+  __syncthreads();
+  {
+#pragma unroll
+    for (int q = 0; q < TPW; ++q)
+#pragma unroll
+      for (int r = 0; r < RB; ++r) lds[q * M + wbo + 16 * r] = u[q][r].y;
+  }
+  __syncthreads();
+  if (pa) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r].y = la[tt + G::NA * r];
+  }
+  if (pa) {
+    // pass C: twiddle W_M^(tt r), DFT_16, the epilogue
+    c6_twiddle<16>(v, tw[16 + tt]);
+    Dft<16>::run(v);
+    epi.issue();
+    epi.apply(v);
+  }
+}
+
 // M = 6144: two workgroups of 6 waves share a CU. Held to 128 VGPRs (4 waves
 // per SIMD of room): at 144 (3 per SIMD) the second workgroup's waves did not
 // fit beside the first's 2-2-1-1 placement and the kernel ran 3.13 against
@@ -252,25 +347,30 @@ __device__ __forceinline__ void c6_fft(cd (&v)[16], int t, const cd *__restrict_
 // with the second one's DMA in flight (26 spilled VGPRs, 5 % slower).
 template <int RB, bool INV, int KN, bool REAL>
 __device__ __forceinline__ void c6_transform(const void *__restrict__ in, cd *__restrict__ out,
-                                             int64_t n, int64_t g, int t, const cd *tw,
-                                             const cd *chirp, const cd *bhat, double scale,
-                                             double *lds) {
+                                             int64_t n, int64_t g, bool ok, int t, int s, int tt,
+                                             const cd *tw, const cd *chirp, const cd *bhat,
+                                             double scale, double *lds) {
   using G = C6Geo<RB>;
-  const uint32_t off = (uint32_t)t * 16u;
+  const uint32_t off = (uint32_t)tt * 16u;
   const int64_t rowb = n * 16;
   const int64_t inb = REAL ? n * 8 : rowb;
   cd v[16];
-  if (G::NA == G::T || t < G::NA) {
-    const rsrc_t rin = make_rsrc(static_cast<const char *>(in) + g * inb, inb);
-    const rsrc_t rch = make_rsrc(chirp, rowb);
+  if (G::TPW * G::NA == G::T || t < G::TPW * G::NA) {
     cd xv[KN], cv[KN];
+    if (G::TPW == 1 || ok) {
+      const rsrc_t rin = make_rsrc(static_cast<const char *>(in) + g * inb, inb);
+      const rsrc_t rch = make_rsrc(chirp, rowb);
 #pragma unroll
-    for (int r = 0; r < KN; ++r) {
-      if constexpr (REAL)
-        xv[r] = {buf_ld1(rin, (uint32_t)t * 8u + (uint32_t)(r * G::NA * 8)), 0.0};
-      else
-        xv[r] = buf_ld(rin, off + (uint32_t)(r * G::NA * 16));
-      cv[r] = buf_ld(rch, off + (uint32_t)(r * G::NA * 16));
+      for (int r = 0; r < KN; ++r) {
+        if constexpr (REAL)
+          xv[r] = {buf_ld1(rin, (uint32_t)tt * 8u + (uint32_t)(r * G::NA * 8)), 0.0};
+        else
+          xv[r] = buf_ld(rin, off + (uint32_t)(r * G::NA * 16));
+        cv[r] = buf_ld(rch, off + (uint32_t)(r * G::NA * 16));
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < KN; ++r) xv[r] = cv[r] = {0.0, 0.0};
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -284,13 +384,17 @@ __device__ __forceinline__ void c6_transform(const void *__restrict__ in, cd *__
     }
   }
   C6Bhat<RB> be{make_rsrc(bhat, (int64_t)G::M * 16), off, {}};
-  c6_fft<RB, KN, C6Bhat<RB>>(v, t, tw, lds, true, be);
+  if constexpr (G::TPW == 1) c6_fft<RB, KN, C6Bhat<RB>>(v, t, tw, lds, true, be);
+  else c6_fft_multi<RB, KN, C6Bhat<RB>>(v, t, s, tt, tw, lds, true, be);
   // the second FFT must not share the first one's addresses (opaque copies:
   // otherwise the compiler keeps them live across both)
-  const int t2 = opaque_int(t);
+  const int t2 = opaque_int(t), tt2 = G::TPW == 1 ? t2 : opaque_int(tt);
   C6Out<RB, KN, INV> oe{make_rsrc(opaque_ptr(chirp), rowb), make_rsrc(out + g * n, rowb),
-                        (uint32_t)t2 * 16u, scale, {}};
-  c6_fft<RB, 0, C6Out<RB, KN, INV>>(v, t2, opaque_ptr(tw), lds, false, oe);
+                        (uint32_t)tt2 * 16u, scale, G::TPW == 1 || ok, {}};
+  if constexpr (G::TPW == 1)
+    c6_fft<RB, 0, C6Out<RB, KN, INV>>(v, t2, opaque_ptr(tw), lds, false, oe);
+  else
+    c6_fft_multi<RB, 0, C6Out<RB, KN, INV>>(v, t2, s, tt2, opaque_ptr(tw), lds, false, oe);
 }
 
 template <int RB, bool INV, int KN, bool REAL = false>
@@ -300,17 +404,21 @@ __global__ __launch_bounds__(C6Geo<RB>::T) __attribute__((amdgpu_waves_per_eu(C6
     double scale) {
   using G = C6Geo<RB>;
   static_assert(KN >= 1 && KN <= 8, "n <= M/2");
-  __shared__ double lds[G::M];
-  const int64_t g = xcd_remap(blockIdx.x, gridDim.x);
-  if (g >= batch) return;  // (grid = batch: never taken)
-  c6_transform<RB, INV, KN, REAL>(in, out, n, g, (int)threadIdx.x, tw, chirp, bhat, scale, lds);
+  __shared__ double lds[G::TPW * G::M];
+  const int t = (int)threadIdx.x;
+  const int s = G::TPW == 1 ? 0 : t / G::NA, tt = t - s * G::NA;
+  const int64_t g = xcd_remap(blockIdx.x, gridDim.x) * G::TPW + s;
+  if constexpr (G::TPW == 1) {
+    if (g >= batch) return;  // (grid = batch: never taken)
+  }
+  const bool ok = s < G::TPW && g < batch;  // (TPW > 1: every thread reaches the barriers)
+  c6_transform<RB, INV, KN, REAL>(in, out, n, g, ok, t, s, tt, tw, chirp, bhat, scale, lds);
 }
 
 template <int RB>
 hipError_t launch_c6(bool inv, int load, const void *in, cd *out, int64_t n, int64_t batch,
-                            const cd *tw, const cd *chirp, const cd *bhat, double scale,
-                            hipStream_t s) {
-  const dim3 grid((unsigned)batch), block(C6Geo<RB>::T);
+                     const cd *tw, const cd *chirp, const cd *bhat, double scale, hipStream_t s) {
+  const dim3 grid((unsigned)((batch + C6Geo<RB>::TPW - 1) / C6Geo<RB>::TPW)), block(C6Geo<RB>::T);
   if (load == LOAD_REAL)
     hipLaunchKernelGGL((chirpz6k_kernel<RB, false, 8, true>), grid, block, 0, s, in, out, n, batch,
                        tw, chirp, bhat, scale);
@@ -322,7 +430,6 @@ hipError_t launch_c6(bool inv, int load, const void *in, cd *out, int64_t n, int
                        chirp, bhat, scale);
   return hipGetLastError();
 }
-
 
 // explicit instantiations (chirpz6k*.hip) and their declarations
 #define GDSP_C6_LAUNCH(PRE, RB)                                                                 \

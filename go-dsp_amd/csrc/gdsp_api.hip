@@ -339,7 +339,7 @@ struct gdsp_plan {
   // convolutions of M = 16384, each giving kpart outputs; bhat holds parts * M
   int parts = 1;
   // fused chirp-z on M = 16 RB 16 (chirpz6k.hip: the smallest such M >= 2n - 1,
-  // 1025 <= n <= 4096, where bluestein.go:70 pads to NextPowerOf2(2n - 1));
+  // 129 <= n <= 3200, where bluestein.go:70 pads to NextPowerOf2(2n - 1));
   // tw6k: its pass twiddle bases
   bool c6k = false;
   cd *tw6k = nullptr;
@@ -1242,9 +1242,9 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz, int skip) {
   }
   bool c6k_ok = !(plan_flags() & GDSP_ALGO_CHIRPZ_POW2);
   if (p->kind == KIND_BLUESTEIN && p->parts == 1 && gdsp::chirpz6k_m(n) && c6k_ok) {
-    // 1025 <= n <= 4096: bluestein.go:70 pads the convolution to
+    // 129 <= n <= 3200: bluestein.go:70 pads the convolution to
     // NextPowerOf2(2n - 1); the smallest M = 16 * RB * 16 >= 2n - 1 of the
-    // compiled RB gives the same linear convolution (and DFT) on up to 44 %
+    // kept RB gives the same linear convolution (and DFT) on up to 44 %
     // fewer points (chirpz6k.hip). GDSP_ALGO_CHIRPZ_POW2 keeps the power of 2.
     p->m = gdsp::chirpz6k_m(n);
     p->log2m = 0;

@@ -128,8 +128,8 @@ hipError_t launch_bluestein(int log2m, bool inv, const cd *in, cd *out, int64_t 
                             int64_t batch, const cd *twm, const cd *chirp, const cd *bhat,
                             double scale, hipStream_t s);
 // fused chirp-z on M = 16 * RB * 16 (chirpz6k.hip): the smallest such M >=
-// 2n - 1 of the compiled pass-B radices RB, n >= 1025 (chirpz6k_m; 0
-// otherwise). tw = W_{16 RB}^k (k < 16) then W_M^k (k < M/16), bhat = FFT_M(b)/M; load LOAD_REAL: float64
+// 2n - 1 of the kept pass-B radices RB, n >= 129, where it is not above the
+// power of 2 (chirpz6k_m; 0 otherwise). tw = W_{16 RB}^k (k < 16) then W_M^k (k < M/16), bhat = FFT_M(b)/M; load LOAD_REAL: float64
 // rows (forward only)
 int chirpz6k_m(int64_t n);
 hipError_t launch_chirpz6k(int64_t m, bool inv, int load, const void *in, cd *out, int64_t n,

@@ -623,21 +623,24 @@ def test_chirpz_plan_vs_oracle(gdsp, oracle, n):
 
 
 # The fused chirp-z on M = 16 * RB * 16 (chirpz6k.hpp): the smallest such M
-# >= 2n - 1 over the compiled pass-B radices (chirpz6k.hip kC6RB), 1025 <= n
-# <= 3200, where bluestein.go:70 pads to NextPowerOf2(2n - 1) (and keeps it
-# above 3200). Per RB the first and last
+# >= 2n - 1 over the kept pass-B radices (chirpz6k.hip kC6RB), 129 <= n <=
+# 3200 (RB <= 6: several transforms per workgroup), where bluestein.go:70 pads
+# to NextPowerOf2(2n - 1) (and keeps it outside that range or where smaller). Per RB the first and last
 # prime of its range, the ranges' ends, and lengths that are smooth (3072 =
 # 2^10 * 3, 1500, 1536: the mixed-radix kernel by default, chirp-z only when
 # forced)
-C6_RB = [9, 10, 12, 13, 14, 15, 16, 18, 20, 21, 24, 25]
-C6K = [1025, 1031, 1151, 1153, 1279, 1283, 1399, 1409, 1531, 1543, 1663, 1667, 1789, 1801,
+C6_RB = [3, 4, 5, 6, 9, 10, 12, 13, 14, 15, 16, 18, 20, 21, 24, 25]
+C6K = [129, 131, 200, 251, 257, 383, 389, 509, 521, 631, 641, 761, 769, 887, 907, 1021, 1024,
+       1025, 1031, 1151, 1153, 1279, 1283, 1399, 1409, 1531, 1543, 1663, 1667, 1789, 1801,
        1913, 1931, 2039, 2049, 2053, 2297, 2307, 2309, 2557, 2579, 2687, 2689, 2729, 2803, 2819,
        3000, 3001, 3067, 3071, 3072, 3073, 3079, 3191, 3203, 3323, 3329, 3583, 3593, 3833,
        3847, 4093, 4096, 1500, 1536, 2062]
 
 
-def c6_m(n):  # (above 256 * 25 / 2: the power of 2)
-    return next((256 * rb for rb in C6_RB if 256 * rb >= 2 * n - 1), 1 << (2 * n - 2).bit_length())
+def c6_m(n):  # (the power of 2 below 129, above 256 * 25 / 2 and where it is smaller)
+    pow2 = 1 << (2 * n - 2).bit_length()
+    m = pow2 if n < 129 else next((256 * rb for rb in C6_RB if 256 * rb >= 2 * n - 1), pow2)
+    return min(m, pow2)
 
 
 @pytest.mark.parametrize("n", C6K)
@@ -671,13 +674,17 @@ def test_chirpz6k_vs_oracle(gdsp, oracle, n):
     assert row_nrel(y8, ref) < TOL
 
 
-def test_chirpz6k_large_batch_properties(gdsp):
-    """A full-occupancy grid (65 536 rows of n = 3000, the BASELINE shape):
-    linearity and the forward/inverse round trip on every row, and eight rows
-    against a float64 direct DFT (numpy)."""
+@pytest.mark.parametrize("n,batch", [(3000, 65536), (1151, 65536), (2297, 32768), (2687, 32768),
+                                     (3191, 32768), (311, 65537), (523, 65535), (700, 65533)])
+def test_chirpz6k_large_batch_properties(gdsp, n, batch):
+    """A full-occupancy grid (65 536 rows of n = 3000, the BASELINE shape; the
+    pass-B radices 9, 18, 21 and 25 — the last one held to 128 VGPRs with 8
+    spilled — and 3, 5, 6, several transforms per workgroup with a partial
+    last one, at 2^24-2^27 samples): linearity and the forward/inverse round
+    trip on every row, and eight rows against a float64 direct DFT (numpy)."""
     import torch
     D = __import__("importlib").import_module("go-dsp_amd.device")
-    n, batch = 3000, 65536
+    assert D.plan(n, chirpz=True).m == c6_m(n)
     g = torch.Generator(device="cuda").manual_seed(5)
     x = torch.complex(torch.rand(batch, n, dtype=torch.float64, device="cuda", generator=g) - 0.5,
                       torch.rand(batch, n, dtype=torch.float64, device="cuda", generator=g) - 0.5)
@@ -688,7 +695,7 @@ def test_chirpz6k_large_batch_properties(gdsp):
     y2 = D.fft_batch(2.0 * x[:64] - 1j * x[64:128], chirpz=True)
     lin = ((y2 - (2.0 * y[:64] - 1j * y[64:128])).abs().max() / y[:128].abs().max()).item()
     assert lin < 1e-13, lin
-    rows = [0, 1, 777, 4096, 30000, 65534, 65535, 12345]
+    rows = [0, 1, 777, 4096, 30000 % batch, batch - 2, batch - 1, 12345]
     xs = x[rows].cpu().numpy()
     ref = np.fft.fft(xs, axis=1)
     assert row_nrel(y[rows].cpu().numpy(), ref) < TOL
