@@ -942,9 +942,11 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz = false, int skip =
 int rader_race(int dev, int64_t n, gdsp_plan *p) {
   if (plan_flags() & GDSP_ALGO_NO_RACE) return GDSP_OK;
   gdsp_plan *alt = new gdsp_plan();
-  int st = build_plan(dev, n, alt, false, SKIP_RADER | SKIP_PFA);
+  // (no alternative to race: Rader's plan stands)
+  const bool have_alt = build_plan(dev, n, alt, false, SKIP_RADER | SKIP_PFA) == GDSP_OK;
   bool rader_wins = true;
-  if (st == GDSP_OK) {
+  int st = GDSP_OK;
+  if (have_alt) {
     Runner rader = [&](const cd *in, cd *out, int64_t batch, hipStream_t s) -> int {
       return exec_plan(p, in, out, batch, false, gdsp::LOAD_COMPLEX, s);
     };
@@ -1004,9 +1006,11 @@ int pfa_rader_try(int dev, int64_t n, gdsp_plan *p, bool *built) {
       return GDSP_OK;
     };
     gdsp_plan *alt = new gdsp_plan();
-    int st = build_plan(dev, n, alt, false, SKIP_PFA);
+    // (no alternative to race: the kind-8 plan stands)
+    const bool have_alt = build_plan(dev, n, alt, false, SKIP_PFA) == GDSP_OK;
     bool pfa_wins = true;
-    if (st == GDSP_OK) {
+    int st = GDSP_OK;
+    if (have_alt) {
       Runner other = [&](const cd *in, cd *out, int64_t batch, hipStream_t s) -> int {
         return exec_plan(alt, in, out, batch, false, gdsp::LOAD_COMPLEX, s);
       };
@@ -1036,7 +1040,7 @@ int pfa_rader_try(int dev, int64_t n, gdsp_plan *p, bool *built) {
 
 // The fused chirp-z on a smooth convolution length L >= 2n - 1
 // (bluestein_fixed_kernel), tried on a complete fused chirp-z plan p on M
-// (a power of 2, or the M = 6144 / 3072 kernel): L where the lane-cost
+// (a power of 2, or the M = 16 RB 16 kernel): L where the lane-cost
 // model puts it below 0.85 of M's kernel (blufix_length: n just above a
 // power of 2 — 4097 <= n <= 6144 on L <= 12288 instead of 16384, ...),
 // built with its own tables (b on L, bhat = FFT_L(b) / L by the engine), and

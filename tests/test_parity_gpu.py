@@ -630,7 +630,8 @@ def test_chirpz_plan_vs_oracle(gdsp, oracle, n):
 # 2^10 * 3, 1500, 1536: the mixed-radix kernel by default, chirp-z only when
 # forced)
 C6_RB = [3, 4, 5, 6, 9, 10, 12, 13, 14, 15, 16, 18, 20, 21, 24, 25]
-C6K = [129, 131, 200, 251, 257, 383, 389, 509, 521, 631, 641, 761, 769, 887, 907, 1021, 1024,
+C6K = [129, 131, 200, 251, 257, 383, 389, 509, 521, 523, 631, 641, 709, 761, 769, 887, 907, 1021,
+       1024,
        1025, 1031, 1151, 1153, 1279, 1283, 1399, 1409, 1531, 1543, 1663, 1667, 1789, 1801,
        1913, 1931, 2039, 2049, 2053, 2297, 2307, 2309, 2557, 2579, 2687, 2689, 2729, 2803, 2819,
        3000, 3001, 3067, 3071, 3072, 3073, 3079, 3191, 3203, 3323, 3329, 3583, 3593, 3833,
