@@ -50,6 +50,9 @@ GDSP_C6_LAUNCH(extern, 18)
 GDSP_C6_LAUNCH(extern, 20)
 GDSP_C6_LAUNCH(extern, 21)
 GDSP_C6_LAUNCH(extern, 25)
+GDSP_C4_LAUNCH(extern, 6, 6)
+GDSP_C4_LAUNCH(extern, 8, 5)
+GDSP_C4_LAUNCH(extern, 8, 6)
 
 // The pass-B radices, ascending: a length takes the first M = 256 RB >=
 // 2n - 1 (n >= 129) unless the power of 2 is smaller (0 = none: the
@@ -62,13 +65,53 @@ GDSP_C6_LAUNCH(extern, 25)
 // 7-8-wave workgroups to one per CU; 26 at 128 VGPRs spills 40 and runs
 // 0.90x), where M = 6144 or the power of 2 stays.
 static const int kC6RB[] = {3, 4, 5, 6, 9, 10, 12, 13, 14, 15, 16, 18, 20, 21, 24, 25};
+// four-pass entries (chirpz4_kernel): M = 256 R1 R2, ascending. Measured
+// against the previous choice (the power of 2, or the smooth-L chirp-z where
+// it won its race) on the first and last prime of each range, forced chirp-z
+// plans, 2^27 samples (profiles/r06/chirpz_rb_sweep.jsonl, session r06s4):
+// kept (6, 6) 1.09-1.10x (1.01x where the smooth-L chirp-z won its race on
+// the same M), (8, 5) 1.13-1.14x, (8, 6) 1.07-1.12x over 5121 ... 6144
+// (session r06t); not kept (9, 3), (7, 4), (6, 5), (8, 4) (0.63-0.96x
+// against the M = 8192 kernel), (7, 6) 1.01-1.02x, (9, 5) 0.96x, (9, 6)
+// 0.88x, (8, 7) 0.97x, (10, 6) 0.86x, (9, 7) 0.89x, (8, 8) 0.97-1.02x
+// against the M = 16384 kernel: one 9-16-wave workgroup per CU and a third
+// exchange cost about what the smaller M saves.
+struct C4Entry {
+  int r1, r2;
+};
+static const C4Entry kC4[] = {{6, 6}, {8, 5}, {8, 6}};
 
 int chirpz6k_m(int64_t n) {
   if (n < 129) return 0;
   int64_t p2 = 1;
   while (p2 < 2 * n - 1) p2 <<= 1;
+  int64_t m = 0;
   for (int rb : kC6RB)
-    if (256 * (int64_t)rb >= 2 * n - 1) return 256 * rb <= p2 ? 256 * rb : 0;
+    if (256 * (int64_t)rb >= 2 * n - 1) {
+      m = 256 * rb;
+      break;
+    }
+  for (const C4Entry &e : kC4) {
+    const int64_t m4 = 256 * (int64_t)e.r1 * e.r2;
+    if (m4 >= 2 * n - 1) {
+      if (!m || m4 < m) m = m4;
+      break;
+    }
+  }
+  return m && m <= p2 ? (int)m : 0;
+}
+
+int chirpz6k_radices(int64_t m, int *rad) {
+  for (int rb : kC6RB)
+    if (256 * (int64_t)rb == m) {
+      rad[0] = 16, rad[1] = rb, rad[2] = 16;
+      return 3;
+    }
+  for (const C4Entry &e : kC4)
+    if (256 * (int64_t)e.r1 * e.r2 == m) {
+      rad[0] = 16, rad[1] = e.r1, rad[2] = e.r2, rad[3] = 16;
+      return 4;
+    }
   return 0;
 }
 
@@ -78,6 +121,16 @@ hipError_t launch_chirpz6k(int64_t m, bool inv, int load, const void *in, cd *ou
   if (chirpz6k_m(n) != m || batch < 0 || batch > 0x7fffffff || (inv && load == LOAD_REAL))
     return hipErrorInvalidValue;
   if (batch == 0) return hipSuccess;
+  int rad[4];
+  if (chirpz6k_radices(m, rad) == 4) {
+    switch (rad[1] * 16 + rad[2]) {
+#define C4_CASE(R1, R2) \
+  case R1 * 16 + R2: return launch_c4<R1, R2>(inv, load, in, out, n, batch, tw, chirp, bhat, scale, s);
+      C4_CASE(6, 6) C4_CASE(8, 5) C4_CASE(8, 6)
+#undef C4_CASE
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (m / 256) {
 #define C6_CASE(RB) \
   case RB: return launch_c6<RB>(inv, load, in, out, n, batch, tw, chirp, bhat, scale, s);

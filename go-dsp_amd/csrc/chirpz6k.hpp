@@ -120,9 +120,8 @@ __device__ __forceinline__ void c6_twiddle(cd (&v)[R], cd w) {
 // postmultiply and store (issue: the loads, apply: the arithmetic). Issued
 // before the pass-C twiddles or the last exchange's reads instead, the loads
 // push the kernel past 128 VGPRs into spills: 2.43 against 2.37 ms.
-template <int RB>
-struct C6Bhat {
-  using G = C6Geo<RB>;
+template <class G>
+struct C6BhatG {
   rsrc_t rb;
   uint32_t off;
   cd f[16];
@@ -136,9 +135,8 @@ struct C6Bhat {
     for (int r = 0; r < 16; ++r) v[r] = conjg(cmul(v[r], f[r]));
   }
 };
-template <int RB, int KN, bool INV>
-struct C6Out {
-  using G = C6Geo<RB>;
+template <class G, int KN, bool INV>
+struct C6OutG {
   rsrc_t rch, rout;
   uint32_t off;
   double scale;
@@ -158,6 +156,10 @@ struct C6Out {
     }
   }
 };
+template <int RB>
+using C6Bhat = C6BhatG<C6Geo<RB>>;
+template <int RB, int KN, bool INV>
+using C6Out = C6OutG<C6Geo<RB>, KN, INV>;
 
 // One FFT_M of the thread's registers v[r] = element t + NA r, in place
 // (natural order in and out), then epi. ZIN: inputs r >= ZIN are zero (pass
@@ -430,6 +432,200 @@ hipError_t launch_c6(bool inv, int load, const void *in, cd *out, int64_t n, int
                        chirp, bhat, scale);
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// The same fused chirp-z with pass B split in two: M = 16 * R1 * R2 * 16
+// (chirpz4_kernel, round 6), for the convolution lengths pass B cannot hold in
+// registers (R1 R2 = 36, 40, 48 as kept, chirpz6k.hip kC4: M = 9216 ...
+// 12288, 4097 <= n <= 6144, where the reference pads to 16384). One workgroup per transform of T = M /
+// 16 threads:
+//   pass A   R = 16, NS = 1:          DFT_16 of t + NA r (pruned input), as c6
+//   pass B1  R = R1, NS = 16:         butterflies j = t + T q (q < J1)
+//   pass B2  R = R2, NS = 16 R1:      butterflies j = t + T q (q < J2)
+//   pass C   R = 16, NS = 16 R1 R2:   outputs t + NA r (natural order)
+// then, as c6, v = conj(A * bhat) in registers, FFT 2 on the same passes, X =
+// conj(v) * conj(w) for r < KN. Exchanges as real then imaginary halves
+// through one M-double buffer: A -> B1 through c6's swizzle (slot e ^ ((e >>
+// 4) & 15)), B1 -> B2 and B2 -> C plain. Twiddle bases (make_mixed_desc of
+// {16, R1, R2, 16}): W_{16 R1}^k (16), W_{16 R1 R2}^k (16 R1), W_M^k (NA);
+// powers by c6_twiddle's recurrence.
+template <int R1_, int R2_>
+struct C4Geo {
+  static constexpr int R1 = R1_, R2 = R2_;
+  static constexpr int M = 256 * R1 * R2;
+  static constexpr int NA = M / 16;  // pass A / C butterflies = threads
+  static constexpr int T = NA;
+  static constexpr int TPW = 1;
+  static constexpr int NB1 = M / R1, NB2 = M / R2;  // pass B1 / B2 butterflies
+  static constexpr int J1 = (NB1 + T - 1) / T, J2 = (NB2 + T - 1) / T;
+  static_assert(T <= 1024, "one workgroup per transform");
+};
+
+__device__ __forceinline__ int c6_swz(int e) { return e ^ ((e >> 4) & 15); }
+
+// one middle pass (radix R, stride NS, twiddle bases twb) between two
+// exchanges: read its J butterflies' inputs from the buffer (SWZ: written by
+// pass A), compute into u
+template <int M, int T, int R, int NS, int J, bool SWZ>
+__device__ __forceinline__ void c4_read(cd (&u)[J][R], int t, const double *lds, int part) {
+  constexpr int NB = M / R;
+#pragma unroll
+  for (int q = 0; q < J; ++q) {
+    const int j = t + T * q;
+    if (NB % T == 0 || j < NB) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int e = j + NB * r;
+        const double x = lds[SWZ ? c6_swz(e) : e];
+        if (part) u[q][r].y = x;
+        else u[q][r].x = x;
+      }
+    }
+  }
+}
+template <int M, int T, int R, int NS, int J>
+__device__ __forceinline__ void c4_compute(cd (&u)[J][R], int t, const cd *__restrict__ twb) {
+  constexpr int NB = M / R;
+#pragma unroll
+  for (int q = 0; q < J; ++q) {
+    const int j = t + T * q;
+    if (NB % T == 0 || j < NB) {
+      c6_twiddle<R>(u[q], twb[j % NS]);
+      dft_m<R>(u[q]);
+    }
+  }
+}
+template <int M, int T, int R, int NS, int J>
+__device__ __forceinline__ void c4_write(const cd (&u)[J][R], int t, double *lds, int part) {
+  constexpr int NB = M / R;
+#pragma unroll
+  for (int q = 0; q < J; ++q) {
+    const int j = t + T * q;
+    if (NB % T == 0 || j < NB) {
+      const int k = j % NS, o = (j - k) * R + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) lds[o + NS * r] = part ? u[q][r].y : u[q][r].x;
+    }
+  }
+}
+
+template <class G, int ZIN, class EPI>
+__device__ __forceinline__ void c4_fft(cd (&v)[16], int t, const cd *__restrict__ tw, double *lds,
+                                       bool first, EPI &epi) {
+  constexpr int M = G::M, T = G::T, NA = G::NA, R1 = G::R1, R2 = G::R2;
+  // pass A
+  if constexpr (ZIN > 0 && ZIN <= 8) dft_half_in<16, ZIN>(v);
+  else Dft<16>::run(v);
+  // exchange A -> B1 (write 16 t + r, swizzled)
+  const int wa = 16 * t, ma = t & 15;
+  cd u1[G::J1][R1];
+  if (!first) __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) lds[wa + (r ^ ma)] = v[r].x;
+  __syncthreads();
+  c4_read<M, T, R1, 16, G::J1, true>(u1, t, lds, 0);
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) lds[wa + (r ^ ma)] = v[r].y;
+  __syncthreads();
+  c4_read<M, T, R1, 16, G::J1, true>(u1, t, lds, 1);
+  // pass B1
+  c4_compute<M, T, R1, 16, G::J1>(u1, t, tw);
+  // exchange B1 -> B2
+  cd u2[G::J2][R2];
+  __syncthreads();
+  c4_write<M, T, R1, 16, G::J1>(u1, t, lds, 0);
+  __syncthreads();
+  c4_read<M, T, R2, 16 * R1, G::J2, false>(u2, t, lds, 0);
+  __syncthreads();
+  c4_write<M, T, R1, 16, G::J1>(u1, t, lds, 1);
+  __syncthreads();
+  c4_read<M, T, R2, 16 * R1, G::J2, false>(u2, t, lds, 1);
+  // pass B2
+  c4_compute<M, T, R2, 16 * R1, G::J2>(u2, t, tw + 16);
+  // exchange B2 -> C (read t + NA r)
+  __syncthreads();
+  c4_write<M, T, R2, 16 * R1, G::J2>(u2, t, lds, 0);
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r].x = lds[t + NA * r];
+  __syncthreads();
+  c4_write<M, T, R2, 16 * R1, G::J2>(u2, t, lds, 1);
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r].y = lds[t + NA * r];
+  // pass C: twiddle W_M^(t r), DFT_16, the epilogue
+  c6_twiddle<16>(v, tw[16 + 16 * R1 + t]);
+  Dft<16>::run(v);
+  epi.issue();
+  epi.apply(v);
+}
+
+template <int R1, int R2, bool INV, int KN, bool REAL = false>
+__global__ __launch_bounds__((C4Geo<R1, R2>::T)) void chirpz4_kernel(
+    const void *__restrict__ in, cd *__restrict__ out, int64_t n, int64_t batch,
+    const cd *__restrict__ tw, const cd *__restrict__ chirp, const cd *__restrict__ bhat,
+    double scale) {
+  using G = C4Geo<R1, R2>;
+  static_assert(KN >= 1 && KN <= 8, "n <= M/2");
+  __shared__ double lds[G::M];
+  const int t = (int)threadIdx.x;
+  const int64_t g = xcd_remap(blockIdx.x, gridDim.x);
+  if (g >= batch) return;  // (grid = batch: never taken)
+  const uint32_t off = (uint32_t)t * 16u;
+  const int64_t rowb = n * 16;
+  const int64_t inb = REAL ? n * 8 : rowb;
+  cd v[16];
+  {
+    const rsrc_t rin = make_rsrc(static_cast<const char *>(in) + g * inb, inb);
+    const rsrc_t rch = make_rsrc(chirp, rowb);
+    cd xv[KN], cv[KN];
+#pragma unroll
+    for (int r = 0; r < KN; ++r) {
+      if constexpr (REAL)
+        xv[r] = {buf_ld1(rin, (uint32_t)t * 8u + (uint32_t)(r * G::NA * 8)), 0.0};
+      else
+        xv[r] = buf_ld(rin, off + (uint32_t)(r * G::NA * 16));
+      cv[r] = buf_ld(rch, off + (uint32_t)(r * G::NA * 16));
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (r < KN) {
+        cd x = xv[r];
+        if constexpr (INV) x.y = -x.y;
+        v[r] = cmul(x, cv[r]);
+      } else {
+        v[r] = {0.0, 0.0};
+      }
+    }
+  }
+  C6BhatG<G> be{make_rsrc(bhat, (int64_t)G::M * 16), off, {}};
+  c4_fft<G, KN, C6BhatG<G>>(v, t, tw, lds, true, be);
+  const int t2 = opaque_int(t);
+  C6OutG<G, KN, INV> oe{make_rsrc(opaque_ptr(chirp), rowb), make_rsrc(out + g * n, rowb),
+                        (uint32_t)t2 * 16u, scale, true, {}};
+  c4_fft<G, 0, C6OutG<G, KN, INV>>(v, t2, opaque_ptr(tw), lds, false, oe);
+}
+
+template <int R1, int R2>
+hipError_t launch_c4(bool inv, int load, const void *in, cd *out, int64_t n, int64_t batch,
+                     const cd *tw, const cd *chirp, const cd *bhat, double scale, hipStream_t s) {
+  const dim3 grid((unsigned)batch), block(C4Geo<R1, R2>::T);
+  if (load == LOAD_REAL)
+    hipLaunchKernelGGL((chirpz4_kernel<R1, R2, false, 8, true>), grid, block, 0, s, in, out, n,
+                       batch, tw, chirp, bhat, scale);
+  else if (inv)
+    hipLaunchKernelGGL((chirpz4_kernel<R1, R2, true, 8>), grid, block, 0, s, in, out, n, batch,
+                       tw, chirp, bhat, scale);
+  else
+    hipLaunchKernelGGL((chirpz4_kernel<R1, R2, false, 8>), grid, block, 0, s, in, out, n, batch,
+                       tw, chirp, bhat, scale);
+  return hipGetLastError();
+}
+#define GDSP_C4_LAUNCH(PRE, R1, R2)                                                             \
+  PRE template hipError_t launch_c4<R1, R2>(bool, int, const void *, cd *, int64_t, int64_t,    \
+                                            const cd *, const cd *, const cd *, double,         \
+                                            hipStream_t);
 
 // explicit instantiations (chirpz6k*.hip) and their declarations
 #define GDSP_C6_LAUNCH(PRE, RB)                                                                 \

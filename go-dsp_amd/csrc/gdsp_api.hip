@@ -432,8 +432,10 @@ bool mixed_radices(int64_t n, std::vector<int> &rad, bool specs = true) {
 
 // Descriptor + per-pass twiddle bases W_{Ns*R}^k (k < Ns; the kernels
 // raise them to the powers r = 1..R-1 in registers) of one radix list.
+// geometry: check the thread count of the mixed-radix kernels' geometry (the
+// fused chirp-z kernels, which only take the twiddle bases, have their own)
 int make_mixed_desc(int dev, int64_t n, const std::vector<int> &rad, gdsp::MixedDesc &d,
-                    cd **tw) {
+                    cd **tw, bool geometry = true) {
   d.n = (int)n;
   d.npass = (int)rad.size();
   d.codes = 0;
@@ -448,7 +450,7 @@ int make_mixed_desc(int dev, int64_t n, const std::vector<int> &rad, gdsp::Mixed
   if (t1 > 64) t1 = (need + 63) / 64 * 64;
   // (the runtime-radix kernels check t1 <= 512 themselves; a compiled or
   // runtime-compiled specialisation may use up to 1024 threads per transform)
-  if (t1 > 1024) return fail(GDSP_ERR_UNSUPPORTED, "mixed-radix geometry");
+  if (geometry && t1 > 1024) return fail(GDSP_ERR_UNSUPPORTED, "mixed-radix geometry");
   d.t1 = t1;
   d.tpw = std::max(1, std::min(256 / t1, gdsp::kMixedMax / (int)n));
   std::vector<cd> h;
@@ -1053,7 +1055,8 @@ int blufix_try(int dev, int64_t n, gdsp_plan *p, const std::vector<cd> &w) {
     return GDSP_OK;
   std::vector<int> now;
   if (p->c6k) {
-    now = {16, (int)(p->m / 256), 16};
+    int rad6[4];
+    now.assign(rad6, rad6 + gdsp::chirpz6k_radices(p->m, rad6));
   } else {
     int a = p->log2m;
     for (; a >= 4; a -= 4) now.push_back(16);
@@ -1254,7 +1257,9 @@ int build_plan(int dev, int64_t n, gdsp_plan *p, bool chirpz, int skip) {
     p->log2m = 0;
     p->c6k = true;
     gdsp::MixedDesc d6{};
-    STCHK(make_mixed_desc(dev, p->m, {16, (int)(p->m / 256), 16}, d6, &p->tw6k));
+    int rad6[4];
+    const int np6 = gdsp::chirpz6k_radices(p->m, rad6);
+    STCHK(make_mixed_desc(dev, p->m, std::vector<int>(rad6, rad6 + np6), d6, &p->tw6k, false));
   }
   if (!p->mplan) STCHK(get_plan_locked(dev, p->m, &p->mplan));
   std::vector<cd> w((size_t)n), chirp((size_t)n),

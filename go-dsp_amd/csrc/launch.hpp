@@ -132,6 +132,9 @@ hipError_t launch_bluestein(int log2m, bool inv, const cd *in, cd *out, int64_t 
 // power of 2 (chirpz6k_m; 0 otherwise). tw = W_{16 RB}^k (k < 16) then W_M^k (k < M/16), bhat = FFT_M(b)/M; load LOAD_REAL: float64
 // rows (forward only)
 int chirpz6k_m(int64_t n);
+// the pass radices of the fused chirp-z on m: {16, RB, 16} or {16, R1, R2, 16}
+// (chirpz4_kernel); returns their count (0: not a chirpz6k length)
+int chirpz6k_radices(int64_t m, int *rad);
 hipError_t launch_chirpz6k(int64_t m, bool inv, int load, const void *in, cd *out, int64_t n,
                            int64_t batch, const cd *tw, const cd *chirp, const cd *bhat,
                            double scale, hipStream_t s);

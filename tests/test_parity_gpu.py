@@ -635,13 +635,22 @@ C6K = [129, 131, 200, 251, 257, 383, 389, 509, 521, 523, 631, 641, 709, 761, 769
        1025, 1031, 1151, 1153, 1279, 1283, 1399, 1409, 1531, 1543, 1663, 1667, 1789, 1801,
        1913, 1931, 2039, 2049, 2053, 2297, 2307, 2309, 2557, 2579, 2687, 2689, 2729, 2803, 2819,
        3000, 3001, 3067, 3071, 3072, 3073, 3079, 3191, 3203, 3323, 3329, 3583, 3593, 3833,
-       3847, 4093, 4096, 1500, 1536, 2062]
+       3847, 4093, 4096, 1500, 1536, 2062,
+       3449, 3457, 4099, 4603, 4621, 5119, 5147, 5351, 5381, 5749, 5779, 6143, 6151, 6911, 6917,
+       7159, 7177, 7673, 7681, 8059, 8069, 8191, 4097, 8192, 6000]
 
 
-def c6_m(n):  # (the power of 2 below 129, above 256 * 25 / 2 and where it is smaller)
+# the four-pass kernel's (R1, R2) (chirpz4_kernel, M = 256 R1 R2; chirpz6k.hip kC4)
+C4_RR = [(6, 6), (8, 5), (8, 6)]
+
+
+def c6_m(n):  # (the power of 2 below 129 and where it is smaller)
     pow2 = 1 << (2 * n - 2).bit_length()
-    m = pow2 if n < 129 else next((256 * rb for rb in C6_RB if 256 * rb >= 2 * n - 1), pow2)
-    return min(m, pow2)
+    if n < 129:
+        return pow2
+    cands = [next((256 * rb for rb in C6_RB if 256 * rb >= 2 * n - 1), pow2),
+             next((256 * a * b for a, b in C4_RR if 256 * a * b >= 2 * n - 1), pow2)]
+    return min(cands + [pow2])
 
 
 @pytest.mark.parametrize("n", C6K)
@@ -676,7 +685,8 @@ def test_chirpz6k_vs_oracle(gdsp, oracle, n):
 
 
 @pytest.mark.parametrize("n,batch", [(3000, 65536), (1151, 65536), (2297, 32768), (2687, 32768),
-                                     (3191, 32768), (311, 65537), (523, 65535), (700, 65533)])
+                                     (3191, 32768), (311, 65537), (523, 65535), (700, 65533),
+                                     (4603, 16384), (6143, 16384), (8191, 8192)])
 def test_chirpz6k_large_batch_properties(gdsp, n, batch):
     """A full-occupancy grid (65 536 rows of n = 3000, the BASELINE shape; the
     pass-B radices 9, 18, 21 and 25 — the last one held to 128 VGPRs with 8
@@ -692,11 +702,12 @@ def test_chirpz6k_large_batch_properties(gdsp, n, batch):
     y = D.fft_batch(x, chirpz=True)
     z = D.fft_batch(y, inverse=True, chirpz=True)
     err = ((z - x).abs().amax(dim=1) / x.abs().amax(dim=1)).max().item()
-    assert err < 1e-12, err
+    # (the reference's unreduced chirp angle, bluestein.go:53: ~1e-12 above n = 4096)
+    assert err < (1e-12 if n <= 3200 else 1e-11), err
     y2 = D.fft_batch(2.0 * x[:64] - 1j * x[64:128], chirpz=True)
     lin = ((y2 - (2.0 * y[:64] - 1j * y[64:128])).abs().max() / y[:128].abs().max()).item()
     assert lin < 1e-13, lin
-    rows = [0, 1, 777, 4096, 30000 % batch, batch - 2, batch - 1, 12345]
+    rows = [r % batch for r in (0, 1, 777, 4096, 30000, batch - 2, batch - 1, 12345)]
     xs = x[rows].cpu().numpy()
     ref = np.fft.fft(xs, axis=1)
     assert row_nrel(y[rows].cpu().numpy(), ref) < TOL
@@ -1505,7 +1516,10 @@ def _pfa_large_batch(D, n, batch):
 # the fused chirp-z (plan kind 3) with L >= 2n - 1 smooth instead of
 # bluestein.go:70's NextPowerOf2(2n - 1) where the lane-cost model expects it
 # cheaper: the same linear convolution, hence the same DFT
-BLUFIX_CASES = [4099, 4402, 4981, 5402, 6011, 6143]
+# (lengths where the lane-cost model has a smooth L below the fused kernel's M
+# of round 6: 1031 on 2160 against 2304, 5209 / 5402 / 5519 on 10800 / 11520
+# against 12288)
+BLUFIX_CASES = [1031, 5209, 5402, 5519]
 
 
 @pytest.mark.parametrize("n", BLUFIX_CASES)
