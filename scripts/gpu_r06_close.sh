@@ -7,3 +7,7 @@ python3 $R/tools/source_stamp.py > $R/gpurun_out/source_stamp.json || exit 1
 GDSP_JIT_CACHE=$R/gpurun_out/jitcache bash $R/scripts/gpu_sq.sh $W || exit 1
 bash $R/scripts/gpu_r06_prof.sh stats || exit 1
 bash $R/scripts/gpu_r06_prof.sh pmc "$W" || exit 1
+# and the random sample of non-smooth lengths at the same sources
+mkdir -p $R/gpurun_out/r06p
+cd $R && GDSP_JIT_CACHE=$R/gpurun_out/jitcache timeout -k 10 500 python3 scripts/sweep_nonsmooth.py --no-chirpz --samples 67108864 $(cat scripts/nonsmooth_sample.txt) > gpurun_out/r06p/sample.jsonl 2> gpurun_out/r06p/sweep.err || exit 1
+echo "sample sweep rc=0"
