@@ -233,3 +233,63 @@ def test_multi_stats_readable_without_gpu(gdsp):
     assert all(v >= 0 for v in s.values())
     if gdsp.device_count() == 0:
         assert all(v == 0 for v in s.values())
+
+
+def _lib_sym(name, restype, argtypes):
+    lib = ctypes.CDLL(os.path.join(REPO, "go-dsp_amd", "lib", "libgdspfft.so"))
+    f = lib[name]
+    f.restype, f.argtypes = restype, argtypes
+    return f
+
+
+def test_chirpz_convolution_length_rule():
+    """The fused chirp-z's convolution length (gdsp::chirpz6k_m, host logic, no
+    GPU): for every 1 <= n <= 16384, the smallest kept M = 256 RB (three-pass)
+    or 256 R1 R2 (four-pass) >= 2n - 1, not above NextPowerOf2(2n - 1)
+    (bluestein.go:70), from n = 129 on; else 0 (the power-of-2 kernels). The
+    radices chirpz6k_radices reports multiply to M."""
+    m_of = _lib_sym("_ZN4gdsp10chirpz6k_mEl", ctypes.c_int, [ctypes.c_int64])
+    rad_of = _lib_sym("_ZN4gdsp16chirpz6k_radicesElPi", ctypes.c_int,
+                      [ctypes.c_int64, ctypes.POINTER(ctypes.c_int)])
+    rb3 = [3, 4, 5, 6, 9, 10, 12, 13, 14, 15, 16, 18, 20, 21, 24, 25]
+    rr4 = [(6, 6), (8, 5), (8, 6)]
+    for n in range(1, 16385):
+        p2 = 1 << (2 * n - 2).bit_length() if n > 1 else 1
+        cand = [256 * r for r in rb3 if 256 * r >= 2 * n - 1][:1] + \
+               [256 * a * b for a, b in rr4 if 256 * a * b >= 2 * n - 1][:1]
+        want = min(cand) if n >= 129 and cand and min(cand) <= p2 else 0
+        got = m_of(n)
+        assert got == want, (n, got, want)
+        if got:
+            r = (ctypes.c_int * 4)()
+            k = rad_of(got, r)
+            assert k in (3, 4) and r[0] == 16 and r[k - 1] == 16, (n, list(r[:k]))
+            assert int(np.prod(r[:k])) == got
+            assert got >= 2 * n  # n <= M/2: the kernels' KN = 8 input / output registers
+
+
+def test_smooth_l_candidates_of_the_gpu_tests():
+    """gdsp::blufix_length (the lane-cost model's smooth L, host logic): the
+    lengths test_chirpz_smooth_l_vs_oracle (-m gpu) runs have a candidate below
+    the fused kernel's M of radices <= 16, and the lengths the four-pass kernel
+    took from it (4099, 4402) have none."""
+    m_of = _lib_sym("_ZN4gdsp10chirpz6k_mEl", ctypes.c_int, [ctypes.c_int64])
+    rad_of = _lib_sym("_ZN4gdsp16chirpz6k_radicesElPi", ctypes.c_int,
+                      [ctypes.c_int64, ctypes.POINTER(ctypes.c_int)])
+    IP = ctypes.POINTER(ctypes.c_int)
+    bl = _lib_sym("_ZN4gdsp13blufix_lengthEllPKiiPiS2_", ctypes.c_int,
+                  [ctypes.c_int64, ctypes.c_int64, IP, ctypes.c_int, IP, IP])
+
+    def candidate(n):
+        m = m_of(n)
+        r = (ctypes.c_int * 4)()
+        k = rad_of(m, r)
+        rad, np_ = (ctypes.c_int * 4)(), ctypes.c_int(0)
+        L = bl(n, m, r, k, rad, ctypes.byref(np_))
+        return m, L, list(rad[:np_.value])
+
+    for n in (1031, 5209, 5402, 5519):
+        m, L, rad = candidate(n)
+        assert 2 * n - 1 <= L < m and int(np.prod(rad)) == L and max(rad) <= 16, (n, m, L, rad)
+    for n in (4099, 4402):
+        assert candidate(n)[1] == 0
