@@ -183,7 +183,7 @@ def setup(w: str, c: Ctx, weak: bool = False) -> dict:
                   5: "fft_mixed_fixed_kernel<25,15,8>",
                   7: "rader_fixed_kernel", 8: "rader_pfa_kernel"}.get(kind, str(kind))
         if kind == 3 and p.m == 6144:
-            # 2049 <= n <= 3072: the convolution on M = 6144 (chirpz6k.hip);
+            # 2817 <= n <= 3072: the convolution on M = 6144 (chirpz6k.hip);
             # bluestein.go:70 pads to 8192 (GDSP_ALGO_CHIRPZ_POW2 keeps it)
             algo = "Bluestein chirp-z (fused, M=6144=16*24*16; the reference pads to 8192)"
             kernel = "chirpz6k_kernel"

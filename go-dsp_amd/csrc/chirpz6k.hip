@@ -8,8 +8,9 @@
 //
 // bluestein.go:70 pads the circular convolution to NextPowerOf2(2n - 1)
 // because its FFT is radix 2. Any M >= 2n - 1 gives the same linear
-// convolution, hence the same DFT; 256 RB is at most 1/8 above 2n - 1 where
-// the power of 2 is up to twice it. At M = 6144 the exchange buffer (48 KiB)
+// convolution, hence the same DFT; where this kernel is taken its M is below
+// the power of 2 (at most 1.5 (2n - 1), where the power of 2 is up to twice
+// it). At M = 6144 the exchange buffer (48 KiB)
 // and a 16-point-per-thread register set let two 384-thread workgroups share
 // a CU at 128 VGPRs, where the M = 8192 kernel (bluestein_kernel<13>, 32
 // points per thread, 256 VGPRs) runs two 256-thread ones.

@@ -437,8 +437,8 @@ hipError_t launch_c6(bool inv, int load, const void *in, cd *out, int64_t n, int
 // The same fused chirp-z with pass B split in two: M = 16 * R1 * R2 * 16
 // (chirpz4_kernel, round 6), for the convolution lengths pass B cannot hold in
 // registers (R1 R2 = 36, 40, 48 as kept, chirpz6k.hip kC4: M = 9216 ...
-// 12288, 4097 <= n <= 6144, where the reference pads to 16384). One workgroup per transform of T = M /
-// 16 threads:
+// 12288, 4097 <= n <= 6144, where the reference pads to 16384). One workgroup
+// per transform of T = M / 16 threads:
 //   pass A   R = 16, NS = 1:          DFT_16 of t + NA r (pruned input), as c6
 //   pass B1  R = R1, NS = 16:         butterflies j = t + T q (q < J1)
 //   pass B2  R = R2, NS = 16 R1:      butterflies j = t + T q (q < J2)

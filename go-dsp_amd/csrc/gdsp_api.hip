@@ -770,7 +770,7 @@ bool rader_radices(int64_t N, std::vector<int> &rad) {
 // Rader's algorithm (rader_fixed_kernel, mixed_fixed.hpp) for a prime n >= 17
 // whose n - 1 has a radix list: the DFT as a cyclic convolution of length
 // n - 1 (two FFTs of n - 1 points in one kernel) instead of bluestein.go:68-94's
-// chirp-z (FFTs of NextPowerOf2(2n - 1), or the M = 6144 / 3072 kernel).
+// chirp-z (FFTs of NextPowerOf2(2n - 1), or of a smaller smooth M, chirpz6k.hip).
 // *built = false (and p untouched) where it does not apply or the kernel
 // does not compile: the plan then takes the chirp-z below.
 int rader_try(int dev, int64_t n, gdsp_plan *p, bool *built) {

@@ -332,7 +332,7 @@ bool jit_radices(int n, int *rad, int *npass) {
 // point) within 1024 threads per transform, the L of the lowest L x
 // lane_cost; taken only where that is below 0.85 of the current kernel's
 // (M x lane_cost of its list: radix-16 passes for a power of 2, 16 x RB x 16
-// for the M = 6144 / 3072 kernel).
+// or 16 x R1 x R2 x 16 for the chirpz6k.hip kernels).
 int blufix_length(int64_t n, int64_t m_now, const int *rad_now, int np_now, int *rad, int *np) {
   if (n < 2 || 2 * n - 1 > 16384 || m_now <= 2 * n - 1) return 0;
   int t_now = 0, tpw_now = 0;

@@ -79,8 +79,9 @@ enum {
   GDSP_ALGO_NO_CHIRPZ_PARTS = 2,
   /* chirp-z on the reference's M = NextPowerOf2(2n-1) (fft/bluestein.go:70)
    * instead of a smaller smooth M: the composed chirp-z, and the fused one
-   * for 129 <= n <= 3200 (by default M = 16 * RB * 16, the smallest of the
-   * kept RB >= 2n - 1 where not above the power of 2) */
+   * for 129 <= n <= 3200 and 4097 <= n <= 6144 (by default M = 16 * RB * 16
+   * or 16 * R1 * R2 * 16, the smallest kept one >= 2n - 1 where not above
+   * the power of 2) */
   GDSP_ALGO_CHIRPZ_POW2 = 4,
   /* the composed chirp-z without its fused transposes */
   GDSP_ALGO_CHIRPZ_UNFUSED = 8,

@@ -625,10 +625,11 @@ def test_chirpz_plan_vs_oracle(gdsp, oracle, n):
 # The fused chirp-z on M = 16 * RB * 16 (chirpz6k.hpp): the smallest such M
 # >= 2n - 1 over the kept pass-B radices (chirpz6k.hip kC6RB), 129 <= n <=
 # 3200 (RB <= 6: several transforms per workgroup), where bluestein.go:70 pads
-# to NextPowerOf2(2n - 1) (and keeps it outside that range or where smaller). Per RB the first and last
-# prime of its range, the ranges' ends, and lengths that are smooth (3072 =
-# 2^10 * 3, 1500, 1536: the mixed-radix kernel by default, chirp-z only when
-# forced)
+# to NextPowerOf2(2n - 1) (and keeps it outside that range or where smaller);
+# the four-pass kernel (R1, R2) for 4097 <= n <= 6144. Per entry the first
+# and last prime of its range, the ranges' ends, and lengths that are smooth
+# (3072 = 2^10 * 3, 1500, 1536: the mixed-radix kernel by default, chirp-z
+# only when forced)
 C6_RB = [3, 4, 5, 6, 9, 10, 12, 13, 14, 15, 16, 18, 20, 21, 24, 25]
 C6K = [129, 131, 200, 251, 257, 383, 389, 509, 521, 523, 631, 641, 709, 761, 769, 887, 907, 1021,
        1024,
