@@ -670,6 +670,11 @@ def test_chirpz6k_vs_oracle(gdsp, oracle, n):
         assert row_nrel(D.fft_batch(xt, chirpz=True).cpu().numpy(), ref) < TOL
         yi = D.fft_batch(xt, inverse=True, chirpz=True).cpu().numpy()
         assert row_nrel(yi, oracle.ifft_rows(x)) < TOL
+        # in place: every row is read into registers before its first store
+        xc = xt.clone()
+        D.fft_batch(xc, xc, chirpz=True)
+        torch.cuda.synchronize()
+        assert row_nrel(xc.cpu().numpy(), ref) < TOL
     # host API (default plan: chirp-z for the primes, mixed radix when smooth)
     x = rng.uniform(-1, 1, (3, n)) + 1j * rng.uniform(-1, 1, (3, n))
     assert row_nrel(gdsp.fft.FFTBatch(x), oracle.fft_rows(x)) < TOL
